@@ -1,0 +1,284 @@
+#!/usr/bin/env python3
+"""Benchmark of the device-resident server-side push aggregation.
+
+Headline workload (BASELINE.json configs[1], "cfg2"): one (channel, time)
+aggregate = 8 worker pushes x 131,072 sorted unique uint64 keys with f32
+values, 10 % of the keys shared by all pushes, U = 956,827 server keys.
+A step is one pass of the hot path (partition + aggregate kernels) over a
+batch of --batch such aggregates per GPU (default 32: 770 MB of distinct
+inputs/outputs, 3x the 256 MB Infinity Cache, so the rate is an HBM rate).
+
+Multi-GPU (one process per GPU, torchrun): the key space is range-
+partitioned with Range<uint64>::all().evenDivide(N, rank) (reference
+linear_method.cc:137-145); each rank holds the shard of every aggregate
+that its key range owns, exactly what the reference's worker-side
+sliceKeyOrderedMsg delivers (message.h:89-123), so the data path has no
+collective and per-GPU work is fixed ("scaling": "weak").  --ingress
+unsliced instead hands every rank whole pushes and re-homes the pieces with
+an RCCL all-to-all before merging (SURVEY 8e mode B).
+
+Prints ONE JSON line on rank 0.
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import sys
+import time
+
+import numpy as np
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, ROOT)
+
+HBM_PEAK_GBPS = 8000.0  # MI355X_MICROARCH.md: HBM3E 8.0 TB/s spec
+METRIC = "aggregated kv-pairs/s (device-resident), N-way sparse push merge at 1/2/4/8 GPU"
+
+
+def parse():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=20)
+    ap.add_argument("--warmup", type=int, default=5)
+    ap.add_argument("--batch", type=int, default=32, help="cfg2 aggregates per GPU per step")
+    ap.add_argument("--npush", type=int, default=8)
+    ap.add_argument("--n", type=int, default=131072)
+    ap.add_argument("--overlap", type=float, default=0.1)
+    ap.add_argument("--ingress", choices=["sliced", "unsliced"], default="sliced")
+    ap.add_argument("--cpu-seconds", type=float, default=10.0)
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--profile-steps", type=int, default=0,
+                    help="only run warmup+steps (for rocprofv3); skip baselines")
+    return ap.parse_args()
+
+
+def log(msg):
+    print(f"[bench] {msg}", file=sys.stderr, flush=True)
+
+
+def main():
+    args = parse()
+    import torch
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    if args.gpus != world and world > 1:
+        log(f"--gpus {args.gpus} but WORLD_SIZE {world}; using WORLD_SIZE")
+    torch.cuda.set_device(local)
+    dist = None
+    if world > 1:
+        import torch.distributed as dist
+        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+
+    from parameter_server_amd import synth
+    from parameter_server_amd.kv_vector import MergePlan, shard_bounds
+    from parameter_server_amd._lib import PSG_F32
+
+    bounds = shard_bounds(world)
+    lo, hi = int(bounds[rank]), int(bounds[rank + 1])
+
+    # ---- synthetic inputs (each rank: its shard of `batch` aggregates) ----
+    t0 = time.time()
+    if args.ingress == "sliced" or world == 1:
+        insts = [synth.shard_instance(seed=1 + j + 1000 * rank, lo=lo, hi=hi,
+                                      npush=args.npush, n=args.n, overlap=args.overlap)
+                 for j in range(args.batch)]
+    else:
+        from parameter_server_amd import shard as S
+        insts = S.exchange_unsliced(args, rank, world, bounds, dist)
+    log(f"rank {rank}: generated {len(insts)} aggregates in {time.time() - t0:.1f}s")
+
+    dev = torch.device("cuda", local)
+
+    def to_dev(a):
+        a = np.ascontiguousarray(a)
+        return torch.from_numpy(a.view(np.int64) if a.dtype == np.uint64 else a).to(dev)
+
+    keep, jobs = [], []
+    for D, pushes in insts:
+        dD = to_dev(D)
+        pk = [to_dev(k) for k, _ in pushes]
+        pv = [[to_dev(v) for v in vs] for _, vs in pushes]
+        out = torch.empty(max(1, D.size), dtype=torch.float32, device=dev)
+        keep.append((dD, pk, pv, out))
+        jobs.append({"keys": dD.data_ptr(), "nslots": int(D.size),
+                     "push_keys": [t.data_ptr() for t in pk],
+                     "push_vals": [[t.data_ptr() for t in vs] for vs in pv],
+                     "push_n": [int(k.size) for k, _ in pushes],
+                     "out": [out.data_ptr()]})
+    plan = MergePlan(local, PSG_F32, 1, jobs)
+    stream = torch.cuda.current_stream()
+    sh = stream.cuda_stream
+
+    # correctness guard: every pushed key matched
+    plan.run(sh)
+    mt = plan.matched()
+    want = np.array([int(k.size) for _, ps in insts for k, _ in ps], np.uint64)
+    assert np.array_equal(mt, want), "unmatched keys in the bench workload"
+
+    for _ in range(args.warmup):
+        plan.run(sh)
+    torch.cuda.synchronize()
+    if dist:
+        dist.barrier()
+    torch.cuda.synchronize()
+
+    K = args.steps
+    ev = [[torch.cuda.Event(enable_timing=True) for _ in range(3)] for _ in range(K)]
+    t_start = time.perf_counter()
+    for s in range(K):
+        ev[s][0].record(stream)
+        plan.run_stage(0, sh)
+        ev[s][1].record(stream)
+        plan.run_stage(1, sh)
+        ev[s][2].record(stream)
+    torch.cuda.synchronize()
+    if dist:
+        dist.barrier()
+    torch.cuda.synchronize()
+    wall = time.perf_counter() - t_start
+
+    part_ms = float(np.mean([ev[s][0].elapsed_time(ev[s][1]) for s in range(K)]))
+    agg_ms = float(np.mean([ev[s][1].elapsed_time(ev[s][2]) for s in range(K)]))
+
+    t = torch.tensor([wall], dtype=torch.float64, device=dev)
+    if dist:
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+    wall_max = float(t.item())
+    kv_rank = plan.kv_pairs
+    kvt = torch.tensor([float(kv_rank)], dtype=torch.float64, device=dev)
+    if dist:
+        dist.all_reduce(kvt)
+    kv_all = float(kvt.item())
+    value = kv_all * K / wall_max
+    ms_per_step = wall_max / K * 1e3
+
+    if args.profile_steps:
+        if rank == 0:
+            log(f"profile run: {ms_per_step:.3f} ms/step, aggregate {agg_ms:.3f} ms")
+        if dist:
+            dist.destroy_process_group()
+        return
+
+    # copy-kernel bandwidth in the same run (read + write bytes / time)
+    nbytes = 1 << 30
+    src = torch.empty(nbytes // 4, dtype=torch.float32, device=dev)
+    dst = torch.empty_like(src)
+    for _ in range(3):
+        dst.copy_(src)
+    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    e0.record(stream)
+    for _ in range(10):
+        dst.copy_(src)
+    e1.record(stream)
+    torch.cuda.synchronize()
+    copy_gbps = 2 * nbytes * 10 / (e0.elapsed_time(e1) * 1e-3) / 1e9
+    del src, dst
+
+    achieved = plan.bytes / (agg_ms * 1e-3) / 1e9
+    traffic = load_traffic(args, plan.bytes)
+
+    result = {
+        "metric": METRIC,
+        "value": value,
+        "unit": "kv-pairs/s",
+        "n_gpus": world,
+        "steps": K,
+        "warmup": args.warmup,
+        "ms_per_step": ms_per_step,
+        "higher_is_better": True,
+        "scaling": "weak",
+        "vs_baseline": None,
+        "dtype": "f32",
+        "data": "synthetic",
+        "config": {
+            "workload": (f"cfg2: {args.npush} pushes x {args.n} sorted unique uint64 keys + f32 "
+                         f"values, {int(args.overlap * 100)}% shared keys (U=956,827 at the "
+                         f"defaults); {args.batch} such (channel,time) aggregates per GPU per step"),
+            "global_batch": args.batch * world,
+            "kv_per_step": kv_all,
+            "parallelism": (f"key-range shards evenDivide({world}); "
+                            + ("worker-sliced ingress, no data-path collective"
+                               if args.ingress == "sliced" or world == 1 else
+                               "unsliced ingress, RCCL all-to-all re-homing")),
+        },
+        "roofline": {
+            "bound": "hbm",
+            "achieved": achieved,
+            "peak": HBM_PEAK_GBPS,
+            "unit": "GB/s",
+            "frac": achieved / HBM_PEAK_GBPS,
+            "traffic": traffic,
+            "kernel": "aggregate_kernel<float,1>",
+            "bytes_per_launch": plan.bytes,
+            "bytes_formula": "sum_p n_p*(8+4) [pushes] + U*(8+4) [server keys + sums]",
+            "kernel_ms": agg_ms,
+            "partition_ms": part_ms,
+            "measured_copy_GBps": copy_gbps,
+            "frac_of_measured_copy": achieved / copy_gbps,
+        },
+    }
+    if rank == 0 and world == 1 and not args.no_cpu_baseline:
+        result["cpu_baseline"] = cpu_baseline(insts[0], args.cpu_seconds)
+    if rank == 0:
+        print(json.dumps(result), flush=True)
+    if dist:
+        dist.destroy_process_group()
+
+
+def load_traffic(args, bytes_per_launch):
+    """HBM bytes per aggregate launch from the committed rocprofv3 PMC
+    summary (profiles/pmc_summary.json, written by tools/pmc_traffic.py),
+    when it was collected on this same workload; else null."""
+    p = os.path.join(ROOT, "profiles", "pmc_summary.json")
+    try:
+        d = json.load(open(p))
+    except Exception:
+        return None
+    if d.get("bytes_per_launch") != bytes_per_launch:
+        return None
+    return d.get("hbm_bytes_per_launch")
+
+
+def cpu_baseline(inst, seconds):
+    """The oracle's restatement of the reference CPU path (serialSetValue:
+    oldMatch + dense +=, the shipped default) on one cfg2 aggregate,
+    repeated for ~`seconds` on this host; plus the threaded match path."""
+    sys.path.insert(0, os.path.join(ROOT, "tests"))
+    import oracle_py as O
+    D, pushes = inst
+    kv = sum(int(k.size) for k, _ in pushes)
+    ALL = (0, (1 << 64) - 1)
+
+    def timed(parallel, nthreads):
+        reps, t0 = 0, time.perf_counter()
+        while True:
+            rc, *_ = O.aggregate(D, *ALL, pushes, parallel, nthreads)
+            assert rc == 0
+            reps += 1
+            el = time.perf_counter() - t0
+            if el >= seconds / 2:
+                return reps * kv / el, reps, el
+
+    v, reps, el = timed(0, 1)
+    nproc = os.cpu_count() or 1
+    vp, repsp, elp = timed(1, nproc)
+    model = ""
+    try:
+        for line in open("/proc/cpuinfo"):
+            if line.startswith("model name"):
+                model = line.split(":", 1)[1].strip()
+                break
+    except Exception:
+        pass
+    return {
+        "value": v, "unit": "kv-pairs/s", "cores": 1, "kind": "port",
+        "sample": (f"{reps} x one cfg2 aggregate (8 x 131072 kv, U={D.size}) through "
+                   f"oracle serialSetValue restatement in {el:.1f}s, 1 thread, {model}"),
+        "parallel_match": {"value": vp, "threads": nproc, "reps": repsp, "seconds": elp},
+    }
+
+
+if __name__ == "__main__":
+    main()

@@ -1,0 +1,171 @@
+/*
+ * psg.h -- C ABI of the MI355X-native server-side push aggregation path.
+ *
+ * This is the drop-in boundary that replaces the host-side hot path of
+ * wakensky/parameter_server:
+ *
+ *   KVVector<uint64,V>::setValue / serialSetValue / parallelSetValue
+ *       src/parameter/kv_vector.h:75-82, 84-137, 171-204
+ *   KVVector<uint64,V>::received          src/parameter/kv_vector.h:65-73
+ *   KVVector<uint64,V>::getValue (pull)   src/parameter/kv_vector.h:206-227
+ *   match / oldMatch merge kernels        src/system/message.h:134-267
+ *   SArray::setUnion / findRange          src/base/shared_array_inl.h:155-171
+ *   sliceKeyOrderedMsg / Range::evenDivide src/system/message.h:89-123,
+ *                                          src/base/range.h:85-98
+ *
+ * The reference calls these from SharedParameter<K>::process on the
+ * customer's executor thread (src/parameter/shared_parameter.h:91-149).
+ * Every entry point here takes plain pointers and sizes; none retains a
+ * caller pointer past the call (host data is staged before return), and
+ * every failure the reference turns into a glog CHECK abort is returned as
+ * a negative psg_status instead (the C++ adapter converts it back to an
+ * abort, see parameter_server_amd/csrc/kv_vector.h).
+ *
+ * Keys are uint64 (the reference's PS::Key); values are float or double
+ * (KVVector<Key,double> in linear_method/batch_solver.h:32).
+ */
+#ifndef PSG_H_
+#define PSG_H_
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define PSG_ABI_VERSION 1
+#define PSG_MAX_VALUE_ARRAYS 4   /* m: value arrays per push (Darling: 2) */
+
+typedef enum psg_status {
+  PSG_OK = 0,
+  PSG_ERR_ARG = -1,        /* bad argument (null pointer, m out of range ...) */
+  PSG_ERR_UNMATCHED = -2,  /* CHECK_EQ(recv_key.size(), n)  kv_vector.h:134,192 */
+  PSG_ERR_RANGE = -3,      /* CHECK_EQ(range, stored range) kv_vector.h:128,199 */
+  PSG_ERR_NO_TIME = -4,    /* CHECK(it != recved_val_.end()) kv_vector.h:69 */
+  PSG_ERR_OOM = -5,
+  PSG_ERR_DEVICE = -6,     /* HIP runtime error / no device */
+  PSG_ERR_UNSORTED = -7,   /* key-only push not strictly increasing */
+  PSG_ERR_SIZE = -8,       /* CHECK_EQ(recv_data.size(), recv_key.size()) :108,187 */
+  PSG_ERR_CHANNEL = -9,    /* pushes of one time t name different channels */
+  PSG_ERR_EMPTY_KEYS = -10 /* value push to a channel with no server keys */
+} psg_status;
+
+typedef enum psg_dtype { PSG_F32 = 0, PSG_F64 = 1 } psg_dtype;
+
+/* Aggregation semantics (FLAGS_parallel_match, system/postoffice.cc:24).
+ * SERIAL (the shipped default, script/local.sh:35) adds an explicit +0.0 for
+ * keys absent from a later push (kv_vector.h:200), so a -0.0 can become
+ * +0.0; PARALLEL touches only matched keys (message.h:195-198).  Both are
+ * reproduced bit-exactly. */
+#define PSG_SERIAL_MATCH 0u
+#define PSG_PARALLEL_MATCH 1u
+
+int psg_abi_version(void);
+const char* psg_status_string(int status);
+/* Thread-local text of the last error returned on this thread. */
+const char* psg_last_error(void);
+int psg_device_count(int* n);
+
+/* ------------------------------------------------------------------ */
+/* Server context: one KVVector<uint64,V> whose keys, values and      */
+/* per-time aggregates are resident in the HBM of one device.         */
+/* ------------------------------------------------------------------ */
+typedef struct psg_ctx psg_ctx;
+
+int psg_create(int device, int dtype, unsigned flags, psg_ctx** out);
+int psg_destroy(psg_ctx* ctx);
+int psg_set_match_flags(psg_ctx* ctx, unsigned flags);
+
+/* Key-only push: key_[chl] = key_[chl].setUnion(keys); val_[chl].clear()
+ * (kv_vector.h:177-182).  keys must be strictly increasing. */
+int psg_key_union(psg_ctx* ctx, int chl, const uint64_t* keys, size_t n);
+/* key(chl).size() / copy of key(chl)[off, off+n) (kv_vector.h:17). */
+int psg_key_size(psg_ctx* ctx, int chl, size_t* n);
+int psg_key_copy(psg_ctx* ctx, int chl, size_t off, size_t n, uint64_t* out);
+/* find(chl, [kb,ke)) = key_[chl].findRange (kv_vector.h:21-23). */
+int psg_find_range(psg_ctx* ctx, int chl, uint64_t kb, uint64_t ke,
+                   size_t* lo, size_t* hi);
+/* value(chl) (kv_vector.h:18): replace / read the server values. */
+int psg_value_assign(psg_ctx* ctx, int chl, const void* vals, size_t n);
+int psg_value_size(psg_ctx* ctx, int chl, size_t* n);
+int psg_value_copy(psg_ctx* ctx, int chl, size_t off, size_t n, void* out);
+
+/* Value push: setValue(msg) for msg->value of m arrays, each n entries,
+ * msg->task.key_range() = [kb, ke), msg->task.time() = time,
+ * msg->task.key_channel() = chl.  vals[i] points to array i.  Host data is
+ * staged before return; the merge runs asynchronously on the context's
+ * stream and its match check is reported by psg_received for `time`. */
+int psg_push(psg_ctx* ctx, int chl, int time, uint64_t kb, uint64_t ke,
+             const uint64_t* keys, size_t n, int m, const void* const* vals);
+/* Shape of the aggregate of `time`: m arrays over server positions
+ * [lo, hi) of key(chl).  PSG_ERR_NO_TIME if nothing was pushed. */
+int psg_received_shape(psg_ctx* ctx, int time, int* m, size_t* lo,
+                       size_t* hi);
+/* received(t): copies the m aggregates (hi-lo entries each) into out[i] and
+ * erases them.  Returns PSG_ERR_UNMATCHED if any push of `time` had a key
+ * that is not a server key of its range (or was unsorted / duplicated). */
+int psg_received(psg_ctx* ctx, int time, int m, void* const* out);
+
+/* Pull reply: getValue(msg) (kv_vector.h:206-227): out[i] = value(chl) at
+ * keys[i], 0 where keys[i] is not a server key.  keys sorted. */
+int psg_gather(psg_ctx* ctx, int chl, const uint64_t* keys, size_t n,
+               void* out, size_t* matched);
+
+/* ------------------------------------------------------------------ */
+/* Device-resident batched merge: the hot path with every buffer      */
+/* already in HBM (benchmarks, multi-GPU shards, graph capture).      */
+/* ------------------------------------------------------------------ */
+typedef struct psg_merge_job {
+  const uint64_t* keys;      /* device: server keys D[lo, hi) (sorted unique) */
+  uint64_t nslots;           /* hi - lo */
+  int npush;                 /* pushes of this (channel, time), arrival order */
+  const uint64_t* const* push_keys; /* host array[npush] of device pointers */
+  const void* const* push_vals;     /* host array[npush*m], [p*m + i] */
+  const uint64_t* push_n;           /* host array[npush] */
+  void* const* out;          /* host array[m] of device pointers, nslots each */
+} psg_merge_job;
+
+typedef struct psg_plan psg_plan;
+
+/* All jobs share dtype, m and flags; npush <= psg_plan_max_push() per job. */
+int psg_plan_create(int device, int dtype, int m, unsigned flags,
+                    const psg_merge_job* jobs, int njobs, psg_plan** out);
+int psg_plan_max_push(void);
+/* Enqueue the merge on `stream` (a hipStream_t; NULL = default stream).
+ * No allocation, no synchronisation: capturable into a hipGraph. */
+int psg_plan_run(psg_plan* plan, void* stream);
+/* One stage of psg_plan_run: 0 = partition (findRange / slice lower
+ * bounds), 1 = aggregate.  Lets a caller bracket the dominant kernel with
+ * its own events on `stream`. */
+int psg_plan_run_stage(psg_plan* plan, int stage, void* stream);
+/* Synchronises the plan's last run and returns per-push matched counts,
+ * jobs in order, pushes in order (sum of npush entries). */
+int psg_plan_matched(psg_plan* plan, uint64_t* matched);
+/* Algorithmic HBM bytes of one run (SURVEY.md 8d general form). */
+int psg_plan_bytes(psg_plan* plan, uint64_t* bytes, uint64_t* kv_pairs);
+int psg_plan_destroy(psg_plan* plan);
+
+/* Device-resident gather (pull reply) over resident keys/values. */
+int psg_gather_dev(int dtype, const uint64_t* dkeys, uint64_t nd,
+                   const void* dvals, const uint64_t* req, uint64_t nreq,
+                   void* out, unsigned long long* matched, void* stream);
+
+/* Device-resident key union: out = a U b (both strictly increasing);
+ * out must hold na+nb; *nout (host) receives |a U b|.  Synchronises. */
+int psg_key_union_dev(const uint64_t* a, uint64_t na, const uint64_t* b,
+                      uint64_t nb, uint64_t* out, uint64_t* nout,
+                      void* stream);
+
+/* Server shard boundaries: Range<uint64>::all().evenDivide(n, i)
+ * (range.h:75-98, linear_method.cc:137-145); bounds[n+1]. */
+int psg_shard_bounds(size_t n, uint64_t* bounds);
+/* sliceKeyOrderedMsg positions (message.h:89-123) of a device-resident
+ * sorted push: pos[nsep] device array, computed on `stream`. */
+int psg_slice_dev(const uint64_t* keys, uint64_t n, uint64_t kb, uint64_t ke,
+                  const uint64_t* sep, int nsep, uint64_t* pos, void* stream);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* PSG_H_ */

@@ -1,0 +1,381 @@
+/*
+ * psg_oracle.c -- TEST INFRASTRUCTURE ONLY (see psg_oracle.h).
+ *
+ * Plain-C restatement of the reference's CPU push-aggregation path.  Every
+ * function cites the reference file:line it restates.  Only tests/,
+ * __graft_entry__.smoke() and bench.py's cpu_baseline leg use it.
+ */
+#include "psg_oracle.h"
+
+#include <pthread.h>
+#include <stdlib.h>
+#include <string.h>
+
+/* std::lower_bound / upper_bound over uint64 */
+static size_t lb_u64(const uint64_t* a, size_t n, uint64_t k) {
+  size_t lo = 0, len = n;
+  while (len > 0) {
+    size_t half = len >> 1;
+    if (a[lo + half] < k) {
+      lo += half + 1;
+      len -= half + 1;
+    } else {
+      len = half;
+    }
+  }
+  return lo;
+}
+static size_t ub_u64(const uint64_t* a, size_t n, uint64_t k) {
+  size_t lo = 0, len = n;
+  while (len > 0) {
+    size_t half = len >> 1;
+    if (!(k < a[lo + half])) {
+      lo += half + 1;
+      len -= half + 1;
+    } else {
+      len = half;
+    }
+  }
+  return lo;
+}
+
+/* shared_array_inl.h:155-162 -> std::set_union (multiset semantics: an
+ * element present c_a times in a and c_b times in b appears max(c_a,c_b)
+ * times). */
+size_t orc_set_union_u64(const uint64_t* a, size_t na, const uint64_t* b,
+                         size_t nb, uint64_t* out) {
+  size_t i = 0, j = 0, k = 0;
+  while (i < na) {
+    if (j == nb) {
+      while (i < na) out[k++] = a[i++];
+      return k;
+    }
+    if (b[j] < a[i]) {
+      out[k++] = b[j++];
+    } else {
+      out[k++] = a[i];
+      if (!(a[i] < b[j])) ++j;
+      ++i;
+    }
+  }
+  while (j < nb) out[k++] = b[j++];
+  return k;
+}
+
+/* shared_array_inl.h:145-153 -> std::set_intersection */
+size_t orc_set_intersection_u64(const uint64_t* a, size_t na,
+                                const uint64_t* b, size_t nb, uint64_t* out) {
+  size_t i = 0, j = 0, k = 0;
+  while (i < na && j < nb) {
+    if (a[i] < b[j]) {
+      ++i;
+    } else {
+      if (!(b[j] < a[i])) out[k++] = a[i++];
+      ++j;
+    }
+  }
+  return k;
+}
+
+/* shared_array_inl.h:164-171 */
+void orc_find_range_u64(const uint64_t* a, size_t n, uint64_t kb, uint64_t ke,
+                        size_t* lo, size_t* hi) {
+  if (n == 0) {
+    *lo = *hi = 0;
+    return;
+  }
+  *lo = lb_u64(a, n, kb);
+  *hi = lb_u64(a, n, ke);
+}
+
+/* range.h:85-98: itv = (long double)(end-begin)/n; [begin+itv*i,
+ * begin+itv*(i+1)) with the last piece ending at end. */
+void orc_even_divide_u64(uint64_t begin, uint64_t end, size_t n, size_t i,
+                         uint64_t* out_begin, uint64_t* out_end) {
+  long double itv = (long double)(end - begin) / (long double)n;
+  uint64_t new_end = (uint64_t)(begin + itv * (long double)(i + 1));
+  if (i + 1 == n) new_end = end;
+  *out_begin = (uint64_t)(begin + itv * (long double)i);
+  *out_end = new_end;
+}
+
+/* message.h:89-123 (positions + validity only; the pieces are zero-copy
+ * segments [pos[i], pos[i+1]) of keys and, proportionally, of values). */
+void orc_slice_key_ordered(const uint64_t* keys, size_t n, uint64_t rb,
+                           uint64_t re, const uint64_t* sep, size_t nsep,
+                           size_t* pos, int* valid) {
+  for (size_t s = 0; s < nsep; ++s) {
+    uint64_t p = sep[s];
+    uint64_t k = p < re ? p : re;       /* std::min(range.end, p) */
+    if (k < rb) k = rb;                 /* std::max(range.begin, .) */
+    pos[s] = lb_u64(keys, n, k);
+  }
+  for (size_t s = 0; s + 1 < nsep; ++s) {
+    uint64_t ib = sep[s] > rb ? sep[s] : rb;
+    uint64_t ie = sep[s + 1] < re ? sep[s + 1] : re;
+    valid[s] = !(ib >= ie);             /* Range::setIntersection().empty() */
+  }
+}
+
+/* ---------------------------------------------------------------------- */
+/* oldMatch (message.h:228-267) and match (message.h:134-226), per V.      */
+/* ---------------------------------------------------------------------- */
+
+#define DEFINE_OLD_MATCH(SUF, V)                                               \
+  int orc_old_match_##SUF(const uint64_t* dst_key, size_t ndst,               \
+                          const uint64_t* src_key, size_t nsrc,               \
+                          const V* src_val, uint64_t kb, uint64_t ke, V* out, \
+                          size_t* lo, size_t* hi, size_t* matched) {          \
+    *matched = 0;                                                              \
+    *lo = *hi = 0;                                                             \
+    if (ndst == 0 || nsrc == 0) return 0; /* message.h:236-238 */              \
+    orc_find_range_u64(dst_key, ndst, kb, ke, lo, hi); /* :240 */              \
+    size_t len = *hi - *lo;                                                    \
+    memset(out, 0, sizeof(V) * len); /* :242-244 */                            \
+    if (len == 0) return 0;                                                    \
+    /* :247-249 binary search the start point */                               \
+    const uint64_t* d = dst_key + *lo;                                         \
+    const uint64_t* dend = dst_key + *hi; /* defined: stop at range end */     \
+    size_t s = lb_u64(src_key, nsrc, *d);                                      \
+    V* o = out;                                                                \
+    while (d != dend && s != nsrc) { /* :251-265 merge walk */                 \
+      if (src_key[s] < *d) {                                                   \
+        ++s;                                                                   \
+      } else {                                                                 \
+        if (!(*d < src_key[s])) {                                              \
+          *o = src_val[s];                                                     \
+          ++s;                                                                 \
+          ++*matched;                                                          \
+        }                                                                      \
+        ++d;                                                                   \
+        ++o;                                                                   \
+      }                                                                        \
+    }                                                                          \
+    return 0;                                                                  \
+  }
+
+DEFINE_OLD_MATCH(f32, float)
+DEFINE_OLD_MATCH(f64, double)
+
+#define DEFINE_MATCH(SUF, V)                                                   \
+  typedef struct {                                                             \
+    size_t b, e, lo;                                                           \
+    const uint64_t* dst_key;                                                   \
+    V* dst_val;                                                                \
+    const uint64_t* src_key;                                                   \
+    size_t nsrc;                                                               \
+    const V* src_val;                                                          \
+    int op;                                                                    \
+    size_t matched;                                                            \
+  } match_arg_##SUF;                                                           \
+  static void* match_worker_##SUF(void* p) {                                   \
+    match_arg_##SUF* a = (match_arg_##SUF*)p;                                  \
+    a->matched = 0;                                                            \
+    if (a->e <= a->b) return NULL; /* Appendix B #5: empty slice */            \
+    const uint64_t* d = a->dst_key + a->b;                                     \
+    const uint64_t* dend = a->dst_key + a->e;                                  \
+    V* o = a->dst_val + (a->b - a->lo);                                        \
+    /* message.h:177-179 */                                                    \
+    size_t s = lb_u64(a->src_key, a->nsrc, *d);                                \
+    size_t send = ub_u64(a->src_key, a->nsrc, *(dend - 1));                    \
+    if (a->op == 0) memset(o, 0, sizeof(V) * (size_t)(dend - d)); /* :182 */   \
+    while (d != dend && s != send) { /* :187-214 */                            \
+      if (a->src_key[s] < *d) {                                                \
+        ++s;                                                                   \
+      } else {                                                                 \
+        if (!(*d < a->src_key[s])) {                                           \
+          if (a->op == 0)                                                      \
+            *o = a->src_val[s];                                                \
+          else                                                                 \
+            *o += a->src_val[s];                                               \
+          ++s;                                                                 \
+          ++a->matched;                                                        \
+        }                                                                      \
+        ++d;                                                                   \
+        ++o;                                                                   \
+      }                                                                        \
+    }                                                                          \
+    return NULL;                                                               \
+  }                                                                            \
+  void orc_match_##SUF(size_t lo, size_t hi, const uint64_t* dst_key,         \
+                       V* dst_val, const uint64_t* src_key, size_t nsrc,      \
+                       const V* src_val, int op, int nthreads,                \
+                       size_t* matched) {                                      \
+    *matched = 0;                                                              \
+    if (hi <= lo || nsrc == 0) return; /* message.h:145-147 */                 \
+    if (nthreads < 1) nthreads = 1;                                            \
+    match_arg_##SUF* args =                                                    \
+        (match_arg_##SUF*)calloc((size_t)nthreads, sizeof(match_arg_##SUF));   \
+    pthread_t* th = (pthread_t*)calloc((size_t)nthreads, sizeof(pthread_t));   \
+    for (int t = 0; t < nthreads; ++t) {                                       \
+      /* message.h:160-166: SizeR::evenDivide, last thread takes the rest */   \
+      uint64_t b, e;                                                           \
+      orc_even_divide_u64(lo, hi, (size_t)nthreads, (size_t)t, &b, &e);       \
+      if (t == nthreads - 1) e = hi;                                           \
+      match_arg_##SUF a = {b, e, lo, dst_key, dst_val, src_key,               \
+                           nsrc, src_val, op, 0};                              \
+      args[t] = a;                                                             \
+    }                                                                          \
+    if (nthreads == 1) {                                                       \
+      match_worker_##SUF(&args[0]);                                            \
+    } else {                                                                   \
+      /* a pool is created and joined on every call (message.h:152-218) */    \
+      for (int t = 0; t < nthreads; ++t)                                       \
+        pthread_create(&th[t], NULL, match_worker_##SUF, &args[t]);            \
+      for (int t = 0; t < nthreads; ++t) pthread_join(th[t], NULL);            \
+    }                                                                          \
+    for (int t = 0; t < nthreads; ++t) *matched += args[t].matched;           \
+    free(args);                                                                \
+    free(th);                                                                  \
+  }
+
+DEFINE_MATCH(f32, float)
+DEFINE_MATCH(f64, double)
+
+/* ---------------------------------------------------------------------- */
+/* KVVector::serialSetValue / parallelSetValue over one time t.            */
+/* ---------------------------------------------------------------------- */
+
+#define DEFINE_AGGREGATE(SUF, V)                                               \
+  int orc_aggregate_##SUF(const uint64_t* D, size_t nD, uint64_t kb,          \
+                          uint64_t ke, int npush,                              \
+                          const uint64_t* const* keys, const size_t* n, int m, \
+                          const V* const* vals, int parallel, int nthreads,   \
+                          V* const* out, size_t* lo, size_t* hi,               \
+                          size_t* matched) {                                   \
+    *lo = *hi = 0;                                                             \
+    int have = 0; /* recved_val_[t] exists */                                  \
+    for (int p = 0; p < npush; ++p) {                                          \
+      matched[p] = 0;                                                          \
+      if (n[p] == 0) continue; /* kv_vector.h:90,177: empty push ignored */    \
+      if (nD == 0) return -1;  /* CHECK_GE / range CHECK fails */              \
+      size_t plo, phi;                                                         \
+      orc_find_range_u64(D, nD, kb, ke, &plo, &phi);                           \
+      if (have && (plo != *lo || phi != *hi)) return -2; /* CHECK_EQ range */  \
+      size_t len = phi - plo;                                                  \
+      for (int i = 0; i < m; ++i) {                                            \
+        const V* v = vals[(size_t)p * m + i];                                  \
+        size_t mt = 0;                                                         \
+        if (!parallel) {                                                       \
+          /* kv_vector.h:190: aligned = oldMatch(...) (new + memset) */       \
+          size_t alo, ahi;                                                     \
+          if (!have) { /* :195-196 the first aligned array is stored */        \
+            orc_old_match_##SUF(D, nD, keys[p], n[p], v, kb, ke, out[i], &alo, \
+                                &ahi, &mt);                                    \
+          } else {                                                             \
+            V* aligned = (V*)malloc(sizeof(V) * (len ? len : 1));              \
+            orc_old_match_##SUF(D, nD, keys[p], n[p], v, kb, ke, aligned,     \
+                                &alo, &ahi, &mt);                              \
+            V* acc = out[i]; /* :200 eigenArray() += */                        \
+            for (size_t j = 0; j < len; ++j) acc[j] += aligned[j];             \
+            free(aligned);                                                     \
+          }                                                                    \
+        } else {                                                               \
+          /* kv_vector.h:114-131: first push ASSIGN, later ADD */              \
+          orc_match_##SUF(plo, phi, D, out[i], keys[p], n[p], v,              \
+                          have ? 1 : 0, nthreads, &mt);                        \
+        }                                                                      \
+        matched[p] = mt;                                                       \
+      }                                                                        \
+      if (!have) {                                                             \
+        *lo = plo;                                                             \
+        *hi = phi;                                                             \
+        have = 1;                                                              \
+      }                                                                        \
+    }                                                                          \
+    return 0;                                                                  \
+  }
+
+DEFINE_AGGREGATE(f32, float)
+DEFINE_AGGREGATE(f64, double)
+
+/* kv_vector.h:215-227: oldMatch(recv_key, key_[ch], val_[ch], union range)
+ * -- a gather aligned to the request keys, zero where absent. */
+#define DEFINE_GATHER(SUF, V)                                                  \
+  void orc_gather_##SUF(const uint64_t* D, size_t nD, const V* W,             \
+                        const uint64_t* req, size_t nreq, V* out,             \
+                        size_t* matched) {                                     \
+    *matched = 0;                                                              \
+    memset(out, 0, sizeof(V) * nreq);                                          \
+    if (nD == 0 || nreq == 0) return;                                          \
+    size_t i = 0, j = lb_u64(D, nD, req[0]);                                   \
+    while (i < nreq && j < nD) {                                               \
+      if (D[j] < req[i]) {                                                     \
+        ++j;                                                                   \
+      } else {                                                                 \
+        if (!(req[i] < D[j])) {                                                \
+          out[i] = W[j];                                                       \
+          ++j;                                                                 \
+          ++*matched;                                                          \
+        }                                                                      \
+        ++i;                                                                   \
+      }                                                                        \
+    }                                                                          \
+  }
+
+DEFINE_GATHER(f32, float)
+DEFINE_GATHER(f64, double)
+
+/* ---------------------------------------------------------------------- */
+/* MurmurHash3_x64_128 (util/MurmurHash3.cc:255-331), restated.            */
+/* ---------------------------------------------------------------------- */
+static inline uint64_t rotl64(uint64_t x, int r) {
+  return (x << r) | (x >> (64 - r));
+}
+static inline uint64_t fmix64(uint64_t k) {
+  k ^= k >> 33;
+  k *= 0xff51afd7ed558ccdULL;
+  k ^= k >> 33;
+  k *= 0xc4ceb9fe1a85ec53ULL;
+  k ^= k >> 33;
+  return k;
+}
+
+void orc_murmur3_x64_128(const void* key, int len, uint32_t seed,
+                         uint64_t out[2]) {
+  const uint8_t* data = (const uint8_t*)key;
+  const int nblocks = len / 16;
+  uint64_t h1 = seed, h2 = seed;
+  const uint64_t c1 = 0x87c37b91114253d5ULL, c2 = 0x4cf5ad432745937fULL;
+  for (int i = 0; i < nblocks; i++) {
+    uint64_t k1, k2;
+    memcpy(&k1, data + 16 * i, 8);
+    memcpy(&k2, data + 16 * i + 8, 8);
+    k1 *= c1; k1 = rotl64(k1, 31); k1 *= c2; h1 ^= k1;
+    h1 = rotl64(h1, 27); h1 += h2; h1 = h1 * 5 + 0x52dce729;
+    k2 *= c2; k2 = rotl64(k2, 33); k2 *= c1; h2 ^= k2;
+    h2 = rotl64(h2, 31); h2 += h1; h2 = h2 * 5 + 0x38495ab5;
+  }
+  const uint8_t* tail = data + nblocks * 16;
+  uint64_t k1 = 0, k2 = 0;
+  int rem = len & 15;
+  for (int t = rem - 1; t >= 8; --t) k2 ^= ((uint64_t)tail[t]) << (8 * (t - 8));
+  if (rem > 8) {
+    k2 *= c2; k2 = rotl64(k2, 33); k2 *= c1; h2 ^= k2;
+  }
+  for (int t = (rem < 8 ? rem : 8) - 1; t >= 0; --t)
+    k1 ^= ((uint64_t)tail[t]) << (8 * t);
+  if (rem > 0) {
+    k1 *= c1; k1 = rotl64(k1, 31); k1 *= c2; h1 ^= k1;
+  }
+  h1 ^= (uint64_t)len;
+  h2 ^= (uint64_t)len;
+  h1 += h2;
+  h2 += h1;
+  h1 = fmix64(h1);
+  h2 = fmix64(h2);
+  h1 += h2;
+  h2 += h1;
+  out[0] = h1;
+  out[1] = h2;
+}
+
+/* data/example_parser.cc:205-208 */
+void orc_shuffle_keys(const uint64_t* ids, size_t n, uint32_t seed,
+                      uint64_t* out) {
+  for (size_t i = 0; i < n; ++i) {
+    uint64_t o[2];
+    orc_murmur3_x64_128(&ids[i], 8, seed, o);
+    out[i] = o[0] ^ o[1];
+  }
+}

@@ -1,0 +1,141 @@
+"""ctypes binding of the native C ABI (include/psg.h) in libpsg.so.
+
+The library is built in-tree by ``__graft_entry__.build()`` (or
+``make -C parameter_server_amd/csrc``).  There is no fallback: if the
+shared object is missing, :func:`lib` raises, so nothing silently runs a CPU
+path in its place.
+
+``torch`` is imported before the library is loaded whenever it is
+available, so that the process holds ONE HIP runtime (torch's bundled
+``libamdhip64.so.7``, which then also satisfies libpsg's dependency by
+soname) and device pointers / streams from torch are valid here.
+"""
+from __future__ import annotations
+
+import ctypes as C
+import os
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(_HERE, "libpsg.so")
+
+PSG_OK = 0
+PSG_ERR_ARG = -1
+PSG_ERR_UNMATCHED = -2
+PSG_ERR_RANGE = -3
+PSG_ERR_NO_TIME = -4
+PSG_ERR_OOM = -5
+PSG_ERR_DEVICE = -6
+PSG_ERR_UNSORTED = -7
+PSG_ERR_SIZE = -8
+PSG_ERR_CHANNEL = -9
+PSG_ERR_EMPTY_KEYS = -10
+
+PSG_F32 = 0
+PSG_F64 = 1
+PSG_SERIAL_MATCH = 0
+PSG_PARALLEL_MATCH = 1
+MAX_VALUE_ARRAYS = 4
+
+# Every symbol include/psg.h declares, with its ctypes signature.
+_u64 = C.c_uint64
+_sz = C.c_size_t
+_p = C.c_void_p
+_pu64 = C.POINTER(C.c_uint64)
+_psz = C.POINTER(C.c_size_t)
+
+
+class MergeJob(C.Structure):
+    """psg_merge_job (include/psg.h)."""
+
+    _fields_ = [
+        ("keys", _p),
+        ("nslots", _u64),
+        ("npush", C.c_int),
+        ("push_keys", C.POINTER(_p)),
+        ("push_vals", C.POINTER(_p)),
+        ("push_n", _pu64),
+        ("out", C.POINTER(_p)),
+    ]
+
+
+SIGNATURES = {
+    "psg_abi_version": (C.c_int, []),
+    "psg_status_string": (C.c_char_p, [C.c_int]),
+    "psg_last_error": (C.c_char_p, []),
+    "psg_device_count": (C.c_int, [C.POINTER(C.c_int)]),
+    "psg_create": (C.c_int, [C.c_int, C.c_int, C.c_uint, C.POINTER(_p)]),
+    "psg_destroy": (C.c_int, [_p]),
+    "psg_set_match_flags": (C.c_int, [_p, C.c_uint]),
+    "psg_key_union": (C.c_int, [_p, C.c_int, _p, _sz]),
+    "psg_key_size": (C.c_int, [_p, C.c_int, _psz]),
+    "psg_key_copy": (C.c_int, [_p, C.c_int, _sz, _sz, _p]),
+    "psg_find_range": (C.c_int, [_p, C.c_int, _u64, _u64, _psz, _psz]),
+    "psg_value_assign": (C.c_int, [_p, C.c_int, _p, _sz]),
+    "psg_value_size": (C.c_int, [_p, C.c_int, _psz]),
+    "psg_value_copy": (C.c_int, [_p, C.c_int, _sz, _sz, _p]),
+    "psg_push": (C.c_int, [_p, C.c_int, C.c_int, _u64, _u64, _p, _sz, C.c_int,
+                           C.POINTER(_p)]),
+    "psg_received_shape": (C.c_int, [_p, C.c_int, C.POINTER(C.c_int), _psz, _psz]),
+    "psg_received": (C.c_int, [_p, C.c_int, C.c_int, C.POINTER(_p)]),
+    "psg_gather": (C.c_int, [_p, C.c_int, _p, _sz, _p, _psz]),
+    "psg_plan_create": (C.c_int, [C.c_int, C.c_int, C.c_int, C.c_uint,
+                                  C.POINTER(MergeJob), C.c_int, C.POINTER(_p)]),
+    "psg_plan_max_push": (C.c_int, []),
+    "psg_plan_run": (C.c_int, [_p, _p]),
+    "psg_plan_run_stage": (C.c_int, [_p, C.c_int, _p]),
+    "psg_plan_matched": (C.c_int, [_p, _pu64]),
+    "psg_plan_bytes": (C.c_int, [_p, _pu64, _pu64]),
+    "psg_plan_destroy": (C.c_int, [_p]),
+    "psg_gather_dev": (C.c_int, [C.c_int, _p, _u64, _p, _p, _u64, _p, _p, _p]),
+    "psg_key_union_dev": (C.c_int, [_p, _u64, _p, _u64, _p, _pu64, _p]),
+    "psg_shard_bounds": (C.c_int, [_sz, _pu64]),
+    "psg_slice_dev": (C.c_int, [_p, _u64, _u64, _u64, _p, C.c_int, _p, _p]),
+}
+
+_LIB = None
+
+
+class PSGError(RuntimeError):
+    """A negative psg_status from the native library."""
+
+    def __init__(self, status: int, msg: str):
+        super().__init__(f"psg status {status}: {msg}")
+        self.status = status
+
+
+def lib() -> C.CDLL:
+    """Load libpsg.so (raises if it has not been built)."""
+    global _LIB
+    if _LIB is not None:
+        return _LIB
+    if not os.path.exists(LIB_PATH):
+        raise ImportError(
+            f"{LIB_PATH} is missing: build it with "
+            "`python -c 'import __graft_entry__ as g; g.build()'` "
+            "(no CPU fallback exists for this path)")
+    try:  # one HIP runtime per process: let torch load it first
+        import torch  # noqa: F401
+    except Exception:  # pragma: no cover - torch is optional for the ABI
+        pass
+    L = C.CDLL(LIB_PATH, mode=C.RTLD_GLOBAL)
+    for name, (res, args) in SIGNATURES.items():
+        f = getattr(L, name)
+        f.restype = res
+        f.argtypes = args
+    if L.psg_abi_version() != 1:
+        raise ImportError("libpsg ABI version mismatch")
+    _LIB = L
+    return L
+
+
+def check(rc: int) -> None:
+    if rc != PSG_OK:
+        L = lib()
+        raise PSGError(rc, L.psg_last_error().decode(errors="replace"))
+
+
+def ptr_array(ptrs) -> "C.Array":
+    arr = (_p * max(1, len(ptrs)))()
+    for i, v in enumerate(ptrs):
+        arr[i] = v
+    return arr

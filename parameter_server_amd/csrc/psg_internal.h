@@ -1,0 +1,64 @@
+// psg_internal.h -- shared between the gfx950 kernels (psg_kernels.hip) and
+// the host runtime behind the C ABI (psg_runtime.hip).  Not installed.
+#pragma once
+
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+namespace psg {
+
+// ---- aggregate kernel geometry (see DESIGN.md "Kernels") ----
+constexpr int kTile = 2048;                 // server slots per workgroup tile
+constexpr int kThreads = 512;               // 8 waves of 64
+constexpr int kSPT = kTile / kThreads;      // slots owned per thread (4)
+constexpr int kEPT = 8;                     // push elements per thread per chunk
+constexpr int kChunk = kThreads * kEPT;     // 4096 elements staged per chunk
+constexpr int kGroup = 64;                  // pushes per chunk (one mask bit each)
+constexpr int kMaxPush = 512;               // pushes per job per launch
+constexpr int kMaxM = 4;                    // value arrays per push
+
+constexpr uint32_t kFlagParallel = 1u;      // PSG_PARALLEL_MATCH
+constexpr uint32_t kFlagCont = 2u;          // continue an aggregate of an earlier launch
+
+// One (channel, time) aggregate as the kernels see it.  All pointers are
+// device pointers.  seg[b*npush + p] = first index of push p whose key is
+// >= D[b*kTile] (b < ntiles) or > D[nslots-1] (b == ntiles).
+struct JobDev {
+  const uint64_t* dkeys;          // D + lo
+  uint64_t nslots;                // hi - lo
+  const uint64_t* const* pkeys;   // [npush]
+  const void* const* pvals;       // [npush * m]
+  const uint64_t* pn;             // [npush]
+  void* const* out;               // [m]
+  uint32_t* seg;                  // [(ntiles + 1) * npush]
+  unsigned long long* fail;       // [npush] in-tile match failures
+  uint32_t npush;
+  uint32_t ntiles;
+  uint32_t tile_begin;            // first global tile (blockIdx.x) of this job
+  uint32_t part_begin;            // first global partition item of this job
+  uint32_t flags;
+  uint32_t pad;
+};
+
+// Kernel launchers (psg_kernels.hip).  All enqueue on `stream` only.
+hipError_t launch_partition(const JobDev* d_jobs, int njobs, uint32_t nitems,
+                            hipStream_t stream);
+hipError_t launch_aggregate(int dtype, int m, const JobDev* d_jobs, int njobs,
+                            uint32_t ntiles, hipStream_t stream);
+hipError_t launch_gather(int dtype, const uint64_t* dkeys, uint64_t nd,
+                         const void* dvals, const uint64_t* req, uint64_t nreq,
+                         void* out, unsigned long long* matched,
+                         hipStream_t stream);
+// keys strictly increasing?  *bad (device) += number of violations.
+hipError_t launch_check_sorted(const uint64_t* keys, uint64_t n,
+                               unsigned long long* bad, hipStream_t stream);
+// out = a U b (strictly increasing inputs).  scratch: >= union_scratch_bytes(nb).
+size_t union_scratch_bytes(uint64_t nb);
+hipError_t launch_union(const uint64_t* a, uint64_t na, const uint64_t* b,
+                        uint64_t nb, uint64_t* out, void* scratch,
+                        uint64_t* d_nout, hipStream_t stream);
+hipError_t launch_slice(const uint64_t* keys, uint64_t n, uint64_t kb,
+                        uint64_t ke, const uint64_t* sep, int nsep,
+                        uint64_t* pos, hipStream_t stream);
+
+}  // namespace psg

@@ -1,0 +1,750 @@
+// psg_runtime.hip -- host side of the C ABI (include/psg.h).
+//
+// psg_ctx mirrors KVVector<uint64,V> (src/parameter/kv_vector.h:13-62): per
+// channel sorted server keys key_[chl] and values val_[chl], and per time t
+// the aggregate recved_val_[t].  Keys/values/aggregates live in the HBM of
+// one device; a host mirror of key_[chl] serves findRange without a device
+// round trip.  All device work is ordered on one HIP stream per context;
+// a mutex gives the reference's threading contract (setValue on the
+// executor thread, received() from the app thread, kv_vector.h:45,67).
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <cstdarg>
+#include <cstdio>
+#include <cstring>
+#include <map>
+#include <mutex>
+#include <string>
+#include <unordered_map>
+#include <vector>
+
+#include "../../include/psg.h"
+#include "psg_internal.h"
+
+using psg::JobDev;
+
+namespace {
+
+thread_local std::string g_err;
+
+int fail(int code, const char* fmt, ...) {
+  char buf[512];
+  va_list ap;
+  va_start(ap, fmt);
+  vsnprintf(buf, sizeof(buf), fmt, ap);
+  va_end(ap);
+  g_err = buf;
+  return code;
+}
+
+#define HIP_TRY(expr)                                                        \
+  do {                                                                       \
+    hipError_t _e = (expr);                                                  \
+    if (_e != hipSuccess)                                                    \
+      return fail(_e == hipErrorOutOfMemory ? PSG_ERR_OOM : PSG_ERR_DEVICE,  \
+                  "%s: %s (%s:%d)", #expr, hipGetErrorString(_e), __FILE__,  \
+                  __LINE__);                                                 \
+  } while (0)
+
+size_t vsize(int dtype) { return dtype == PSG_F32 ? 4 : 8; }
+
+size_t align_up(size_t x, size_t a) { return (x + a - 1) / a * a; }
+
+// --------------------------------------------------------------------------
+// Job table: device image of a batch of merge jobs (shared by psg_plan and
+// the context's flushes).
+// --------------------------------------------------------------------------
+struct JobSpec {
+  const uint64_t* keys;
+  uint64_t nslots;
+  std::vector<const uint64_t*> pkeys;
+  std::vector<const void*> pvals;  // [p*m + i]
+  std::vector<uint64_t> pn;
+  std::vector<void*> out;
+  uint32_t flags;
+};
+
+struct JobTable {
+  int device = -1;
+  int dtype = 0, m = 1;
+  std::vector<JobDev> h;
+  std::vector<std::vector<uint64_t>> pn;
+  std::vector<uint64_t> nslots;
+  uint32_t ntiles = 0, nitems = 0;
+  void* blob = nullptr;
+  size_t blob_bytes = 0;
+  JobDev* d_jobs = nullptr;
+  std::vector<char> host_img;
+
+  void release() {
+    if (blob) (void)hipFree(blob);
+    blob = nullptr;
+    blob_bytes = 0;
+  }
+
+  // Builds (or rebuilds, reusing the allocation when it fits) the device image.
+  int build(int dev, int dt, int mm, const std::vector<JobSpec>& jobs) {
+    device = dev;
+    dtype = dt;
+    m = mm;
+    h.clear();
+    pn.clear();
+    nslots.clear();
+    ntiles = nitems = 0;
+    // layout: [JobDev x njobs] then per job: pkeys, pvals, pn, out, fail, seg
+    size_t off = align_up(sizeof(JobDev) * jobs.size(), 256);
+    struct Offs { size_t pk, pv, pn, out, fail, seg; };
+    std::vector<Offs> offs(jobs.size());
+    uint64_t tiles = 0, items = 0;
+    for (size_t j = 0; j < jobs.size(); ++j) {
+      const JobSpec& s = jobs[j];
+      const size_t np = s.pn.size();
+      const uint64_t nt = (s.nslots + psg::kTile - 1) / psg::kTile;
+      if (np > (size_t)psg::kMaxPush)
+        return fail(PSG_ERR_ARG, "job %zu: %zu pushes > max %d", j, np, psg::kMaxPush);
+      for (size_t p = 0; p < np; ++p)
+        if (s.pn[p] >= (1ull << 32))
+          return fail(PSG_ERR_ARG, "push of %llu keys >= 2^32", (unsigned long long)s.pn[p]);
+      Offs& o = offs[j];
+      o.pk = off; off = align_up(off + 8 * np, 64);
+      o.pv = off; off = align_up(off + 8 * np * m, 64);
+      o.pn = off; off = align_up(off + 8 * np, 64);
+      o.out = off; off = align_up(off + 8 * m, 64);
+      o.fail = off; off = align_up(off + 8 * np, 64);
+      o.seg = off; off = align_up(off + 4 * (nt + 1) * np, 256);
+      JobDev d{};
+      d.nslots = s.nslots;
+      d.dkeys = s.keys;
+      d.npush = (uint32_t)np;
+      d.ntiles = (uint32_t)nt;
+      d.tile_begin = (uint32_t)tiles;
+      d.part_begin = (uint32_t)items;
+      d.flags = s.flags;
+      tiles += nt;
+      items += (nt + 1) * np;
+      if (tiles >= (1ull << 31) || items >= (1ull << 31))
+        return fail(PSG_ERR_ARG, "batch too large (%llu tiles)", (unsigned long long)tiles);
+      h.push_back(d);
+      pn.push_back(s.pn);
+      nslots.push_back(s.nslots);
+    }
+    ntiles = (uint32_t)tiles;
+    nitems = (uint32_t)items;
+    if (off > blob_bytes) {
+      release();
+      HIP_TRY(hipMalloc(&blob, off));
+      blob_bytes = off;
+    }
+    char* base = (char*)blob;
+    host_img.assign(off, 0);
+    for (size_t j = 0; j < jobs.size(); ++j) {
+      const JobSpec& s = jobs[j];
+      const Offs& o = offs[j];
+      const size_t np = s.pn.size();
+      memcpy(&host_img[o.pk], s.pkeys.data(), 8 * np);
+      memcpy(&host_img[o.pv], s.pvals.data(), 8 * np * m);
+      memcpy(&host_img[o.pn], s.pn.data(), 8 * np);
+      memcpy(&host_img[o.out], s.out.data(), 8 * m);
+      JobDev& d = h[j];
+      d.pkeys = (const uint64_t* const*)(base + o.pk);
+      d.pvals = (const void* const*)(base + o.pv);
+      d.pn = (const uint64_t*)(base + o.pn);
+      d.out = (void* const*)(base + o.out);
+      d.fail = (unsigned long long*)(base + o.fail);
+      d.seg = (uint32_t*)(base + o.seg);
+    }
+    memcpy(host_img.data(), h.data(), sizeof(JobDev) * h.size());
+    d_jobs = (JobDev*)blob;
+    HIP_TRY(hipMemcpy(blob, host_img.data(), off, hipMemcpyHostToDevice));
+    return PSG_OK;
+  }
+
+  int run(hipStream_t s) const {
+    if (h.empty()) return PSG_OK;
+    HIP_TRY(psg::launch_partition(d_jobs, (int)h.size(), nitems, s));
+    HIP_TRY(psg::launch_aggregate(dtype, m, d_jobs, (int)h.size(), ntiles, s));
+    return PSG_OK;
+  }
+
+  // matched[p] = (covered elements) - (in-tile failures); stream must be idle.
+  int matched(std::vector<uint64_t>& out) const {
+    out.clear();
+    for (size_t j = 0; j < h.size(); ++j) {
+      const JobDev& d = h[j];
+      const uint32_t np = d.npush;
+      std::vector<uint32_t> first(np), last(np);
+      std::vector<unsigned long long> f(np);
+      if (np == 0) continue;
+      HIP_TRY(hipMemcpy(first.data(), d.seg, 4 * np, hipMemcpyDeviceToHost));
+      HIP_TRY(hipMemcpy(last.data(), d.seg + (size_t)d.ntiles * np, 4 * np,
+                        hipMemcpyDeviceToHost));
+      HIP_TRY(hipMemcpy(f.data(), d.fail, 8 * np, hipMemcpyDeviceToHost));
+      for (uint32_t p = 0; p < np; ++p) {
+        const uint64_t covered = nslots[j] ? (uint64_t)(last[p] - first[p]) : 0;
+        out.push_back(covered >= f[p] ? covered - f[p] : 0);
+      }
+    }
+    return PSG_OK;
+  }
+};
+
+}  // namespace
+
+// ==========================================================================
+// plan API (device-resident batch)
+// ==========================================================================
+struct psg_plan {
+  JobTable table;
+  hipStream_t last = nullptr;
+  uint64_t bytes = 0, kv = 0;
+};
+
+// ==========================================================================
+// server context
+// ==========================================================================
+namespace {
+
+struct Channel {
+  uint64_t* d_keys = nullptr;
+  size_t n = 0, cap = 0;
+  std::vector<uint64_t> h_keys;  // host mirror of key_[chl]
+  void* d_vals = nullptr;
+  size_t nvals = 0;
+};
+
+struct PendingPush {
+  uint64_t* d_keys = nullptr;      // keys then values in one allocation
+  void* d_vals[psg::kMaxM] = {};
+  uint64_t n = 0;
+};
+
+struct Aggregate {
+  int chl = 0, m = 0;
+  size_t lo = 0, hi = 0;
+  void* d_out[psg::kMaxM] = {};
+  std::vector<PendingPush> pending;
+  uint64_t folded = 0;               // pushes already merged into d_out
+  uint64_t expected_total = 0, matched_total = 0;
+  bool unmatched = false;
+};
+
+}  // namespace
+
+struct psg_ctx {
+  int device = 0;
+  int dtype = PSG_F32;
+  unsigned flags = PSG_SERIAL_MATCH;
+  hipStream_t stream = nullptr;
+  std::mutex mu;
+  std::unordered_map<int, Channel> ch;
+  std::map<int, Aggregate> agg;
+  JobTable table;
+  unsigned long long* d_counter = nullptr;  // scratch counter (8 words)
+  void* scratch = nullptr;
+  size_t scratch_bytes = 0;
+
+  int ensure_scratch(size_t b) {
+    if (b <= scratch_bytes) return PSG_OK;
+    if (scratch) HIP_TRY(hipFree(scratch));
+    scratch = nullptr;
+    scratch_bytes = 0;
+    HIP_TRY(hipMalloc(&scratch, b));
+    scratch_bytes = b;
+    return PSG_OK;
+  }
+
+  // Merge every pending push of aggregate `a` into its device output.
+  int flush(Aggregate& a) {
+    while (!a.pending.empty()) {
+      const size_t take = std::min(a.pending.size(), (size_t)psg::kMaxPush);
+      JobSpec js;
+      js.keys = ch[a.chl].d_keys + a.lo;
+      js.nslots = a.hi - a.lo;
+      js.flags = (flags & PSG_PARALLEL_MATCH ? psg::kFlagParallel : 0u) |
+                 (a.folded > 0 ? psg::kFlagCont : 0u);
+      for (size_t p = 0; p < take; ++p) {
+        const PendingPush& pp = a.pending[p];
+        js.pkeys.push_back(pp.d_keys);
+        for (int i = 0; i < a.m; ++i) js.pvals.push_back(pp.d_vals[i]);
+        js.pn.push_back(pp.n);
+      }
+      for (int i = 0; i < a.m; ++i) js.out.push_back(a.d_out[i]);
+      int rc = table.build(device, dtype, a.m, {js});
+      if (rc) return rc;
+      rc = table.run(stream);
+      if (rc) return rc;
+      HIP_TRY(hipStreamSynchronize(stream));
+      std::vector<uint64_t> mt;
+      rc = table.matched(mt);
+      if (rc) return rc;
+      for (size_t p = 0; p < take; ++p) {
+        a.matched_total += mt[p];
+        if (mt[p] != a.pending[p].n) a.unmatched = true;
+        HIP_TRY(hipFree(a.pending[p].d_keys));
+      }
+      a.pending.erase(a.pending.begin(), a.pending.begin() + take);
+      a.folded += take;
+    }
+    return PSG_OK;
+  }
+};
+
+namespace {
+
+int set_dev(int d) {
+  HIP_TRY(hipSetDevice(d));
+  return PSG_OK;
+}
+
+}  // namespace
+
+extern "C" {
+
+int psg_abi_version(void) { return PSG_ABI_VERSION; }
+
+const char* psg_status_string(int s) {
+  switch (s) {
+    case PSG_OK: return "ok";
+    case PSG_ERR_ARG: return "invalid argument";
+    case PSG_ERR_UNMATCHED: return "pushed key not matched";
+    case PSG_ERR_RANGE: return "position range mismatch";
+    case PSG_ERR_NO_TIME: return "no data received at time";
+    case PSG_ERR_OOM: return "out of device memory";
+    case PSG_ERR_DEVICE: return "device error";
+    case PSG_ERR_UNSORTED: return "keys not strictly increasing";
+    case PSG_ERR_SIZE: return "value/key size mismatch";
+    case PSG_ERR_CHANNEL: return "channel mismatch";
+    case PSG_ERR_EMPTY_KEYS: return "channel has no server keys";
+    default: return "unknown status";
+  }
+}
+
+const char* psg_last_error(void) { return g_err.c_str(); }
+
+int psg_device_count(int* n) {
+  if (!n) return fail(PSG_ERR_ARG, "null");
+  HIP_TRY(hipGetDeviceCount(n));
+  return PSG_OK;
+}
+
+int psg_plan_max_push(void) { return psg::kMaxPush; }
+
+// ---------------------------------------------------------------- plans --
+int psg_plan_create(int device, int dtype, int m, unsigned flags,
+                    const psg_merge_job* jobs, int njobs, psg_plan** out) {
+  if (!out || (njobs > 0 && !jobs)) return fail(PSG_ERR_ARG, "null argument");
+  if (dtype != PSG_F32 && dtype != PSG_F64) return fail(PSG_ERR_ARG, "dtype %d", dtype);
+  if (m < 1 || m > PSG_MAX_VALUE_ARRAYS) return fail(PSG_ERR_ARG, "m=%d", m);
+  if (int rc = set_dev(device)) return rc;
+  std::vector<JobSpec> specs(njobs);
+  uint64_t bytes = 0, kv = 0;
+  const uint64_t sv = vsize(dtype);
+  for (int j = 0; j < njobs; ++j) {
+    const psg_merge_job& J = jobs[j];
+    if (J.npush < 0 || (J.npush > 0 && (!J.push_keys || !J.push_vals || !J.push_n)) ||
+        !J.out || (J.nslots > 0 && !J.keys))
+      return fail(PSG_ERR_ARG, "job %d: null pointer", j);
+    JobSpec& s = specs[j];
+    s.keys = J.keys;
+    s.nslots = J.nslots;
+    s.flags = (flags & PSG_PARALLEL_MATCH) ? psg::kFlagParallel : 0u;
+    for (int p = 0; p < J.npush; ++p) {
+      s.pkeys.push_back(J.push_keys[p]);
+      for (int i = 0; i < m; ++i) s.pvals.push_back(J.push_vals[(size_t)p * m + i]);
+      s.pn.push_back(J.push_n[p]);
+      bytes += J.push_n[p] * (8 + m * sv);
+      kv += J.push_n[p];
+    }
+    for (int i = 0; i < m; ++i) s.out.push_back(J.out[i]);
+    bytes += J.nslots * (8 + m * sv);
+  }
+  psg_plan* p = new psg_plan();
+  int rc = p->table.build(device, dtype, m, specs);
+  if (rc) {
+    p->table.release();
+    delete p;
+    return rc;
+  }
+  p->bytes = bytes;
+  p->kv = kv;
+  *out = p;
+  return PSG_OK;
+}
+
+int psg_plan_run(psg_plan* plan, void* stream) {
+  if (!plan) return fail(PSG_ERR_ARG, "null plan");
+  plan->last = (hipStream_t)stream;
+  return plan->table.run((hipStream_t)stream);
+}
+
+int psg_plan_run_stage(psg_plan* plan, int stage, void* stream) {
+  if (!plan || stage < 0 || stage > 1) return fail(PSG_ERR_ARG, "bad plan/stage");
+  plan->last = (hipStream_t)stream;
+  const JobTable& t = plan->table;
+  if (t.h.empty()) return PSG_OK;
+  if (stage == 0)
+    HIP_TRY(psg::launch_partition(t.d_jobs, (int)t.h.size(), t.nitems, (hipStream_t)stream));
+  else
+    HIP_TRY(psg::launch_aggregate(t.dtype, t.m, t.d_jobs, (int)t.h.size(), t.ntiles,
+                                  (hipStream_t)stream));
+  return PSG_OK;
+}
+
+int psg_plan_matched(psg_plan* plan, uint64_t* matched) {
+  if (!plan || !matched) return fail(PSG_ERR_ARG, "null argument");
+  if (int rc = set_dev(plan->table.device)) return rc;
+  HIP_TRY(hipStreamSynchronize(plan->last));
+  std::vector<uint64_t> mt;
+  if (int rc = plan->table.matched(mt)) return rc;
+  std::copy(mt.begin(), mt.end(), matched);
+  return PSG_OK;
+}
+
+int psg_plan_bytes(psg_plan* plan, uint64_t* bytes, uint64_t* kv) {
+  if (!plan) return fail(PSG_ERR_ARG, "null plan");
+  if (bytes) *bytes = plan->bytes;
+  if (kv) *kv = plan->kv;
+  return PSG_OK;
+}
+
+int psg_plan_destroy(psg_plan* plan) {
+  if (!plan) return PSG_OK;
+  (void)hipSetDevice(plan->table.device);
+  plan->table.release();
+  delete plan;
+  return PSG_OK;
+}
+
+// -------------------------------------------------------- device helpers --
+int psg_gather_dev(int dtype, const uint64_t* dkeys, uint64_t nd,
+                   const void* dvals, const uint64_t* req, uint64_t nreq,
+                   void* out, unsigned long long* matched, void* stream) {
+  if (dtype != PSG_F32 && dtype != PSG_F64) return fail(PSG_ERR_ARG, "dtype");
+  HIP_TRY(psg::launch_gather(dtype, dkeys, nd, dvals, req, nreq, out, matched,
+                             (hipStream_t)stream));
+  return PSG_OK;
+}
+
+int psg_key_union_dev(const uint64_t* a, uint64_t na, const uint64_t* b,
+                      uint64_t nb, uint64_t* out, uint64_t* nout, void* stream) {
+  if (!out || !nout || (na && !a) || (nb && !b)) return fail(PSG_ERR_ARG, "null");
+  if (nb >= (1ull << 32)) return fail(PSG_ERR_ARG, "nb >= 2^32");
+  hipStream_t s = (hipStream_t)stream;
+  void* scratch = nullptr;
+  unsigned long long* bad = nullptr;
+  const size_t sb = psg::union_scratch_bytes(nb);
+  HIP_TRY(hipMalloc(&scratch, sb + 64));
+  uint64_t* d_nout = (uint64_t*)((char*)scratch + align_up(sb, 16));
+  bad = (unsigned long long*)(d_nout + 1);
+  HIP_TRY(hipMemsetAsync(bad, 0, 16, s));
+  HIP_TRY(psg::launch_check_sorted(a, na, bad, s));
+  HIP_TRY(psg::launch_check_sorted(b, nb, bad, s));
+  HIP_TRY(psg::launch_union(a, na, b, nb, out, scratch, d_nout, s));
+  unsigned long long h[2] = {0, 0};
+  HIP_TRY(hipMemcpyAsync(h, d_nout, 16, hipMemcpyDeviceToHost, s));
+  HIP_TRY(hipStreamSynchronize(s));
+  HIP_TRY(hipFree(scratch));
+  if (h[1]) return fail(PSG_ERR_UNSORTED, "%llu order violations", h[1]);
+  *nout = h[0];
+  return PSG_OK;
+}
+
+int psg_shard_bounds(size_t n, uint64_t* bounds) {
+  if (n == 0 || !bounds) return fail(PSG_ERR_ARG, "n == 0");
+  // Range<uint64>::all() = [0, 2^64-1)  (range.h:75-78); evenDivide (:85-98)
+  const uint64_t b = 0, e = ~0ull;
+  const long double itv = (long double)(e - b) / (long double)n;
+  for (size_t i = 0; i < n; ++i) bounds[i] = (uint64_t)(b + itv * (long double)i);
+  bounds[n] = e;
+  return PSG_OK;
+}
+
+int psg_slice_dev(const uint64_t* keys, uint64_t n, uint64_t kb, uint64_t ke,
+                  const uint64_t* sep, int nsep, uint64_t* pos, void* stream) {
+  if (nsep < 0 || (nsep > 0 && (!sep || !pos))) return fail(PSG_ERR_ARG, "null");
+  HIP_TRY(psg::launch_slice(keys, n, kb, ke, sep, nsep, pos, (hipStream_t)stream));
+  return PSG_OK;
+}
+
+// --------------------------------------------------------------- context --
+int psg_create(int device, int dtype, unsigned flags, psg_ctx** out) {
+  if (!out) return fail(PSG_ERR_ARG, "null out");
+  if (dtype != PSG_F32 && dtype != PSG_F64) return fail(PSG_ERR_ARG, "dtype %d", dtype);
+  if (int rc = set_dev(device)) return rc;
+  psg_ctx* c = new psg_ctx();
+  c->device = device;
+  c->dtype = dtype;
+  c->flags = flags;
+  hipError_t e = hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking);
+  if (e == hipSuccess) e = hipMalloc((void**)&c->d_counter, 64);
+  if (e != hipSuccess) {
+    delete c;
+    return fail(PSG_ERR_DEVICE, "psg_create: %s", hipGetErrorString(e));
+  }
+  *out = c;
+  return PSG_OK;
+}
+
+int psg_destroy(psg_ctx* c) {
+  if (!c) return PSG_OK;
+  (void)hipSetDevice(c->device);
+  (void)hipStreamSynchronize(c->stream);
+  for (auto& kv : c->agg) {
+    for (auto& pp : kv.second.pending) (void)hipFree(pp.d_keys);
+    for (int i = 0; i < kv.second.m; ++i) (void)hipFree(kv.second.d_out[i]);
+  }
+  for (auto& kv : c->ch) {
+    (void)hipFree(kv.second.d_keys);
+    (void)hipFree(kv.second.d_vals);
+  }
+  c->table.release();
+  (void)hipFree(c->d_counter);
+  (void)hipFree(c->scratch);
+  (void)hipStreamDestroy(c->stream);
+  delete c;
+  return PSG_OK;
+}
+
+int psg_set_match_flags(psg_ctx* c, unsigned flags) {
+  if (!c) return fail(PSG_ERR_ARG, "null ctx");
+  std::lock_guard<std::mutex> l(c->mu);
+  c->flags = flags;
+  return PSG_OK;
+}
+
+int psg_key_union(psg_ctx* c, int chl, const uint64_t* keys, size_t n) {
+  if (!c || (n && !keys)) return fail(PSG_ERR_ARG, "null argument");
+  std::lock_guard<std::mutex> l(c->mu);
+  if (n == 0) return PSG_OK;  // kv_vector.h:177: empty key list is ignored
+  if (int rc = set_dev(c->device)) return rc;
+  Channel& C = c->ch[chl];
+  const size_t sb = psg::union_scratch_bytes(n);
+  if (int rc = c->ensure_scratch(align_up(sb, 256) + 8 * n)) return rc;
+  uint64_t* d_new = (uint64_t*)((char*)c->scratch + align_up(sb, 256));
+  HIP_TRY(hipMemcpyAsync(d_new, keys, 8 * n, hipMemcpyHostToDevice, c->stream));
+  HIP_TRY(hipMemsetAsync(c->d_counter, 0, 16, c->stream));
+  HIP_TRY(psg::launch_check_sorted(d_new, n, c->d_counter, c->stream));
+  uint64_t* d_out = nullptr;
+  HIP_TRY(hipMalloc(&d_out, 8 * (C.n + n)));
+  HIP_TRY(psg::launch_union(C.d_keys, C.n, d_new, n, d_out, c->scratch,
+                            (uint64_t*)(c->d_counter + 1), c->stream));
+  unsigned long long h[2];
+  HIP_TRY(hipMemcpyAsync(h, c->d_counter, 16, hipMemcpyDeviceToHost, c->stream));
+  HIP_TRY(hipStreamSynchronize(c->stream));
+  if (h[0]) {
+    (void)hipFree(d_out);
+    return fail(PSG_ERR_UNSORTED, "key-only push: %llu order violations", h[0]);
+  }
+  HIP_TRY(hipFree(C.d_keys));
+  C.d_keys = d_out;
+  C.n = (size_t)h[1];
+  C.cap = C.n;
+  C.h_keys.resize(C.n);
+  HIP_TRY(hipMemcpy(C.h_keys.data(), C.d_keys, 8 * C.n, hipMemcpyDeviceToHost));
+  // val_[chl].clear()  (kv_vector.h:180)
+  HIP_TRY(hipFree(C.d_vals));
+  C.d_vals = nullptr;
+  C.nvals = 0;
+  return PSG_OK;
+}
+
+int psg_key_size(psg_ctx* c, int chl, size_t* n) {
+  if (!c || !n) return fail(PSG_ERR_ARG, "null argument");
+  std::lock_guard<std::mutex> l(c->mu);
+  auto it = c->ch.find(chl);
+  *n = it == c->ch.end() ? 0 : it->second.n;
+  return PSG_OK;
+}
+
+int psg_key_copy(psg_ctx* c, int chl, size_t off, size_t n, uint64_t* out) {
+  if (!c || (n && !out)) return fail(PSG_ERR_ARG, "null argument");
+  std::lock_guard<std::mutex> l(c->mu);
+  auto it = c->ch.find(chl);
+  const size_t have = it == c->ch.end() ? 0 : it->second.n;
+  if (off + n > have) return fail(PSG_ERR_ARG, "key copy out of range");
+  if (n) memcpy(out, it->second.h_keys.data() + off, 8 * n);
+  return PSG_OK;
+}
+
+int psg_find_range(psg_ctx* c, int chl, uint64_t kb, uint64_t ke, size_t* lo,
+                   size_t* hi) {
+  if (!c || !lo || !hi) return fail(PSG_ERR_ARG, "null argument");
+  if (ke < kb) return fail(PSG_ERR_ARG, "invalid key range");  // CHECK(bound.valid())
+  std::lock_guard<std::mutex> l(c->mu);
+  auto it = c->ch.find(chl);
+  if (it == c->ch.end() || it->second.n == 0) {
+    *lo = *hi = 0;
+    return PSG_OK;
+  }
+  const auto& k = it->second.h_keys;
+  *lo = std::lower_bound(k.begin(), k.end(), kb) - k.begin();
+  *hi = std::lower_bound(k.begin(), k.end(), ke) - k.begin();
+  return PSG_OK;
+}
+
+int psg_value_assign(psg_ctx* c, int chl, const void* vals, size_t n) {
+  if (!c || (n && !vals)) return fail(PSG_ERR_ARG, "null argument");
+  std::lock_guard<std::mutex> l(c->mu);
+  if (int rc = set_dev(c->device)) return rc;
+  Channel& C = c->ch[chl];
+  const size_t b = n * vsize(c->dtype);
+  if (n != C.nvals) {
+    HIP_TRY(hipFree(C.d_vals));
+    C.d_vals = nullptr;
+    if (n) HIP_TRY(hipMalloc(&C.d_vals, b));
+    C.nvals = n;
+  }
+  if (n) HIP_TRY(hipMemcpyAsync(C.d_vals, vals, b, hipMemcpyHostToDevice, c->stream));
+  HIP_TRY(hipStreamSynchronize(c->stream));
+  return PSG_OK;
+}
+
+int psg_value_size(psg_ctx* c, int chl, size_t* n) {
+  if (!c || !n) return fail(PSG_ERR_ARG, "null argument");
+  std::lock_guard<std::mutex> l(c->mu);
+  auto it = c->ch.find(chl);
+  *n = it == c->ch.end() ? 0 : it->second.nvals;
+  return PSG_OK;
+}
+
+int psg_value_copy(psg_ctx* c, int chl, size_t off, size_t n, void* out) {
+  if (!c || (n && !out)) return fail(PSG_ERR_ARG, "null argument");
+  std::lock_guard<std::mutex> l(c->mu);
+  auto it = c->ch.find(chl);
+  const size_t have = it == c->ch.end() ? 0 : it->second.nvals;
+  if (off + n > have) return fail(PSG_ERR_ARG, "value copy out of range");
+  if (int rc = set_dev(c->device)) return rc;
+  const size_t sv = vsize(c->dtype);
+  if (n)
+    HIP_TRY(hipMemcpy(out, (char*)it->second.d_vals + off * sv, n * sv,
+                      hipMemcpyDeviceToHost));
+  return PSG_OK;
+}
+
+int psg_push(psg_ctx* c, int chl, int time, uint64_t kb, uint64_t ke,
+             const uint64_t* keys, size_t n, int m, const void* const* vals) {
+  if (!c) return fail(PSG_ERR_ARG, "null ctx");
+  if (n == 0) return PSG_OK;  // kv_vector.h:90,177 -- empty push ignored
+  if (!keys || !vals) return fail(PSG_ERR_ARG, "null keys/values");
+  if (m < 1 || m > PSG_MAX_VALUE_ARRAYS) return fail(PSG_ERR_ARG, "m=%d", m);
+  for (int i = 0; i < m; ++i)
+    if (!vals[i]) return fail(PSG_ERR_ARG, "null value array %d", i);
+  if (ke < kb) return fail(PSG_ERR_ARG, "invalid key range");
+  std::lock_guard<std::mutex> l(c->mu);
+  if (int rc = set_dev(c->device)) return rc;
+  auto cit = c->ch.find(chl);
+  if (cit == c->ch.end() || cit->second.n == 0)
+    return fail(PSG_ERR_EMPTY_KEYS, "channel %d has no server keys", chl);
+  Channel& C = cit->second;
+  const size_t lo = std::lower_bound(C.h_keys.begin(), C.h_keys.end(), kb) - C.h_keys.begin();
+  const size_t hi = std::lower_bound(C.h_keys.begin(), C.h_keys.end(), ke) - C.h_keys.begin();
+  if (hi - lo < n)  // pigeonhole: some key cannot match (CHECK_GE, kv_vector.h:121,191)
+    return fail(PSG_ERR_UNMATCHED, "push of %zu keys into a range of %zu server keys",
+                n, hi - lo);
+  auto ait = c->agg.find(time);
+  if (ait != c->agg.end()) {
+    Aggregate& A = ait->second;
+    if (A.chl != chl) return fail(PSG_ERR_CHANNEL, "time %d: channel %d != %d", time, chl, A.chl);
+    if (A.lo != lo || A.hi != hi)  // CHECK_EQ(aligned.first, stored) kv_vector.h:199
+      return fail(PSG_ERR_RANGE, "time %d: range [%zu,%zu) != [%zu,%zu)", time, lo, hi,
+                  A.lo, A.hi);
+    if (A.m != m) return fail(PSG_ERR_ARG, "time %d: %d value arrays != %d", time, m, A.m);
+  }
+  const size_t sv = vsize(c->dtype);
+  PendingPush pp;
+  pp.n = n;
+  const size_t kbytes = align_up(8 * n, 256), vbytes = align_up(sv * n, 256);
+  HIP_TRY(hipMalloc(&pp.d_keys, kbytes + m * vbytes));
+  HIP_TRY(hipMemcpyAsync(pp.d_keys, keys, 8 * n, hipMemcpyHostToDevice, c->stream));
+  for (int i = 0; i < m; ++i) {
+    pp.d_vals[i] = (char*)pp.d_keys + kbytes + i * vbytes;
+    HIP_TRY(hipMemcpyAsync(pp.d_vals[i], vals[i], sv * n, hipMemcpyHostToDevice, c->stream));
+  }
+  // the caller's buffers are free after return
+  HIP_TRY(hipStreamSynchronize(c->stream));
+  if (ait == c->agg.end()) {
+    Aggregate A;
+    A.chl = chl;
+    A.m = m;
+    A.lo = lo;
+    A.hi = hi;
+    for (int i = 0; i < m; ++i)
+      if (hi > lo) HIP_TRY(hipMalloc(&A.d_out[i], (hi - lo) * sv));
+    ait = c->agg.emplace(time, A).first;
+  }
+  Aggregate& A = ait->second;
+  A.pending.push_back(pp);
+  A.expected_total += n;
+  if (A.pending.size() >= (size_t)psg::kMaxPush) return c->flush(A);
+  return PSG_OK;
+}
+
+int psg_received_shape(psg_ctx* c, int time, int* m, size_t* lo, size_t* hi) {
+  if (!c) return fail(PSG_ERR_ARG, "null ctx");
+  std::lock_guard<std::mutex> l(c->mu);
+  auto it = c->agg.find(time);
+  if (it == c->agg.end()) return fail(PSG_ERR_NO_TIME, "no data received at time %d", time);
+  if (m) *m = it->second.m;
+  if (lo) *lo = it->second.lo;
+  if (hi) *hi = it->second.hi;
+  return PSG_OK;
+}
+
+int psg_received(psg_ctx* c, int time, int m, void* const* out) {
+  if (!c) return fail(PSG_ERR_ARG, "null ctx");
+  std::lock_guard<std::mutex> l(c->mu);
+  auto it = c->agg.find(time);
+  if (it == c->agg.end()) return fail(PSG_ERR_NO_TIME, "no data received at time %d", time);
+  if (int rc = set_dev(c->device)) return rc;
+  Aggregate& A = it->second;
+  if (m != A.m || !out) return fail(PSG_ERR_ARG, "expected %d output arrays", A.m);
+  int rc = c->flush(A);
+  const size_t len = A.hi - A.lo, sv = vsize(c->dtype);
+  if (rc == PSG_OK) {
+    for (int i = 0; i < A.m && len; ++i) {
+      hipError_t e = hipMemcpy(out[i], A.d_out[i], len * sv, hipMemcpyDeviceToHost);
+      if (e != hipSuccess) {
+        rc = fail(PSG_ERR_DEVICE, "D2H: %s", hipGetErrorString(e));
+        break;
+      }
+    }
+  }
+  const bool bad = A.unmatched;
+  const unsigned long long got = A.matched_total, want = A.expected_total;
+  for (auto& pp : A.pending) (void)hipFree(pp.d_keys);
+  for (int i = 0; i < A.m; ++i) (void)hipFree(A.d_out[i]);
+  c->agg.erase(it);
+  if (rc) return rc;
+  if (bad)
+    return fail(PSG_ERR_UNMATCHED, "time %d: matched %llu of %llu pushed keys", time, got, want);
+  return PSG_OK;
+}
+
+int psg_gather(psg_ctx* c, int chl, const uint64_t* keys, size_t n, void* out,
+               size_t* matched) {
+  if (!c || (n && (!keys || !out))) return fail(PSG_ERR_ARG, "null argument");
+  std::lock_guard<std::mutex> l(c->mu);
+  if (matched) *matched = 0;
+  if (n == 0) return PSG_OK;  // kv_vector.h:218
+  if (int rc = set_dev(c->device)) return rc;
+  Channel& C = c->ch[chl];
+  if (C.n != C.nvals)  // CHECK_EQ(key_[ch].size(), val_[ch].size()) kv_vector.h:220
+    return fail(PSG_ERR_SIZE, "channel %d: %zu keys but %zu values", chl, C.n, C.nvals);
+  const size_t sv = vsize(c->dtype);
+  if (int rc = c->ensure_scratch(align_up(8 * n, 256) + n * sv)) return rc;
+  uint64_t* d_req = (uint64_t*)c->scratch;
+  void* d_out = (char*)c->scratch + align_up(8 * n, 256);
+  HIP_TRY(hipMemcpyAsync(d_req, keys, 8 * n, hipMemcpyHostToDevice, c->stream));
+  HIP_TRY(hipMemsetAsync(c->d_counter, 0, 8, c->stream));
+  HIP_TRY(psg::launch_gather(c->dtype, C.d_keys, C.n, C.d_vals, d_req, n, d_out,
+                             c->d_counter, c->stream));
+  unsigned long long mt = 0;
+  HIP_TRY(hipMemcpyAsync(out, d_out, n * sv, hipMemcpyDeviceToHost, c->stream));
+  HIP_TRY(hipMemcpyAsync(&mt, c->d_counter, 8, hipMemcpyDeviceToHost, c->stream));
+  HIP_TRY(hipStreamSynchronize(c->stream));
+  if (matched) *matched = (size_t)mt;
+  return PSG_OK;
+}
+
+}  // extern "C"

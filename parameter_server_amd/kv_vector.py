@@ -1,0 +1,220 @@
+"""Python mirror of the reference's server-side KV surface over the C ABI.
+
+``KVVector`` follows ``PS::KVVector<Key,V>`` (reference
+src/parameter/kv_vector.h:13-62) method for method -- ``key``, ``value``,
+``find``, ``received``, ``setValue``, ``getValue`` -- with the message
+fields of ``PS::Message``/``Task`` that the path reads
+(src/system/message.h:17-87, src/proto/task.proto:12-62).  Every call goes
+to libpsg.so; a failing reference ``CHECK`` surfaces as :class:`PSGError`.
+
+``MergePlan`` is the device-resident batched form used by bench.py and the
+multi-GPU shards: every buffer is a device pointer (e.g. a torch tensor's
+``data_ptr()``), and a run is two kernel launches on a caller stream.
+"""
+from __future__ import annotations
+
+import ctypes as C
+from dataclasses import dataclass, field
+from typing import List, Optional, Sequence
+
+import numpy as np
+
+from . import _lib
+from ._lib import PSG_F32, PSG_F64, PSG_PARALLEL_MATCH, PSG_SERIAL_MATCH
+
+KEY_ALL = (0, (1 << 64) - 1)  # Range<uint64>::all() (range.h:75-78)
+
+
+def _np_dtype(dtype: int):
+    return np.float32 if dtype == PSG_F32 else np.float64
+
+
+def _ptr(a: np.ndarray) -> int:
+    return a.ctypes.data
+
+
+@dataclass
+class Message:
+    """The fields of PS::Message / Task the aggregation path reads."""
+
+    time: int = 0
+    key_channel: int = 0
+    key_range: tuple = KEY_ALL
+    push: bool = True
+    request: bool = True
+    key: np.ndarray = field(default_factory=lambda: np.zeros(0, np.uint64))
+    value: List[np.ndarray] = field(default_factory=list)
+
+
+class KVVector:
+    """KVVector<uint64, V> with keys, values and aggregates resident in HBM."""
+
+    def __init__(self, device: int = 0, dtype: int = PSG_F32,
+                 parallel_match: bool = False):
+        self._L = _lib.lib()
+        self.dtype = dtype
+        self.np_dtype = _np_dtype(dtype)
+        h = C.c_void_p()
+        flags = PSG_PARALLEL_MATCH if parallel_match else PSG_SERIAL_MATCH
+        _lib.check(self._L.psg_create(device, dtype, flags, C.byref(h)))
+        self._h = h
+
+    def close(self):
+        if getattr(self, "_h", None):
+            self._L.psg_destroy(self._h)
+            self._h = None
+
+    def __del__(self):  # pragma: no cover
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    def set_parallel_match(self, on: bool):
+        """FLAGS_parallel_match (system/postoffice.cc:24)."""
+        _lib.check(self._L.psg_set_match_flags(
+            self._h, PSG_PARALLEL_MATCH if on else PSG_SERIAL_MATCH))
+
+    # -- key(ch) / value(ch) / find(ch, range): kv_vector.h:17-23 ---------
+    def key(self, channel: int) -> np.ndarray:
+        n = C.c_size_t()
+        _lib.check(self._L.psg_key_size(self._h, channel, C.byref(n)))
+        out = np.empty(n.value, np.uint64)
+        _lib.check(self._L.psg_key_copy(self._h, channel, 0, n.value, _ptr(out)))
+        return out
+
+    def value(self, channel: int) -> np.ndarray:
+        n = C.c_size_t()
+        _lib.check(self._L.psg_value_size(self._h, channel, C.byref(n)))
+        out = np.empty(n.value, self.np_dtype)
+        _lib.check(self._L.psg_value_copy(self._h, channel, 0, n.value, _ptr(out)))
+        return out
+
+    def set_value_array(self, channel: int, vals) -> None:
+        """Assign value(channel) (the app side writes it, e.g. Darling
+        updateWeight, darling.cc:437-477)."""
+        v = np.ascontiguousarray(vals, dtype=self.np_dtype)
+        _lib.check(self._L.psg_value_assign(self._h, channel, _ptr(v), v.size))
+
+    def find(self, channel: int, key_range) -> tuple:
+        lo, hi = C.c_size_t(), C.c_size_t()
+        _lib.check(self._L.psg_find_range(self._h, channel, int(key_range[0]),
+                                          int(key_range[1]), C.byref(lo),
+                                          C.byref(hi)))
+        return lo.value, hi.value
+
+    # -- setValue: kv_vector.h:75-82 ---------------------------------------
+    def setValue(self, msg: Message) -> None:
+        keys = np.ascontiguousarray(msg.key, dtype=np.uint64)
+        if keys.size == 0:
+            return
+        if not msg.value:  # key-only push: key_ = key_.setUnion(recv) (:177-182)
+            _lib.check(self._L.psg_key_union(self._h, msg.key_channel, _ptr(keys),
+                                             keys.size))
+            return
+        vals = []
+        for v in msg.value:
+            a = np.ascontiguousarray(v, dtype=self.np_dtype)
+            if a.size != keys.size:  # CHECK_EQ(recv_data.size(), recv_key.size())
+                raise _lib.PSGError(_lib.PSG_ERR_SIZE,
+                                    f"{a.size} values for {keys.size} keys")
+            vals.append(a)
+        arr = _lib.ptr_array([_ptr(a) for a in vals])
+        _lib.check(self._L.psg_push(self._h, msg.key_channel, msg.time,
+                                    int(msg.key_range[0]), int(msg.key_range[1]),
+                                    _ptr(keys), keys.size, len(vals), arr))
+
+    # -- received(t): kv_vector.h:65-73 ------------------------------------
+    def received(self, t: int):
+        """Returns [((lo, hi), values_i) for each value array], then erases t."""
+        m, lo, hi = C.c_int(), C.c_size_t(), C.c_size_t()
+        _lib.check(self._L.psg_received_shape(self._h, t, C.byref(m), C.byref(lo),
+                                              C.byref(hi)))
+        outs = [np.empty(hi.value - lo.value, self.np_dtype) for _ in range(m.value)]
+        arr = _lib.ptr_array([_ptr(o) for o in outs])
+        _lib.check(self._L.psg_received(self._h, t, m.value, arr))
+        return [((lo.value, hi.value), o) for o in outs]
+
+    # -- getValue (pull request): kv_vector.h:206-227 ----------------------
+    def getValue(self, msg: Message) -> int:
+        """Fills msg.value with value(channel) gathered at msg.key; returns
+        the matched count."""
+        keys = np.ascontiguousarray(msg.key, dtype=np.uint64)
+        if keys.size == 0:
+            return 0
+        out = np.empty(keys.size, self.np_dtype)
+        matched = C.c_size_t()
+        _lib.check(self._L.psg_gather(self._h, msg.key_channel, _ptr(keys), keys.size,
+                                      _ptr(out), C.byref(matched)))
+        msg.value.append(out)
+        return matched.value
+
+
+class MergePlan:
+    """A prepared device-resident batch of (channel, time) merges.
+
+    jobs: list of dicts with device pointers
+        {"keys": int, "nslots": int, "push_keys": [int], "push_vals": [[int]*m],
+         "push_n": [int], "out": [int]*m}
+    """
+
+    def __init__(self, device: int, dtype: int, m: int, jobs: Sequence[dict],
+                 parallel_match: bool = False):
+        self._L = _lib.lib()
+        self._keep = []
+        cj = (_lib.MergeJob * max(1, len(jobs)))()
+        for j, J in enumerate(jobs):
+            npush = len(J["push_keys"])
+            pk = _lib.ptr_array(J["push_keys"])
+            pv = _lib.ptr_array([v for vs in J["push_vals"] for v in vs])
+            pn = (C.c_uint64 * max(1, npush))(*J["push_n"])
+            out = _lib.ptr_array(J["out"])
+            self._keep += [pk, pv, pn, out]
+            cj[j].keys = J["keys"]
+            cj[j].nslots = J["nslots"]
+            cj[j].npush = npush
+            cj[j].push_keys = C.cast(pk, C.POINTER(C.c_void_p))
+            cj[j].push_vals = C.cast(pv, C.POINTER(C.c_void_p))
+            cj[j].push_n = C.cast(pn, C.POINTER(C.c_uint64))
+            cj[j].out = C.cast(out, C.POINTER(C.c_void_p))
+        h = C.c_void_p()
+        flags = PSG_PARALLEL_MATCH if parallel_match else PSG_SERIAL_MATCH
+        _lib.check(self._L.psg_plan_create(device, dtype, m, flags, cj, len(jobs),
+                                           C.byref(h)))
+        self._h = h
+        self.npush_total = sum(len(J["push_keys"]) for J in jobs)
+        b, kv = C.c_uint64(), C.c_uint64()
+        _lib.check(self._L.psg_plan_bytes(h, C.byref(b), C.byref(kv)))
+        self.bytes, self.kv_pairs = b.value, kv.value
+
+    def run(self, stream: Optional[int] = None) -> None:
+        _lib.check(self._L.psg_plan_run(self._h, stream or None))
+
+    def run_stage(self, stage: int, stream: Optional[int] = None) -> None:
+        """0 = partition, 1 = aggregate (the dominant kernel)."""
+        _lib.check(self._L.psg_plan_run_stage(self._h, stage, stream or None))
+
+    def matched(self) -> np.ndarray:
+        out = np.zeros(max(1, self.npush_total), np.uint64)
+        _lib.check(self._L.psg_plan_matched(
+            self._h, out.ctypes.data_as(C.POINTER(C.c_uint64))))
+        return out[: self.npush_total]
+
+    def close(self):
+        if getattr(self, "_h", None):
+            self._L.psg_plan_destroy(self._h)
+            self._h = None
+
+    def __del__(self):  # pragma: no cover
+        try:
+            self.close()
+        except Exception:
+            pass
+
+
+def shard_bounds(n: int) -> np.ndarray:
+    """Range<uint64>::all().evenDivide(n, i) boundaries (range.h:85-98)."""
+    L = _lib.lib()
+    out = np.zeros(n + 1, np.uint64)
+    _lib.check(L.psg_shard_bounds(n, out.ctypes.data_as(C.POINTER(C.c_uint64))))
+    return out
