@@ -8,43 +8,58 @@
 namespace psg {
 
 // ---- aggregate kernel geometry (see DESIGN.md "Kernels") ----
-constexpr int kTile = 2048;                 // server slots per workgroup tile
-constexpr int kThreads = 512;               // 8 waves of 64
-constexpr int kSPT = kTile / kThreads;      // slots owned per thread (4)
-constexpr int kEPT = 8;                     // push elements per thread per chunk
-constexpr int kChunk = kThreads * kEPT;     // 4096 elements staged per chunk
-constexpr int kGroup = 64;                  // pushes per chunk (one mask bit each)
-constexpr int kMaxPush = 512;               // pushes per job per launch
-constexpr int kMaxM = 4;                    // value arrays per push
+constexpr int kEPT = 8;          // push elements per thread per chunk
+constexpr int kGroup = 64;       // pushes per chunk (one mask bit each)
+constexpr int kMaxPush = 4096;   // pushes per job per launch
+constexpr int kMaxM = 4;         // value arrays per push
 
-constexpr uint32_t kFlagParallel = 1u;      // PSG_PARALLEL_MATCH
-constexpr uint32_t kFlagCont = 2u;          // continue an aggregate of an earlier launch
+// Tile geometries: server slots per workgroup tile / threads per workgroup
+// (4 slots per thread in every geometry).
+enum Geometry { kGeoS = 0, kGeoM = 1, kGeoL = 2, kNumGeo = 3 };
+constexpr int geo_tile(int g) { return g == kGeoS ? 512 : g == kGeoM ? 1024 : 2048; }
+constexpr int geo_threads(int g) { return geo_tile(g) / 4; }
 
-// One (channel, time) aggregate as the kernels see it.  All pointers are
-// device pointers.  seg[b*npush + p] = first index of push p whose key is
-// >= D[b*kTile] (b < ntiles) or > D[nslots-1] (b == ntiles).
+constexpr uint32_t kFlagParallel = 1u;  // PSG_PARALLEL_MATCH
+constexpr uint32_t kFlagCont = 2u;      // continue an aggregate of an earlier launch
+
+// One (channel, time) aggregate as the partition kernel sees it.  All
+// pointers are device pointers.  seg[b*npush + p] = first index of push p
+// whose key is >= D[b*tile] (b < ntiles) or > D[nslots-1] (b == ntiles).
 struct JobDev {
   const uint64_t* dkeys;          // D + lo
   uint64_t nslots;                // hi - lo
   const uint64_t* const* pkeys;   // [npush]
-  const void* const* pvals;       // [npush * m]
   const uint64_t* pn;             // [npush]
-  void* const* out;               // [m]
   uint32_t* seg;                  // [(ntiles + 1) * npush]
   unsigned long long* fail;       // [npush] in-tile match failures
   uint32_t npush;
   uint32_t ntiles;
-  uint32_t tile_begin;            // first global tile (blockIdx.x) of this job
   uint32_t part_begin;            // first global partition item of this job
+  uint32_t tile;                  // slots per tile
+};
+
+// One workgroup tile of the aggregate kernel: everything it needs is one
+// scalar-load round trip away.
+struct TileDesc {
+  const uint64_t* dk;             // D + lo + slot0
+  const uint32_t* seg;            // &job.seg[t * npush]; row t+1 follows
+  const uint64_t* const* pkeys;   // job push key pointers [npush]
+  const void* const* pvals;       // job push value pointers [npush * m]
+  void* const* out;               // job output pointers [m]
+  unsigned long long* fail;       // job fail counters [npush]
+  uint64_t slot0;                 // first slot of the tile in the job
+  uint32_t nt;                    // slots in this tile (<= tile)
+  uint32_t np;                    // pushes of the job
   uint32_t flags;
   uint32_t pad;
 };
 
 // Kernel launchers (psg_kernels.hip).  All enqueue on `stream` only.
-hipError_t launch_partition(const JobDev* d_jobs, int njobs, uint32_t nitems,
-                            hipStream_t stream);
-hipError_t launch_aggregate(int dtype, int m, const JobDev* d_jobs, int njobs,
-                            uint32_t ntiles, hipStream_t stream);
+hipError_t launch_partition(const JobDev* d_jobs, const uint32_t* d_item_job,
+                            uint32_t nitems, hipStream_t stream);
+size_t aggregate_lds_bytes(int geo, int dtype, int m, uint32_t maxnp);
+hipError_t launch_aggregate(int dtype, int m, int geo, const TileDesc* d_tiles,
+                            uint32_t ntiles, uint32_t maxnp, hipStream_t stream);
 hipError_t launch_gather(int dtype, const uint64_t* dkeys, uint64_t nd,
                          const void* dvals, const uint64_t* req, uint64_t nreq,
                          void* out, unsigned long long* matched,

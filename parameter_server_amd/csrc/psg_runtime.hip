@@ -12,6 +12,7 @@
 #include <algorithm>
 #include <cstdarg>
 #include <cstdio>
+#include <cstdlib>
 #include <cstring>
 #include <map>
 #include <mutex>
@@ -67,14 +68,19 @@ struct JobSpec {
 
 struct JobTable {
   int device = -1;
-  int dtype = 0, m = 1;
+  int dtype = 0, m = 1, geo = psg::kGeoM;
   std::vector<JobDev> h;
-  std::vector<std::vector<uint64_t>> pn;
   std::vector<uint64_t> nslots;
-  uint32_t ntiles = 0, nitems = 0;
+  std::vector<uint32_t*> seg_first;  // device row 0 of each job's seg
+  std::vector<uint32_t*> seg_last;   // device row ntiles
+  std::vector<unsigned long long*> fails;
+  std::vector<uint32_t> npush;
+  uint32_t ntiles = 0, nitems = 0, maxnp = 0;
   void* blob = nullptr;
   size_t blob_bytes = 0;
   JobDev* d_jobs = nullptr;
+  psg::TileDesc* d_tiles = nullptr;
+  uint32_t* d_item_job = nullptr;
   std::vector<char> host_img;
 
   void release() {
@@ -83,29 +89,56 @@ struct JobTable {
     blob_bytes = 0;
   }
 
-  // Builds (or rebuilds, reusing the allocation when it fits) the device image.
+  static int pick_geometry() {
+    const char* g = getenv("PSG_GEOMETRY");  // S / M / L (benchmarking aid)
+    if (g && (g[0] == 'S' || g[0] == 's')) return psg::kGeoS;
+    if (g && (g[0] == 'L' || g[0] == 'l')) return psg::kGeoL;
+    if (g && (g[0] == 'M' || g[0] == 'm')) return psg::kGeoM;
+    return psg::kGeoM;
+  }
+
+  // Builds (or rebuilds, reusing the allocation when it fits) the device image:
+  // [JobDev x njobs][TileDesc x ntiles][item->job x nitems] then per job:
+  // pkeys, pvals, pn, out, fail, seg.
   int build(int dev, int dt, int mm, const std::vector<JobSpec>& jobs) {
     device = dev;
     dtype = dt;
     m = mm;
+    geo = pick_geometry();
+    const uint32_t tile = (uint32_t)psg::geo_tile(geo);
     h.clear();
-    pn.clear();
     nslots.clear();
-    ntiles = nitems = 0;
-    // layout: [JobDev x njobs] then per job: pkeys, pvals, pn, out, fail, seg
-    size_t off = align_up(sizeof(JobDev) * jobs.size(), 256);
+    seg_first.clear();
+    seg_last.clear();
+    fails.clear();
+    npush.clear();
+    ntiles = nitems = maxnp = 0;
     struct Offs { size_t pk, pv, pn, out, fail, seg; };
     std::vector<Offs> offs(jobs.size());
     uint64_t tiles = 0, items = 0;
     for (size_t j = 0; j < jobs.size(); ++j) {
       const JobSpec& s = jobs[j];
       const size_t np = s.pn.size();
-      const uint64_t nt = (s.nslots + psg::kTile - 1) / psg::kTile;
       if (np > (size_t)psg::kMaxPush)
         return fail(PSG_ERR_ARG, "job %zu: %zu pushes > max %d", j, np, psg::kMaxPush);
       for (size_t p = 0; p < np; ++p)
         if (s.pn[p] >= (1ull << 32))
           return fail(PSG_ERR_ARG, "push of %llu keys >= 2^32", (unsigned long long)s.pn[p]);
+      const uint64_t nt = (s.nslots + tile - 1) / tile;
+      tiles += nt;
+      items += (nt + 1) * np;
+      if (tiles >= (1ull << 31) || items >= (1ull << 31))
+        return fail(PSG_ERR_ARG, "batch too large (%llu tiles)", (unsigned long long)tiles);
+      maxnp = std::max(maxnp, (uint32_t)np);
+    }
+    size_t off = align_up(sizeof(JobDev) * jobs.size(), 256);
+    const size_t tiles_off = off;
+    off = align_up(off + sizeof(psg::TileDesc) * tiles, 256);
+    const size_t items_off = off;
+    off = align_up(off + 4 * items, 256);
+    for (size_t j = 0; j < jobs.size(); ++j) {
+      const size_t np = jobs[j].pn.size();
+      const uint64_t nt = (jobs[j].nslots + tile - 1) / tile;
       Offs& o = offs[j];
       o.pk = off; off = align_up(off + 8 * np, 64);
       o.pv = off; off = align_up(off + 8 * np * m, 64);
@@ -113,24 +146,7 @@ struct JobTable {
       o.out = off; off = align_up(off + 8 * m, 64);
       o.fail = off; off = align_up(off + 8 * np, 64);
       o.seg = off; off = align_up(off + 4 * (nt + 1) * np, 256);
-      JobDev d{};
-      d.nslots = s.nslots;
-      d.dkeys = s.keys;
-      d.npush = (uint32_t)np;
-      d.ntiles = (uint32_t)nt;
-      d.tile_begin = (uint32_t)tiles;
-      d.part_begin = (uint32_t)items;
-      d.flags = s.flags;
-      tiles += nt;
-      items += (nt + 1) * np;
-      if (tiles >= (1ull << 31) || items >= (1ull << 31))
-        return fail(PSG_ERR_ARG, "batch too large (%llu tiles)", (unsigned long long)tiles);
-      h.push_back(d);
-      pn.push_back(s.pn);
-      nslots.push_back(s.nslots);
     }
-    ntiles = (uint32_t)tiles;
-    nitems = (uint32_t)items;
     if (off > blob_bytes) {
       release();
       HIP_TRY(hipMalloc(&blob, off));
@@ -138,48 +154,85 @@ struct JobTable {
     }
     char* base = (char*)blob;
     host_img.assign(off, 0);
+    psg::TileDesc* htiles = (psg::TileDesc*)&host_img[tiles_off];
+    uint32_t* hitems = (uint32_t*)&host_img[items_off];
+    uint32_t tcur = 0, icur = 0;
     for (size_t j = 0; j < jobs.size(); ++j) {
       const JobSpec& s = jobs[j];
       const Offs& o = offs[j];
-      const size_t np = s.pn.size();
+      const uint32_t np = (uint32_t)s.pn.size();
+      const uint64_t nt = (s.nslots + tile - 1) / tile;
       memcpy(&host_img[o.pk], s.pkeys.data(), 8 * np);
       memcpy(&host_img[o.pv], s.pvals.data(), 8 * np * m);
       memcpy(&host_img[o.pn], s.pn.data(), 8 * np);
       memcpy(&host_img[o.out], s.out.data(), 8 * m);
-      JobDev& d = h[j];
+      JobDev d{};
+      d.dkeys = s.keys;
+      d.nslots = s.nslots;
       d.pkeys = (const uint64_t* const*)(base + o.pk);
-      d.pvals = (const void* const*)(base + o.pv);
       d.pn = (const uint64_t*)(base + o.pn);
-      d.out = (void* const*)(base + o.out);
-      d.fail = (unsigned long long*)(base + o.fail);
       d.seg = (uint32_t*)(base + o.seg);
+      d.fail = (unsigned long long*)(base + o.fail);
+      d.npush = np;
+      d.ntiles = (uint32_t)nt;
+      d.part_begin = icur;
+      d.tile = tile;
+      h.push_back(d);
+      for (uint64_t b = 0; b < (nt + 1) * np; ++b) hitems[icur++] = (uint32_t)j;
+      for (uint64_t t = 0; t < nt; ++t) {
+        psg::TileDesc& T = htiles[tcur++];
+        T.dk = s.keys + t * tile;
+        T.seg = d.seg + t * np;
+        T.pkeys = d.pkeys;
+        T.pvals = (const void* const*)(base + o.pv);
+        T.out = (void* const*)(base + o.out);
+        T.fail = d.fail;
+        T.slot0 = t * tile;
+        T.nt = (uint32_t)std::min<uint64_t>(tile, s.nslots - t * tile);
+        T.np = np;
+        T.flags = s.flags;
+      }
+      nslots.push_back(s.nslots);
+      seg_first.push_back(d.seg);
+      seg_last.push_back(d.seg + nt * np);
+      fails.push_back(d.fail);
+      npush.push_back(np);
     }
     memcpy(host_img.data(), h.data(), sizeof(JobDev) * h.size());
+    ntiles = (uint32_t)tiles;
+    nitems = (uint32_t)items;
     d_jobs = (JobDev*)blob;
+    d_tiles = (psg::TileDesc*)(base + tiles_off);
+    d_item_job = (uint32_t*)(base + items_off);
     HIP_TRY(hipMemcpy(blob, host_img.data(), off, hipMemcpyHostToDevice));
     return PSG_OK;
   }
 
-  int run(hipStream_t s) const {
+  int run_stage(int stage, hipStream_t s) const {
     if (h.empty()) return PSG_OK;
-    HIP_TRY(psg::launch_partition(d_jobs, (int)h.size(), nitems, s));
-    HIP_TRY(psg::launch_aggregate(dtype, m, d_jobs, (int)h.size(), ntiles, s));
+    if (stage == 0)
+      HIP_TRY(psg::launch_partition(d_jobs, d_item_job, nitems, s));
+    else
+      HIP_TRY(psg::launch_aggregate(dtype, m, geo, d_tiles, ntiles, maxnp, s));
     return PSG_OK;
+  }
+
+  int run(hipStream_t s) const {
+    if (int rc = run_stage(0, s)) return rc;
+    return run_stage(1, s);
   }
 
   // matched[p] = (covered elements) - (in-tile failures); stream must be idle.
   int matched(std::vector<uint64_t>& out) const {
     out.clear();
     for (size_t j = 0; j < h.size(); ++j) {
-      const JobDev& d = h[j];
-      const uint32_t np = d.npush;
+      const uint32_t np = npush[j];
+      if (np == 0) continue;
       std::vector<uint32_t> first(np), last(np);
       std::vector<unsigned long long> f(np);
-      if (np == 0) continue;
-      HIP_TRY(hipMemcpy(first.data(), d.seg, 4 * np, hipMemcpyDeviceToHost));
-      HIP_TRY(hipMemcpy(last.data(), d.seg + (size_t)d.ntiles * np, 4 * np,
-                        hipMemcpyDeviceToHost));
-      HIP_TRY(hipMemcpy(f.data(), d.fail, 8 * np, hipMemcpyDeviceToHost));
+      HIP_TRY(hipMemcpy(first.data(), seg_first[j], 4 * np, hipMemcpyDeviceToHost));
+      HIP_TRY(hipMemcpy(last.data(), seg_last[j], 4 * np, hipMemcpyDeviceToHost));
+      HIP_TRY(hipMemcpy(f.data(), fails[j], 8 * np, hipMemcpyDeviceToHost));
       for (uint32_t p = 0; p < np; ++p) {
         const uint64_t covered = nslots[j] ? (uint64_t)(last[p] - first[p]) : 0;
         out.push_back(covered >= f[p] ? covered - f[p] : 0);
@@ -381,14 +434,7 @@ int psg_plan_run(psg_plan* plan, void* stream) {
 int psg_plan_run_stage(psg_plan* plan, int stage, void* stream) {
   if (!plan || stage < 0 || stage > 1) return fail(PSG_ERR_ARG, "bad plan/stage");
   plan->last = (hipStream_t)stream;
-  const JobTable& t = plan->table;
-  if (t.h.empty()) return PSG_OK;
-  if (stage == 0)
-    HIP_TRY(psg::launch_partition(t.d_jobs, (int)t.h.size(), t.nitems, (hipStream_t)stream));
-  else
-    HIP_TRY(psg::launch_aggregate(t.dtype, t.m, t.d_jobs, (int)t.h.size(), t.ntiles,
-                                  (hipStream_t)stream));
-  return PSG_OK;
+  return plan->table.run_stage(stage, (hipStream_t)stream);
 }
 
 int psg_plan_matched(psg_plan* plan, uint64_t* matched) {
