@@ -36,6 +36,49 @@ namespace {
 
 constexpr uint32_t kInvalid = 0xFFFFFFFFu;
 
+// Two concurrent 32-ary searches (lanes 0-31: key a, lanes 32-63: key b):
+// first index whose key is >= k (or > k when `up`), per half-wave.
+__device__ __forceinline__ void wave_search2(const uint64_t* __restrict__ S,
+                                             uint64_t n, uint64_t ka, bool ua,
+                                             uint64_t kb, bool ub, int lane,
+                                             uint64_t* ra, uint64_t* rb) {
+  const int h = lane >> 5, hl = lane & 31;
+  const uint64_t key = h ? kb : ka;
+  const bool up = h ? ub : ua;
+  uint64_t lo = 0, hi = n;  // answer in [lo, hi]
+  for (;;) {
+    const bool active = hi > lo;
+    if (__ballot(active) == 0ull) break;
+    const uint64_t len = hi - lo;
+    const uint64_t step = (len + 31) >> 5;
+    const uint64_t idx = lo + (uint64_t)(hl + 1) * step - 1;
+    bool pred = true;
+    if (active && idx < hi) {
+      const uint64_t s = S[idx];
+      pred = up ? (s > key) : (s >= key);
+    }
+    const unsigned long long m = __ballot(pred);
+    const uint32_t mh = (uint32_t)(m >> (32 * h));
+    if (active) {
+      if (mh == 0u) {
+        lo = hi;
+      } else {
+        const uint64_t f = (uint64_t)(__ffs(mh) - 1);
+        const uint64_t nhi = lo + (f + 1) * step - 1;
+        lo = lo + f * step;
+        hi = nhi < hi ? nhi : hi;
+      }
+    }
+  }
+  *ra = __shfl(lo, 0, 64);
+  *rb = __shfl(lo, 32, 64);
+}
+
+// partition: one wave per (job, push p, group of 64 consecutive tile
+// boundaries).  The group's first and last boundaries bracket a window of
+// the push (two 32-ary searches); each lane then binary-searches its own
+// boundary inside that window (L2-resident).  Boundary b < ntiles is
+// lower_bound(S_p, D[b*tile]); b == ntiles is upper_bound(S_p, D[nslots-1]).
 __global__ __launch_bounds__(256) void partition_kernel(
     const JobDev* __restrict__ jobs, const uint32_t* __restrict__ item_job,
     uint32_t nitems) {
@@ -45,17 +88,41 @@ __global__ __launch_bounds__(256) void partition_kernel(
   const uint32_t j = __builtin_amdgcn_readfirstlane(item_job[item]);
   const JobDev& J = jobs[j];
   const uint32_t local = item - J.part_begin;
-  const uint32_t b = local / J.npush;
-  const uint32_t p = local - b * J.npush;
+  const uint32_t ng = (J.ntiles + 64u) >> 6;  // ceil((ntiles + 1) / 64)
+  const uint32_t p = local / ng;
+  const uint32_t g = local - p * ng;
+  const uint32_t b = (g << 6) + (uint32_t)lane;
+  const bool valid = b <= J.ntiles;
   uint64_t res = 0;
   if (J.nslots > 0) {
-    const bool upper = (b == J.ntiles);
-    const uint64_t key =
-        upper ? J.dkeys[J.nslots - 1] : J.dkeys[(uint64_t)b * J.tile];
-    res = wave_search(J.pkeys[p], J.pn[p], key, upper, lane);
+    const uint64_t* S = J.pkeys[p];
+    const uint64_t n = J.pn[p];
+    auto key_of = [&](uint32_t bb) {
+      return bb == J.ntiles ? J.dkeys[J.nslots - 1] : J.dkeys[(uint64_t)bb * J.tile];
+    };
+    const uint32_t bf = g << 6;
+    const uint32_t bl = bf + 63 < J.ntiles ? bf + 63 : J.ntiles;
+    uint64_t wlo, whi;
+    wave_search2(S, n, key_of(bf), bf == J.ntiles, key_of(bl), bl == J.ntiles, lane,
+                 &wlo, &whi);
+    const uint32_t bc = valid ? b : bl;
+    const uint64_t k = key_of(bc);
+    const bool up = bc == J.ntiles;
+    uint64_t lo = wlo, len = whi - wlo;
+    while (len > 0) {
+      const uint64_t half = len >> 1;
+      const uint64_t s = S[lo + half];
+      if (up ? !(k < s) : (s < k)) {
+        lo += half + 1;
+        len -= half + 1;
+      } else {
+        len = half;
+      }
+    }
+    res = lo;
   }
-  if (lane == 0) {
-    J.seg[local] = (uint32_t)res;
+  if (valid) {
+    J.seg[(size_t)b * J.npush + p] = (uint32_t)res;
     if (b == 0) J.fail[p] = 0ull;  // the aggregate launch follows in-stream
   }
 }

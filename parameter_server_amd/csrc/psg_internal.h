@@ -60,6 +60,8 @@ hipError_t launch_partition(const JobDev* d_jobs, const uint32_t* d_item_job,
 size_t aggregate_lds_bytes(int geo, int dtype, int m, uint32_t maxnp);
 hipError_t launch_aggregate(int dtype, int m, int geo, const TileDesc* d_tiles,
                             uint32_t ntiles, uint32_t maxnp, hipStream_t stream);
+hipError_t launch_aggregate_v4(int dtype, int m, int geo, const TileDesc* d_tiles,
+                               uint32_t ntiles, uint32_t maxnp, hipStream_t stream);
 hipError_t launch_gather(int dtype, const uint64_t* dkeys, uint64_t nd,
                          const void* dvals, const uint64_t* req, uint64_t nreq,
                          void* out, unsigned long long* matched,

@@ -68,7 +68,7 @@ struct JobSpec {
 
 struct JobTable {
   int device = -1;
-  int dtype = 0, m = 1, geo = psg::kGeoM;
+  int dtype = 0, m = 1, geo = psg::kGeoM, kernel = 4;
   std::vector<JobDev> h;
   std::vector<uint64_t> nslots;
   std::vector<uint32_t*> seg_first;  // device row 0 of each job's seg
@@ -105,6 +105,10 @@ struct JobTable {
     dtype = dt;
     m = mm;
     geo = pick_geometry();
+    {
+      const char* k = getenv("PSG_KERNEL");  // 2 = one-tile-per-workgroup kernel
+      kernel = (k && k[0] == '2') ? 2 : 4;
+    }
     const uint32_t tile = (uint32_t)psg::geo_tile(geo);
     h.clear();
     nslots.clear();
@@ -126,7 +130,7 @@ struct JobTable {
           return fail(PSG_ERR_ARG, "push of %llu keys >= 2^32", (unsigned long long)s.pn[p]);
       const uint64_t nt = (s.nslots + tile - 1) / tile;
       tiles += nt;
-      items += (nt + 1) * np;
+      items += ((nt + 64) / 64) * np;  // partition: one wave per 64 boundaries
       if (tiles >= (1ull << 31) || items >= (1ull << 31))
         return fail(PSG_ERR_ARG, "batch too large (%llu tiles)", (unsigned long long)tiles);
       maxnp = std::max(maxnp, (uint32_t)np);
@@ -178,7 +182,7 @@ struct JobTable {
       d.part_begin = icur;
       d.tile = tile;
       h.push_back(d);
-      for (uint64_t b = 0; b < (nt + 1) * np; ++b) hitems[icur++] = (uint32_t)j;
+      for (uint64_t b = 0; b < ((nt + 64) / 64) * np; ++b) hitems[icur++] = (uint32_t)j;
       for (uint64_t t = 0; t < nt; ++t) {
         psg::TileDesc& T = htiles[tcur++];
         T.dk = s.keys + t * tile;
@@ -212,8 +216,10 @@ struct JobTable {
     if (h.empty()) return PSG_OK;
     if (stage == 0)
       HIP_TRY(psg::launch_partition(d_jobs, d_item_job, nitems, s));
-    else
+    else if (kernel == 2)
       HIP_TRY(psg::launch_aggregate(dtype, m, geo, d_tiles, ntiles, maxnp, s));
+    else
+      HIP_TRY(psg::launch_aggregate_v4(dtype, m, geo, d_tiles, ntiles, maxnp, s));
     return PSG_OK;
   }
 
@@ -296,6 +302,7 @@ struct psg_ctx {
   unsigned long long* d_counter = nullptr;  // scratch counter (8 words)
   void* scratch = nullptr;
   size_t scratch_bytes = 0;
+  size_t flush_pushes = psg::kMaxPush;  // pushes per aggregate launch
 
   int ensure_scratch(size_t b) {
     if (b <= scratch_bytes) return PSG_OK;
@@ -310,7 +317,7 @@ struct psg_ctx {
   // Merge every pending push of aggregate `a` into its device output.
   int flush(Aggregate& a) {
     while (!a.pending.empty()) {
-      const size_t take = std::min(a.pending.size(), (size_t)psg::kMaxPush);
+      const size_t take = std::min(a.pending.size(), flush_pushes);
       JobSpec js;
       js.keys = ch[a.chl].d_keys + a.lo;
       js.nslots = a.hi - a.lo;
@@ -522,6 +529,10 @@ int psg_create(int device, int dtype, unsigned flags, psg_ctx** out) {
   c->device = device;
   c->dtype = dtype;
   c->flags = flags;
+  if (const char* f = getenv("PSG_FLUSH_PUSHES")) {  // testing aid: force launch seams
+    const long v = atol(f);
+    if (v >= 1 && v <= psg::kMaxPush) c->flush_pushes = (size_t)v;
+  }
   hipError_t e = hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking);
   if (e == hipSuccess) e = hipMalloc((void**)&c->d_counter, 64);
   if (e != hipSuccess) {
@@ -722,7 +733,7 @@ int psg_push(psg_ctx* c, int chl, int time, uint64_t kb, uint64_t ke,
   Aggregate& A = ait->second;
   A.pending.push_back(pp);
   A.expected_total += n;
-  if (A.pending.size() >= (size_t)psg::kMaxPush) return c->flush(A);
+  if (A.pending.size() >= c->flush_pushes) return c->flush(A);
   return PSG_OK;
 }
 

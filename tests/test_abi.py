@@ -34,7 +34,7 @@ def test_host_only_entry_points():
     L = _lib.lib()
     assert L.psg_abi_version() == 1
     assert L.psg_status_string(_lib.PSG_ERR_UNMATCHED) == b"pushed key not matched"
-    assert L.psg_plan_max_push() == 512
+    assert L.psg_plan_max_push() == 4096
     # shard bounds is pure host arithmetic (range.h:85-98)
     import numpy as np
     from parameter_server_amd.kv_vector import shard_bounds

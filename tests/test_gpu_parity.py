@@ -146,9 +146,11 @@ def test_random_vs_oracle(torch_cuda, seed, parallel):
         assert_bitexact(out[i][1], want[i])
 
 
-def test_more_pushes_than_one_launch(torch_cuda):
-    """> 512 pushes for one time: two launches, the second continuing the
-    aggregate (serial zero semantics across the launch seam)."""
+@pytest.mark.parametrize("per_launch", [7, 64, 4096])
+def test_launch_seams(torch_cuda, per_launch, monkeypatch):
+    """600 pushes for one time split into launches of `per_launch` pushes,
+    each continuing the aggregate (serial zero semantics across seams)."""
+    monkeypatch.setenv("PSG_FLUSH_PUSHES", str(per_launch))
     D, pushes = random_case(11, np.float32, 1, 600, 0.02, 4000)
     pushes = [p for p in pushes if p[0].size]
     for parallel in (False, True):
