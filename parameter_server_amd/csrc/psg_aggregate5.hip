@@ -1,27 +1,21 @@
-// psg_aggregate4.hip -- lean aggregate kernel (one workgroup per tile).
+// psg_aggregate5.hip -- aggregate kernel v5 (one workgroup per tile).
 //
-// Same contract and bit-exact output as aggregate_kernel (psg_aggregate.hip;
-// reference KVVector::serialSetValue / parallelSetValue, kv_vector.h:84-204,
-// over match / oldMatch, message.h:134-267), with the instruction stream
-// cut down (DESIGN.md "Kernels"):
+// Same contract and bit-exact output as the v2/v4 kernels (reference
+// KVVector::serialSetValue / parallelSetValue, kv_vector.h:84-204, over
+// match / oldMatch, message.h:134-267).  Relative to v4:
 //
-//   * element -> push: one wave-uniform lookup per round when the wave's 64
-//     elements belong to one push (the common case), a 6-probe branchless
-//     search otherwise;
-//   * slot search: the D tile is padded with UINT64_MAX sentinels to a power
-//     of two; log2(TILE)+1 unguarded probes on a byte offset, so each probe
-//     is one ds_read_b64 with an immediate offset + compare + select;
-//   * push order is checked on slot positions (u16 in LDS): all keys matched
-//     and strictly increasing slots <=> strictly increasing keys inside the
-//     range, i.e. the reference's matched == n (kv_vector.h:134,192);
-//   * fold: a slot with one contribution in the chunk is folded in O(1) by
-//     its owner; slots with >= 2 (cross-push duplicates) go to a compacted
-//     hot list folded in push order by one thread each, so waves no longer
-//     loop max(popcount) times per slot;
-//   * accumulators and last-push indices live in LDS for the whole tile.
+//   * slot search through a per-tile bucket table: bucket(k) =
+//     (k - D[0]) >> shift with TILE/4 buckets over the tile's key range;
+//     btab[b] = first slot of bucket b, so lower_bound(k) lies in
+//     [btab[b], btab[b+1]] and a 4-probe search covers windows <= 8 slots
+//     (uniform / hashed / contiguous keys); wider windows fall back to the
+//     full sentinel-padded search;
+//   * an element alone in its slot within the chunk (one mask bit) folds
+//     directly into the LDS accumulator; only slots with >= 2 pushes in the
+//     chunk ("hot") stage their values, in push order, for one folding
+//     thread each.  No per-chunk rank scan, no full scatter.
 #include <hip/hip_runtime.h>
 #include <stdint.h>
-#include <stdlib.h>
 
 #include "psg_device.h"
 #include "psg_internal.h"
@@ -48,19 +42,23 @@ __device__ __forceinline__ AS1 T* GW(T* p) {
 }
 
 template <typename V, int M, int TILE, int NT>
-struct L4 {
+struct L5 {
   static constexpr int kSPT = TILE / NT;
   static constexpr int kChunk = NT * kEPT;
-  static constexpr size_t dk = 0;                               // u64[TILE]
-  static constexpr size_t mask = dk + 8 * TILE;                 // u64[TILE]
+  static constexpr int kNB = TILE / 4;                          // buckets
+  static constexpr size_t dk = 0;                               // u64[TILE + 8]
+  static constexpr size_t mask = dk + 8 * (TILE + 8);           // u64[TILE]
   static constexpr size_t acc = mask + 8 * TILE;                // V[M][TILE]
-  static constexpr size_t base = acc + sizeof(V) * M * TILE;    // u16[TILE]
-  static constexpr size_t sorted = base + 2 * TILE;             // V[kChunk] + dummy
-  static constexpr size_t epos = sorted;                        // u16[kChunk], aliases sorted
-  static constexpr size_t bpush = sorted + sizeof(V) * kChunk + 16;  // u32[kChunk/64]
-  static constexpr size_t last = bpush + 4 * (kChunk / 64);     // i16[TILE]
-  static constexpr size_t hot = last + 2 * TILE;                // u16[TILE]
-  static constexpr size_t gk = hot + 2 * TILE;                  // ptr[kGroup]
+  static constexpr size_t last = acc + sizeof(V) * M * TILE;    // i16[TILE]
+  static constexpr size_t hoff = last + 2 * TILE;               // u16[TILE]
+  static constexpr size_t hot = hoff + 2 * TILE;                // u16[TILE]
+  static constexpr size_t btab = hot + 2 * TILE;                // u32[kNB + 1]
+  static constexpr size_t hv = (btab + 4 * (kNB + 1) + 15) / 16 * 16;  // V[kChunk*M]
+  static constexpr size_t epos = hv;                            // u16[kChunk] (aliases hv)
+  static constexpr size_t hvb = sizeof(V) * M * kChunk > 2 * kChunk
+                                    ? sizeof(V) * M * kChunk : 2 * kChunk;
+  static constexpr size_t bpush = hv + hvb;                     // u32[kChunk/64]
+  static constexpr size_t gk = bpush + 4 * (kChunk / 64);       // ptr[kGroup]
   static constexpr size_t gv = gk + 8 * kGroup;                 // ptr[kGroup*M]
   static constexpr size_t wsum = gv + 8 * kGroup * M;           // u32[16]
   static constexpr size_t misc = wsum + 64;                     // u32[16]
@@ -70,9 +68,8 @@ struct L4 {
   }
 };
 
-enum { kMiscHot = 0, kMiscCarry = 1 };
+enum { kMiscHot = 0, kMiscCarry = 1, kMiscHv = 2 };
 
-// largest p in [pf, pl) with pstart[p] <= e  (pl - pf <= 64)
 __device__ __forceinline__ uint32_t locate(const uint32_t* pstart, uint32_t pf,
                                            uint32_t pl, uint32_t e) {
   uint32_t p = pf;
@@ -85,10 +82,8 @@ __device__ __forceinline__ uint32_t locate(const uint32_t* pstart, uint32_t pf,
   return p;
 }
 
-// branchless lower_bound over a sentinel-padded power-of-two tile; works on
-// byte offsets so every probe is one ds_read_b64 with an immediate offset.
 template <int TILE>
-__device__ __forceinline__ int lb_padded(const uint64_t* a, uint64_t k) {
+__device__ __forceinline__ uint32_t lb_padded(const uint64_t* a, uint64_t k) {
   const char* ab = (const char*)a;
   uint32_t off = 0;
 #pragma unroll
@@ -98,10 +93,9 @@ __device__ __forceinline__ int lb_padded(const uint64_t* a, uint64_t k) {
   }
   const uint64_t v = *(const uint64_t*)(ab + off);
   off = (v < k) ? off + 8 : off;
-  return (int)(off >> 3);
+  return off >> 3;
 }
 
-// one fold step in push-arrival order (fold_step in psg_device.h), branchless
 template <typename V>
 __device__ __forceinline__ V fold1(V acc, int lp, int p, V v, bool parallel,
                                    bool cont) {
@@ -110,25 +104,27 @@ __device__ __forceinline__ V fold1(V acc, int lp, int p, V v, bool parallel,
   return (p == 0 && !cont) ? v : a1 + v;
 }
 
-// MODE (diagnostic ablation, 0 = the product kernel): 1 = loads + store
-// only, 2 = + slot search and mask, 3 = + ranks (no scatter/fold).
-template <typename V, int M, int TILE, int NT, int MODE = 0>
-__global__ __launch_bounds__(NT) void aggregate_v4_kernel(
+template <typename V, int M, int TILE, int NT>
+__global__ __launch_bounds__(NT) void aggregate_v5_kernel(
     const TileDesc* __restrict__ tiles, uint32_t maxnp) {
-  using L = L4<V, M, TILE, NT>;
+  using L = L5<V, M, TILE, NT>;
   constexpr int SPT = L::kSPT;
   constexpr int CHUNK = L::kChunk;
+  constexpr int NB = L::kNB;
+  constexpr int LOGNB = __builtin_ctz(NB);
   static_assert(SPT == 4, "4 slots per thread");
+  static_assert(NB <= NT, "one bucket per thread");
   extern __shared__ __attribute__((aligned(16))) char smem[];
   uint64_t* dk = (uint64_t*)(smem + L::dk);
   unsigned long long* mask = (unsigned long long*)(smem + L::mask);
   V* accl = (V*)(smem + L::acc);
-  uint16_t* base = (uint16_t*)(smem + L::base);
-  V* sorted = (V*)(smem + L::sorted);
+  int16_t* lastl = (int16_t*)(smem + L::last);
+  uint16_t* hoff = (uint16_t*)(smem + L::hoff);
+  uint16_t* hot = (uint16_t*)(smem + L::hot);
+  uint32_t* btab = (uint32_t*)(smem + L::btab);
+  V* hv = (V*)(smem + L::hv);
   uint16_t* epos = (uint16_t*)(smem + L::epos);
   uint32_t* bpush = (uint32_t*)(smem + L::bpush);
-  int16_t* lastl = (int16_t*)(smem + L::last);
-  uint16_t* hot = (uint16_t*)(smem + L::hot);
   const uint64_t** gk = (const uint64_t**)(smem + L::gk);
   const V** gv = (const V**)(smem + L::gv);
   uint32_t* wsum = (uint32_t*)(smem + L::wsum);
@@ -137,7 +133,6 @@ __global__ __launch_bounds__(NT) void aggregate_v4_kernel(
   uint32_t* segb = pstart + maxnp + 1;
 
   const int tid = threadIdx.x;
-  const int lane = tid & 63;
   const int s0 = tid * SPT;
   const TileDesc T = tiles[blockIdx.x];
   const int nt = (int)T.nt;
@@ -148,13 +143,14 @@ __global__ __launch_bounds__(NT) void aggregate_v4_kernel(
 #pragma unroll
   for (int mi = 0; mi < M; ++mi) outp[mi] = (V*)T.out[mi] + T.slot0;
 
-  // ---- tile setup: D (sentinel padded), segments, first push group,
-  //      accumulators, last-push indices: one round trip
+  // ---- tile setup (one round trip): D (sentinel padded), segments, first
+  //      push group, accumulators, last-push indices
 #pragma unroll
   for (int k = 0; k < SPT; ++k) {
     const int i = tid + k * NT;
     dk[i] = i < nt ? G(T.dk)[i] : ~0ull;
   }
+  if (tid < 8) dk[TILE + tid] = ~0ull;
   for (uint32_t p = tid; p < np; p += NT) {
     const uint32_t b = G(T.seg)[p];
     segb[p] = b;
@@ -175,6 +171,21 @@ __global__ __launch_bounds__(NT) void aggregate_v4_kernel(
       accl[mi * TILE + s0 + j] = (cont && s0 + j < nt) ? G(outp[mi])[s0 + j] : V(0);
   }
   __syncthreads();
+  // bucket table over [D[0], D[nt-1]]
+  const uint64_t klo = dk[0];
+  const uint64_t range = nt > 0 ? dk[nt - 1] - klo : 0ull;
+  const int bits = range ? 64 - __builtin_clzll(range) : 0;
+  const int shift = bits > LOGNB ? bits - LOGNB : 0;
+  if (tid <= NB) {
+    uint32_t s = (uint32_t)nt;
+    if (tid < NB) {
+      const uint64_t d = (uint64_t)tid << shift;
+      const uint64_t key = d > ~0ull - klo ? ~0ull : klo + d;
+      s = lb_padded<TILE>(dk, key);
+      s = s < (uint32_t)nt ? s : (uint32_t)nt;
+    }
+    btab[tid] = s;
+  }
   uint32_t E = 0;
   for (uint32_t c0 = 0; c0 < np; c0 += NT) {
     const uint32_t idx = c0 + tid;
@@ -185,11 +196,10 @@ __global__ __launch_bounds__(NT) void aggregate_v4_kernel(
     __syncthreads();
   }
   if (tid == 0) pstart[np] = E;
-  __syncthreads();
 
   uint32_t gbase = 0;
   for (uint32_t e0 = 0; e0 < E;) {
-    // chunk bounds (uniform)
+    __syncthreads();
     uint32_t pf;
     {
       int lo = 0, hi = (int)np - 1;
@@ -204,7 +214,6 @@ __global__ __launch_bounds__(NT) void aggregate_v4_kernel(
     if (e1 > E) e1 = E;
     if (e1 > pstart[pl]) e1 = pstart[pl];
     if (pf < gbase || pl > gbase + kGroup) {  // uniform: stage push pointers
-      __syncthreads();
       gbase = pf;
       const uint32_t w = pl - pf;
       for (uint32_t q = tid; q < w * (1 + M); q += NT) {
@@ -214,9 +223,10 @@ __global__ __launch_bounds__(NT) void aggregate_v4_kernel(
     }
 #pragma unroll
     for (int k = 0; k < SPT; ++k) mask[tid + k * NT] = 0ull;
-    if (tid == 0) misc[kMiscHot] = 0;
-    // push of the first element of every 64-element block of the chunk, and
-    // whether the whole block lies in that push (bit 31)
+    if (tid == 0) {
+      misc[kMiscHot] = 0;
+      misc[kMiscHv] = 0;
+    }
     {
       const uint32_t nblk = (e1 - e0 + 63) >> 6;
       for (uint32_t b = tid; b < nblk; b += NT) {
@@ -228,8 +238,7 @@ __global__ __launch_bounds__(NT) void aggregate_v4_kernel(
     }
     __syncthreads();
 
-    // ---- 2a. every element load of the chunk, branch-free (lanes past the
-    //          chunk re-load its last element and are masked off below)
+    // ---- loads (branch-free; lanes past the chunk re-load its last element)
     uint64_t ekey[kEPT];
     uint32_t einfo[kEPT];
     V ev[kEPT][M];
@@ -240,7 +249,7 @@ __global__ __launch_bounds__(NT) void aggregate_v4_kernel(
       const uint32_t ec = valid ? e : e1 - 1;
       const uint32_t bi = __builtin_amdgcn_readfirstlane(bpush[(ec - e0) >> 6]);
       uint32_t p = bi & 0x7FFFFFFFu;
-      if (!(bi >> 31)) p = locate(pstart, p, pl, ec);  // wave-uniform branch
+      if (!(bi >> 31)) p = locate(pstart, p, pl, ec);
       const uint32_t li = ec - pstart[p];
       const uint64_t i = (uint64_t)segb[p] + li;
       ekey[r] = G(gk[p - gbase])[i];
@@ -249,27 +258,39 @@ __global__ __launch_bounds__(NT) void aggregate_v4_kernel(
       einfo[r] = valid ? (((p - pf) << kLiBits) | (li < kLiMask ? li : kLiMask)) : kInv;
     }
 
-    if constexpr (MODE == 1) {
-      V sink = V(0);
+    // ---- slot search through the bucket table, mask bit, slot position
+    uint32_t spos[kEPT];
 #pragma unroll
-      for (int r = 0; r < kEPT; ++r)
-        if (einfo[r] != kInv) sink += ev[r][0] + V(ekey[r] & 1u);
-      accl[s0] += sink;
-      __syncthreads();
-      e0 = e1;
-      continue;
+    for (int r = 0; r < kEPT; ++r) {
+      const uint64_t k = ekey[r];
+      const uint64_t d = k - klo;
+      const uint32_t b = (k < klo) ? 0u : (d >> shift) < (uint64_t)NB ? (uint32_t)(d >> shift) : NB;
+      const uint32_t lo = btab[b];
+      const uint32_t hi = btab[b + (b < (uint32_t)NB ? 1 : 0)];
+      spos[r] = lo;
+      if (hi - lo > 8u) spos[r] = kInv;  // wide window: full search below
+      else {
+        uint32_t off = lo * 8;
+        const char* ab = (const char*)dk;
+#pragma unroll
+        for (int step = 4; step > 0; step >>= 1) {
+          const uint64_t v = *(const uint64_t*)(ab + off + 8 * (step - 1));
+          off = (v < k) ? off + 8 * step : off;
+        }
+        const uint64_t v = *(const uint64_t*)(ab + off);
+        off = (v < k) ? off + 8 : off;
+        spos[r] = off >> 3;
+      }
     }
-    // ---- 2b. slot of every element (independent chains interleave), mask
-    //          bit, slot position for the order check
-    uint32_t rec[kEPT];
-    int spos[kEPT];
 #pragma unroll
-    for (int r = 0; r < kEPT; ++r) spos[r] = lb_padded<TILE>(dk, ekey[r]);
+    for (int r = 0; r < kEPT; ++r)
+      if (spos[r] == kInv) spos[r] = lb_padded<TILE>(dk, ekey[r]);
+    uint32_t rec[kEPT];
 #pragma unroll
     for (int r = 0; r < kEPT; ++r) {
       const uint32_t e = e0 + (uint32_t)tid + (uint32_t)r * NT;
       const uint32_t b = einfo[r] >> kLiBits;
-      const int pos = spos[r];
+      const int pos = (int)spos[r];
       const bool ok = einfo[r] != kInv && pos < nt && dk[pos] == ekey[r];
       if (ok) atomicOr(&mask[pos], 1ull << b);
       rec[r] = ok ? ((uint32_t)pos | (b << 16)) : kInv;
@@ -280,100 +301,88 @@ __global__ __launch_bounds__(NT) void aggregate_v4_kernel(
     }
     __syncthreads();
 
-    if constexpr (MODE == 2) {
-      e0 = e1;
-      continue;
-    }
-    // ---- 3. counts -> rank bases; hot list; order check
-    unsigned long long mymask[SPT];
-    uint32_t mybase[SPT];
-    {
-      uint32_t c[SPT], csum = 0;
-#pragma unroll
-      for (int j = 0; j < SPT; ++j) {
-        mymask[j] = mask[s0 + j];
-        c[j] = (uint32_t)__popcll(mymask[j]);
-        csum += c[j];
-        if (c[j] >= 2) hot[atomicAdd(&misc[kMiscHot], 1u)] = (uint16_t)(s0 + j);
-      }
-      uint32_t tot;
-      uint32_t run = block_excl_scan<NT>(csum, wsum, &tot);
-#pragma unroll
-      for (int j = 0; j < SPT; ++j) {
-        mybase[j] = run;
-        base[s0 + j] = (uint16_t)run;
-        run += c[j];
-      }
-    }
+    // ---- singles fold directly; hot slots register; order check
+    uint32_t hrank[kEPT];
     {
       const uint32_t carry = misc[kMiscCarry];
 #pragma unroll
       for (int r = 0; r < kEPT; ++r) {
+        hrank[r] = kInv;
+        if (rec[r] == kInv) continue;
+        const int pos = (int)(rec[r] & 0xFFFFu);
+        const int b = (int)(rec[r] >> 16);
+        const int p = (int)pf + b;
+        const unsigned long long mk = mask[pos];
+        if ((mk & (mk - 1ull)) == 0ull) {  // alone in its slot: fold now
+          const int lp = lastl[pos];
+#pragma unroll
+          for (int mi = 0; mi < M; ++mi)
+            accl[mi * TILE + pos] = fold1<V>(accl[mi * TILE + pos], lp, p, ev[r][mi],
+                                            parallel, cont);
+          lastl[pos] = (int16_t)p;
+        } else {
+          const uint32_t rk = (uint32_t)__popcll(mk & ((1ull << b) - 1ull));
+          hrank[r] = rk;
+          if (rk == 0u) {  // the slot's first contributor registers it
+            const uint32_t h = atomicAdd(&misc[kMiscHot], 1u);
+            hot[h] = (uint16_t)pos;
+            hoff[pos] = (uint16_t)atomicAdd(&misc[kMiscHv], (uint32_t)__popcll(mk));
+          }
+        }
+      }
+#pragma unroll
+      for (int r = 0; r < kEPT; ++r) {
         const uint32_t e = e0 + (uint32_t)tid + (uint32_t)r * NT;
-        const uint32_t prev = e > e0 ? epos[e - 1 - e0] : carry;
         if (rec[r] != kInv && (einfo[r] & kLiMask) > 0) {
+          const uint32_t prev = e > e0 ? epos[e - 1 - e0] : carry;
           if (!(prev < (rec[r] & 0xFFFFu)))
             __hip_atomic_fetch_add(GW(T.fail) + pf + (einfo[r] >> kLiBits), 1ull,
                                    __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         }
       }
     }
-    const uint32_t next_carry = epos[e1 - 1 - e0];  // before sorted overwrites epos
+    const uint32_t next_carry = epos[e1 - 1 - e0];  // before hv overwrites epos
     __syncthreads();
     const uint32_t nhot = misc[kMiscHot];
     if (tid == 0) misc[kMiscCarry] = next_carry;
-
-    if constexpr (MODE == 3) {
-      e0 = e1;
-      continue;
-    }
-    // ---- 4. scatter into (slot, push) order; fold singles and hot slots
-#pragma unroll
-    for (int mi = 0; mi < M; ++mi) {
+    if (nhot > 0) {  // uniform
 #pragma unroll
       for (int r = 0; r < kEPT; ++r) {
-        const bool ok = rec[r] != kInv;
-        const int pos = (int)(rec[r] & 0x07FFu) & (TILE - 1);
-        const int b = (int)((rec[r] >> 16) & 63u);
-        const unsigned long long below = (1ull << b) - 1ull;
-        const uint32_t rank = base[pos] + (uint32_t)__popcll(mask[pos] & below);
-        sorted[ok ? rank : (uint32_t)CHUNK] = ev[r][mi];
+        if (hrank[r] != kInv) {
+          const int pos = (int)(rec[r] & 0xFFFFu);
+#pragma unroll
+          for (int mi = 0; mi < M; ++mi) hv[(hoff[pos] + hrank[r]) * M + mi] = ev[r][mi];
+        }
       }
       __syncthreads();
-#pragma unroll
-      for (int j = 0; j < SPT; ++j) {
-        const unsigned long long mk = mymask[j];
-        const bool single = mk != 0ull && (mk & (mk - 1ull)) == 0ull;
-        const int p = (int)pf + (__ffsll((long long)mk) - 1);
-        const int lp = lastl[s0 + j];
-        V* a = &accl[mi * TILE + s0 + j];
-        const V cur = *a;
-        const V nv = fold1<V>(cur, lp, p, sorted[mybase[j] < (uint32_t)CHUNK ? mybase[j] : CHUNK],
-                              parallel, cont);
-        *a = single ? nv : cur;
-        if (mi == M - 1 && single) lastl[s0 + j] = (int16_t)p;
-      }
       for (uint32_t h = tid; h < nhot; h += NT) {
         const int slot = hot[h];
         unsigned long long mk = mask[slot];
-        uint32_t rr = base[slot];
-        int lp = lastl[slot];
-        V a = accl[mi * TILE + slot];
-        while (mk) {
-          const int p = (int)pf + (__ffsll((long long)mk) - 1);
-          mk &= mk - 1ull;
-          a = fold1<V>(a, lp, p, sorted[rr++], parallel, cont);
-          lp = p;
+        const uint32_t o = hoff[slot];
+        const int lp0 = lastl[slot];
+        int lp = lp0;
+#pragma unroll
+        for (int mi = 0; mi < M; ++mi) {
+          unsigned long long m2 = mk;
+          uint32_t rr = o;
+          lp = lp0;
+          V a = accl[mi * TILE + slot];
+          while (m2) {
+            const int p = (int)pf + (__ffsll((long long)m2) - 1);
+            m2 &= m2 - 1ull;
+            a = fold1<V>(a, lp, p, hv[(rr++) * M + mi], parallel, cont);
+            lp = p;
+          }
+          accl[mi * TILE + slot] = a;
         }
-        accl[mi * TILE + slot] = a;
-        if (mi == M - 1) lastl[slot] = (int16_t)lp;
+        lastl[slot] = (int16_t)lp;
       }
-      __syncthreads();
     }
     e0 = e1;
   }
+  __syncthreads();
 
-  // ---- 5. trailing absent pushes (serial path: one "+ 0.0"), store
+  // ---- trailing absent pushes (serial path: one "+ 0.0"), store
   V res[M][SPT];
 #pragma unroll
   for (int j = 0; j < SPT; ++j) {
@@ -417,13 +426,13 @@ __global__ __launch_bounds__(NT) void aggregate_v4_kernel(
   }
 }
 
-template <typename V, int M, int G_, int MODE = 0>
-hipError_t launch_one4(const TileDesc* d_tiles, uint32_t ntiles, uint32_t maxnp,
+template <typename V, int M, int G_>
+hipError_t launch_one5(const TileDesc* d_tiles, uint32_t ntiles, uint32_t maxnp,
                        hipStream_t stream) {
   constexpr int TILE = geo_tile(G_), NT = geo_threads(G_);
-  using L = L4<V, M, TILE, NT>;
+  using L = L5<V, M, TILE, NT>;
   const size_t lds = L::bytes(maxnp);
-  auto kern = aggregate_v4_kernel<V, M, TILE, NT, MODE>;
+  auto kern = aggregate_v5_kernel<V, M, TILE, NT>;
   if (lds > 65536) {
     static size_t attr = 0;
     if (attr < lds) {
@@ -439,50 +448,35 @@ hipError_t launch_one4(const TileDesc* d_tiles, uint32_t ntiles, uint32_t maxnp,
 }
 
 template <typename V, int M>
-hipError_t launch_geo4(int geo, const TileDesc* t, uint32_t n, uint32_t maxnp,
+hipError_t launch_geo5(int geo, const TileDesc* t, uint32_t n, uint32_t maxnp,
                        hipStream_t s) {
-  if constexpr (sizeof(V) == 4 && M == 1) {
-    static const int mode = [] {
-      const char* e = getenv("PSG_AGG_MODE");  // diagnostic ablation only
-      return e ? atoi(e) : 0;
-    }();
-    if (geo == kGeoS) {
-      if (mode == 1) return launch_one4<V, M, kGeoS, 1>(t, n, maxnp, s);
-      if (mode == 2) return launch_one4<V, M, kGeoS, 2>(t, n, maxnp, s);
-      if (mode == 3) return launch_one4<V, M, kGeoS, 3>(t, n, maxnp, s);
-    } else {
-      if (mode == 1) return launch_one4<V, M, kGeoM, 1>(t, n, maxnp, s);
-      if (mode == 2) return launch_one4<V, M, kGeoM, 2>(t, n, maxnp, s);
-      if (mode == 3) return launch_one4<V, M, kGeoM, 3>(t, n, maxnp, s);
-    }
-  }
   switch (geo) {
-    case kGeoS: return launch_one4<V, M, kGeoS>(t, n, maxnp, s);
-    case kGeoM: return launch_one4<V, M, kGeoM>(t, n, maxnp, s);
-    case kGeoL: return launch_one4<V, M, kGeoL>(t, n, maxnp, s);
+    case kGeoS: return launch_one5<V, M, kGeoS>(t, n, maxnp, s);
+    case kGeoM: return launch_one5<V, M, kGeoM>(t, n, maxnp, s);
+    case kGeoL: return launch_one5<V, M, kGeoL>(t, n, maxnp, s);
     default: return hipErrorInvalidValue;
   }
 }
 
 template <typename V>
-hipError_t launch_m4(int m, int geo, const TileDesc* t, uint32_t n, uint32_t maxnp,
+hipError_t launch_m5(int m, int geo, const TileDesc* t, uint32_t n, uint32_t maxnp,
                      hipStream_t s) {
   switch (m) {
-    case 1: return launch_geo4<V, 1>(geo, t, n, maxnp, s);
-    case 2: return launch_geo4<V, 2>(geo, t, n, maxnp, s);
-    case 3: return launch_geo4<V, 3>(geo, t, n, maxnp, s);
-    case 4: return launch_geo4<V, 4>(geo, t, n, maxnp, s);
+    case 1: return launch_geo5<V, 1>(geo, t, n, maxnp, s);
+    case 2: return launch_geo5<V, 2>(geo, t, n, maxnp, s);
+    case 3: return launch_geo5<V, 3>(geo, t, n, maxnp, s);
+    case 4: return launch_geo5<V, 4>(geo, t, n, maxnp, s);
     default: return hipErrorInvalidValue;
   }
 }
 
 }  // namespace
 
-hipError_t launch_aggregate_v4(int dtype, int m, int geo, const TileDesc* d_tiles,
+hipError_t launch_aggregate_v5(int dtype, int m, int geo, const TileDesc* d_tiles,
                                uint32_t ntiles, uint32_t maxnp, hipStream_t stream) {
   if (ntiles == 0) return hipSuccess;
-  return dtype == 0 ? launch_m4<float>(m, geo, d_tiles, ntiles, maxnp, stream)
-                    : launch_m4<double>(m, geo, d_tiles, ntiles, maxnp, stream);
+  return dtype == 0 ? launch_m5<float>(m, geo, d_tiles, ntiles, maxnp, stream)
+                    : launch_m5<double>(m, geo, d_tiles, ntiles, maxnp, stream);
 }
 
 }  // namespace psg

@@ -62,6 +62,15 @@ hipError_t launch_aggregate(int dtype, int m, int geo, const TileDesc* d_tiles,
                             uint32_t ntiles, uint32_t maxnp, hipStream_t stream);
 hipError_t launch_aggregate_v4(int dtype, int m, int geo, const TileDesc* d_tiles,
                                uint32_t ntiles, uint32_t maxnp, hipStream_t stream);
+hipError_t launch_aggregate_v5(int dtype, int m, int geo, const TileDesc* d_tiles,
+                               uint32_t ntiles, uint32_t maxnp, hipStream_t stream);
+// streaming kernel: one wave per coarse tile of kStreamTile slots, np <= 64
+constexpr int kStreamTile = 4096;
+constexpr int kStreamMaxPush = 64;
+hipError_t launch_aggregate_stream(int dtype, int m, const TileDesc* d_tiles,
+                                   uint32_t ncoarse, hipStream_t stream);
+hipError_t launch_aggregate_stream2(int dtype, int m, const TileDesc* d_tiles,
+                                    uint32_t ncoarse, hipStream_t stream);
 hipError_t launch_gather(int dtype, const uint64_t* dkeys, uint64_t nd,
                          const void* dvals, const uint64_t* req, uint64_t nreq,
                          void* out, unsigned long long* matched,

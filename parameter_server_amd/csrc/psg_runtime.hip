@@ -68,7 +68,7 @@ struct JobSpec {
 
 struct JobTable {
   int device = -1;
-  int dtype = 0, m = 1, geo = psg::kGeoM, kernel = 4;
+  int dtype = 0, m = 1, geo = psg::kGeoS, kernel = 7;
   std::vector<JobDev> h;
   std::vector<uint64_t> nslots;
   std::vector<uint32_t*> seg_first;  // device row 0 of each job's seg
@@ -94,7 +94,7 @@ struct JobTable {
     if (g && (g[0] == 'S' || g[0] == 's')) return psg::kGeoS;
     if (g && (g[0] == 'L' || g[0] == 'l')) return psg::kGeoL;
     if (g && (g[0] == 'M' || g[0] == 'm')) return psg::kGeoM;
-    return psg::kGeoM;
+    return psg::kGeoS;
   }
 
   // Builds (or rebuilds, reusing the allocation when it fits) the device image:
@@ -107,9 +107,13 @@ struct JobTable {
     geo = pick_geometry();
     {
       const char* k = getenv("PSG_KERNEL");  // 2 = one-tile-per-workgroup kernel
-      kernel = (k && k[0] == '2') ? 2 : 4;
+      kernel = (k && k[0] >= '2' && k[0] <= '7' && k[0] != '3') ? k[0] - '0' : 7;
     }
-    const uint32_t tile = (uint32_t)psg::geo_tile(geo);
+    uint32_t maxnp_all = 0;
+    for (const JobSpec& s : jobs) maxnp_all = std::max(maxnp_all, (uint32_t)s.pn.size());
+    if (kernel >= 6 && maxnp_all > (uint32_t)psg::kStreamMaxPush) kernel = 4;  // many pushes
+    const uint32_t tile =
+        kernel >= 6 ? (uint32_t)psg::kStreamTile : (uint32_t)psg::geo_tile(geo);
     h.clear();
     nslots.clear();
     seg_first.clear();
@@ -218,8 +222,14 @@ struct JobTable {
       HIP_TRY(psg::launch_partition(d_jobs, d_item_job, nitems, s));
     else if (kernel == 2)
       HIP_TRY(psg::launch_aggregate(dtype, m, geo, d_tiles, ntiles, maxnp, s));
-    else
+    else if (kernel == 7)
+      HIP_TRY(psg::launch_aggregate_stream2(dtype, m, d_tiles, ntiles, s));
+    else if (kernel == 6)
+      HIP_TRY(psg::launch_aggregate_stream(dtype, m, d_tiles, ntiles, s));
+    else if (kernel == 4)
       HIP_TRY(psg::launch_aggregate_v4(dtype, m, geo, d_tiles, ntiles, maxnp, s));
+    else
+      HIP_TRY(psg::launch_aggregate_v5(dtype, m, geo, d_tiles, ntiles, maxnp, s));
     return PSG_OK;
   }
 
