@@ -210,7 +210,7 @@ def main():
             "unit": "GB/s",
             "frac": achieved / HBM_PEAK_GBPS,
             "traffic": traffic,
-            "kernel": "aggregate_kernel<float,1>",
+            "kernel": kernel_name(),
             "bytes_per_launch": plan.bytes,
             "bytes_formula": "sum_p n_p*(8+4) [pushes] + U*(8+4) [server keys + sums]",
             "kernel_ms": agg_ms,
@@ -220,11 +220,48 @@ def main():
         },
     }
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
+        result["end_to_end"] = end_to_end(insts[0], local)
         result["cpu_baseline"] = cpu_baseline(insts[0], args.cpu_seconds)
     if rank == 0:
         print(json.dumps(result), flush=True)
     if dist:
         dist.destroy_process_group()
+
+
+def kernel_name():
+    """The aggregate kernel the runtime selects (psg_runtime.hip JobTable)."""
+    k = os.environ.get("PSG_KERNEL", "7")
+    return {"7": "stream2_kernel<float,1,2,8,0,0,1>", "6": "stream_kernel<float,1>",
+            "4": "aggregate4_kernel<float,1>", "2": "aggregate_kernel<float,1>"}.get(k, k)
+
+
+def end_to_end(inst, device, reps=5):
+    """PCIe-inclusive rate of one cfg2 aggregate through the host API
+    (KVVector.setValue per push from pageable host memory + received(t)
+    D2H), the reference's own call pattern.  Reported beside `value`,
+    never as it."""
+    import ctypes
+    from parameter_server_amd.kv_vector import KVVector, Message
+    D, pushes = inst
+    kv = sum(int(k.size) for k, _ in pushes)
+    v = KVVector(device)
+    v.setValue(Message(key=D))  # key-only push: the server key set
+    times = []
+    for r in range(reps + 1):
+        t0 = time.perf_counter()
+        for k, vs in pushes:
+            v.setValue(Message(time=r, key=k, value=list(vs)))
+        out = v.received(r)
+        el = time.perf_counter() - t0
+        if r:
+            times.append(el)
+    assert out[0][1].size == D.size
+    v.close()
+    t = float(np.median(times))
+    return {"value": kv / t, "unit": "kv-pairs/s", "ms_per_aggregate": t * 1e3,
+            "scope": ("one cfg2 aggregate: 8 x psg_push (H2D of keys+values from pageable "
+                      "host memory, merge) + psg_received (D2H of the merged shard), "
+                      f"median of {reps}")}
 
 
 def load_traffic(args, bytes_per_launch):
@@ -262,8 +299,16 @@ def cpu_baseline(inst, seconds):
                 return reps * kv / el, reps, el
 
     v, reps, el = timed(0, 1)
-    nproc = os.cpu_count() or 1
-    vp, repsp, elp = timed(1, nproc)
+    # the threaded match path (FLAGS_parallel_match) at 4 threads (local.sh:25)
+    # and at this job's CPU share (<= 16 on the GPU box)
+    try:
+        share = len(os.sched_getaffinity(0))
+    except AttributeError:
+        share = os.cpu_count() or 1
+    par = {}
+    for nt in sorted({4, max(1, min(16, share))}):
+        vp, repsp, elp = timed(1, nt)
+        par[str(nt)] = {"value": vp, "reps": repsp, "seconds": elp}
     model = ""
     try:
         for line in open("/proc/cpuinfo"):
@@ -276,7 +321,7 @@ def cpu_baseline(inst, seconds):
         "value": v, "unit": "kv-pairs/s", "cores": 1, "kind": "port",
         "sample": (f"{reps} x one cfg2 aggregate (8 x 131072 kv, U={D.size}) through "
                    f"oracle serialSetValue restatement in {el:.1f}s, 1 thread, {model}"),
-        "parallel_match": {"value": vp, "threads": nproc, "reps": repsp, "seconds": elp},
+        "parallel_match_by_threads": par,
     }
 
 

@@ -79,9 +79,12 @@ __device__ __forceinline__ V fold1(V acc, int lp, int p, V v, bool parallel,
   return (p == 0 && !cont) ? v : a1 + v;
 }
 
-template <typename V, int M, int NPW, int WPS>
+// SR: slot search by dependent probes (0) or one round of wide window reads (1)
+// BTT: bucket table by per-bucket searches (0) or slot transitions (1)
+// PR: first window of a push per tile sized by its expected share (1) or 64 (0)
+template <typename V, int M, int NPW, int WPS, int SR = 0, int BTT = 0, int PR = 1>
 __global__ __launch_bounds__(64, WPS) void stream2_kernel(const TileDesc* __restrict__ tiles) {
-  __shared__ uint64_t dk[kFT + 8];
+  __shared__ __attribute__((aligned(16))) uint64_t dk[kFT + 16];
   __shared__ V acc[M * kFT];
   __shared__ int16_t lastl[kFT];
   __shared__ uint32_t btab[kNB + 1];
@@ -95,7 +98,7 @@ __global__ __launch_bounds__(64, WPS) void stream2_kernel(const TileDesc* __rest
   const uint32_t nft = (ncs + kFT - 1) / kFT;
   const uint64_t* Dg = T.dk;
 
-  uint32_t cur = 0, cend = 0;
+  uint32_t cur = 0, cend = 0, pred = 64;
   uint64_t kp = 0;
   uint64_t vp[M];
 #pragma unroll
@@ -106,14 +109,22 @@ __global__ __launch_bounds__(64, WPS) void stream2_kernel(const TileDesc* __rest
     kp = (uint64_t)G(T.pkeys)[lane];
 #pragma unroll
     for (int mi = 0; mi < M; ++mi) vp[mi] = (uint64_t)G(T.pvals)[(size_t)lane * M + mi];
+    if (PR && ncs > 0) {
+      // expected keys of push p per fine tile, + 2 sigma (Poisson) + 4: a
+      // short first window leaves fewer over-fetched keys to re-read next tile
+      const float mu = (float)(cend - cur) * (float)kFT / (float)ncs;
+      const float w = mu + 2.0f * __builtin_sqrtf(mu) + 4.0f;
+      pred = w >= 64.0f ? 64u : (uint32_t)w + 1u;
+    }
   }
-  if (lane < 8) dk[kFT + lane] = ~0ull;
+  if (lane < 16) dk[kFT + lane] = ~0ull;
 
-  // window of push p at its cursor: 64 keys (lanes past the end hold ~0)
-  auto load_window = [&](uint64_t& wk, V (&wv)[M], uint32_t& wc, uint32_t& wn, uint32_t p) {
+  // window of push p at its cursor: W keys (lanes past the end hold ~0)
+  auto load_window = [&](uint64_t& wk, V (&wv)[M], uint32_t& wc, uint32_t& wn, uint32_t p,
+                         uint32_t W) {
     const uint32_t c = (uint32_t)__builtin_amdgcn_readlane(cur, p);
     const uint32_t e = (uint32_t)__builtin_amdgcn_readlane(cend, p);
-    const uint32_t n = e - c < 64u ? e - c : 64u;
+    const uint32_t n = e - c < W ? e - c : W;
     wc = c;
     wn = n;
     const uint64_t* sk = (const uint64_t*)readlane64(kp, p);
@@ -134,6 +145,9 @@ __global__ __launch_bounds__(64, WPS) void stream2_kernel(const TileDesc* __rest
 #pragma unroll
     for (int mi = 0; mi < M; ++mi) outp[mi] = (V*)T.out[mi] + T.slot0 + base;
 
+    auto first_w = [&](uint32_t p) -> uint32_t {
+      return PR ? (uint32_t)__builtin_amdgcn_readlane(pred, p) : 64u;
+    };
     // ---- one round trip: D keys, bound, first batch of windows
     uint64_t dreg[4];
 #pragma unroll
@@ -147,7 +161,7 @@ __global__ __launch_bounds__(64, WPS) void stream2_kernel(const TileDesc* __rest
     uint32_t wc[NPW], wn[NPW];
 #pragma unroll
     for (int q = 0; q < NPW; ++q) {
-      if ((uint32_t)q < np) load_window(wk[q], wv[q], wc[q], wn[q], q);
+      if ((uint32_t)q < np) load_window(wk[q], wv[q], wc[q], wn[q], q, first_w(q));
       else { wk[q] = ~0ull; wn[q] = 0; wc[q] = 0; }
     }
 
@@ -168,12 +182,29 @@ __global__ __launch_bounds__(64, WPS) void stream2_kernel(const TileDesc* __rest
     const uint64_t range = dk[nt - 1] - klo;
     const int bits = range ? 64 - __builtin_clzll(range) : 0;
     const int shift = bits > 6 ? bits - 6 : 0;
-    {
+    if constexpr (BTT == 0) {
       const uint64_t d = (uint64_t)lane << shift;
       const uint64_t key = d > ~0ull - klo ? ~0ull : klo + d;
       const uint32_t sb = lb_pow2<kFT>(dk, 0, key);
       btab[lane] = sb < (uint32_t)nt ? sb : (uint32_t)nt;
       if (lane == 0) btab[kNB] = (uint32_t)nt;
+    } else {
+      // btab[b] = first slot whose bucket >= b: a slot opens the buckets
+      // between its predecessor's and its own; the last slot closes the table
+#pragma unroll
+      for (int k = 0; k < 4; ++k) {
+        const uint64_t up = __shfl_up(dreg[k], 1, 64);
+        const uint64_t wrap = k > 0 ? __shfl(dreg[k > 0 ? k - 1 : 0], 63, 64) : 0ull;
+        const uint64_t prevkey = lane > 0 ? up : wrap;
+        const int sidx = lane + 64 * k;
+        if (sidx < nt) {
+          const int bcur = (int)((dreg[k] - klo) >> shift);
+          const int bprev = sidx == 0 ? -1 : (int)((prevkey - klo) >> shift);
+          for (int b = bprev + 1; b <= bcur; ++b) btab[b] = (uint32_t)sidx;
+          if (sidx == nt - 1)
+            for (int b = bcur + 1; b <= kNB; ++b) btab[b] = (uint32_t)nt;
+        }
+      }
     }
     __syncthreads();
 
@@ -193,11 +224,34 @@ __global__ __launch_bounds__(64, WPS) void stream2_kernel(const TileDesc* __rest
       const uint32_t lo = btab[b];
       const uint32_t hi = btab[b < (uint32_t)kNB ? b + 1 : b];
       uint32_t pos;
-      if (hi - lo <= 8u) pos = lb_pow2<8>(dk, lo, k);
-      else pos = lb_pow2<kFT>(dk, 0, k);
+      bool found;
+      if constexpr (SR == 1) {
+        if (hi - lo <= 8u) {
+          // one round of 5 independent 16-byte reads covers [lo, lo+8]
+          const uint32_t w0 = lo & ~1u;
+          typedef uint64_t u2 __attribute__((ext_vector_type(2)));
+          const u2* wp = (const u2*)(dk + w0);
+          uint32_t cnt = 0;
+          found = false;
+#pragma unroll
+          for (int i = 0; i < 5; ++i) {
+            const u2 v = wp[i];
+            cnt += (v.x < k ? 1u : 0u) + (v.y < k ? 1u : 0u);
+            found = found || v.x == k || v.y == k;
+          }
+          pos = w0 + cnt;
+        } else {
+          pos = lb_pow2<kFT>(dk, 0, k);
+          found = dk[pos] == k;
+        }
+      } else {
+        if (hi - lo <= 8u) pos = lb_pow2<8>(dk, lo, k);
+        else pos = lb_pow2<kFT>(dk, 0, k);
+        found = dk[pos] == k;
+      }
       const uint32_t prev_in = __shfl_up(pos, 1, 64);
       const int prev = lane == 0 ? carry : (int)prev_in;
-      const bool ok = act && (int)pos < nt && dk[pos] == k && prev < (int)pos;
+      const bool ok = act && (int)pos < nt && found && prev < (int)pos;
       if (ok) {
         const int lp = lastl[pos];
 #pragma unroll
@@ -211,16 +265,18 @@ __global__ __launch_bounds__(64, WPS) void stream2_kernel(const TileDesc* __rest
       return Lq;
     };
     // push p after its first window: keep streaming while windows are full
-    auto rest = [&](uint32_t p, uint32_t Lq, uint32_t c, uint32_t n, int& carry,
+    // (a window shorter than requested reached the coarse end)
+    auto rest = [&](uint32_t p, uint32_t Lq, uint32_t n, uint32_t W, int& carry,
                     uint32_t& fails) {
-      while (Lq == 64u && n == 64u) {
+      while (Lq == n && n == W) {
         uint64_t k2;
         V v2[M];
         uint32_t c2, n2;
-        load_window(k2, v2, c2, n2, p);
+        load_window(k2, v2, c2, n2, p, 64u);
         if (n2 == 0u) break;
         Lq = process(k2, v2, c2, n2, p, carry, fails);
         n = n2;
+        W = 64u;
       }
     };
     auto flush_fails = [&](uint32_t p, uint32_t fails) {
@@ -235,7 +291,7 @@ __global__ __launch_bounds__(64, WPS) void stream2_kernel(const TileDesc* __rest
         int carry = -1;
         uint32_t fails = 0;
         const uint32_t Lq = process(wk[q], wv[q], wc[q], wn[q], q, carry, fails);
-        rest(q, Lq, wc[q], wn[q], carry, fails);
+        rest(q, Lq, wn[q], first_w(q), carry, fails);
         flush_fails(q, fails);
       }
     }
@@ -243,7 +299,7 @@ __global__ __launch_bounds__(64, WPS) void stream2_kernel(const TileDesc* __rest
     for (uint32_t b0 = NPW; b0 < np; b0 += NPW) {
 #pragma unroll
       for (int q = 0; q < NPW; ++q) {
-        if (b0 + q < np) load_window(wk[q], wv[q], wc[q], wn[q], b0 + q);
+        if (b0 + q < np) load_window(wk[q], wv[q], wc[q], wn[q], b0 + q, first_w(b0 + q));
       }
 #pragma unroll
       for (int q = 0; q < NPW; ++q) {
@@ -251,7 +307,7 @@ __global__ __launch_bounds__(64, WPS) void stream2_kernel(const TileDesc* __rest
           int carry = -1;
           uint32_t fails = 0;
           const uint32_t Lq = process(wk[q], wv[q], wc[q], wn[q], b0 + q, carry, fails);
-          rest(b0 + q, Lq, wc[q], wn[q], carry, fails);
+          rest(b0 + q, Lq, wn[q], first_w(b0 + q), carry, fails);
           flush_fails(b0 + q, fails);
         }
       }
@@ -306,9 +362,9 @@ __global__ __launch_bounds__(64, WPS) void stream2_kernel(const TileDesc* __rest
   }
 }
 
-template <typename V, int M, int NPW, int WPS>
+template <typename V, int M, int NPW, int WPS, int SR = 0, int BTT = 0, int PR = 1>
 hipError_t go(const TileDesc* t, uint32_t n, hipStream_t s) {
-  hipLaunchKernelGGL((stream2_kernel<V, M, NPW, WPS>), dim3(n), dim3(64), 0, s, t);
+  hipLaunchKernelGGL((stream2_kernel<V, M, NPW, WPS, SR, BTT, PR>), dim3(n), dim3(64), 0, s, t);
   return hipGetLastError();
 }
 
@@ -320,12 +376,11 @@ hipError_t launch_s2m(const TileDesc* t, uint32_t n, hipStream_t s) {
       return e ? atoi(e) : 0;
     }();
     switch (variant) {
-      case 1: return go<V, M, 8, 1>(t, n, s);
-      case 2: return go<V, M, 4, 1>(t, n, s);
-      case 3: return go<V, M, 2, 1>(t, n, s);
-      case 4: return go<V, M, 4, 8>(t, n, s);
-      case 5: return go<V, M, 2, 8>(t, n, s);
-      case 6: return go<V, M, 4, 6>(t, n, s);
+      case 1: return go<V, M, 2, 8, 0, 0, 0>(t, n, s);  // 64-key first windows
+      case 2: return go<V, M, 2, 8, 1, 0, 1>(t, n, s);  // wide reads
+      case 3: return go<V, M, 2, 8, 0, 1, 1>(t, n, s);  // transitions
+      case 4: return go<V, M, 4, 8, 0, 0, 1>(t, n, s);
+      case 5: return go<V, M, 1, 8, 0, 0, 1>(t, n, s);
       default: break;
     }
   }

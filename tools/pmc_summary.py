@@ -16,8 +16,8 @@ def rows(pattern):
 
 
 def short(name):
-    for k in ("aggregate_v4_kernel", "aggregate_kernel", "partition_kernel", "gather_kernel",
-              "union", "slice_kernel"):
+    for k in ("stream2_kernel", "stream_kernel", "aggregate_v5_kernel", "aggregate_v4_kernel",
+              "aggregate_kernel", "partition_kernel", "gather_kernel", "union", "slice_kernel"):
         if k in name:
             return k
     return None
