@@ -142,15 +142,7 @@ def main():
     part_ms = float(np.mean([ev[s][0].elapsed_time(ev[s][1]) for s in range(K)]))
     agg_ms = float(np.mean([ev[s][1].elapsed_time(ev[s][2]) for s in range(K)]))
 
-    t = torch.tensor([wall], dtype=torch.float64, device=dev)
-    if dist:
-        dist.all_reduce(t, op=dist.ReduceOp.MAX)
-    wall_max = float(t.item())
-    kv_rank = plan.kv_pairs
-    kvt = torch.tensor([float(kv_rank)], dtype=torch.float64, device=dev)
-    if dist:
-        dist.all_reduce(kvt)
-    kv_all = float(kvt.item())
+    wall_max, kv_all = reduce_over_ranks(wall, plan.kv_pairs, dist, dev)
     value = kv_all * K / wall_max
     ms_per_step = wall_max / K * 1e3
 
@@ -226,6 +218,20 @@ def main():
         print(json.dumps(result), flush=True)
     if dist:
         dist.destroy_process_group()
+
+
+def reduce_over_ranks(wall, kv_rank, dist, dev):
+    """Whole-job timing: the slowest rank's wall time and the kv-pairs all
+    ranks merged (bench contract: value = all units / max-over-ranks time)."""
+    import torch
+    t = torch.tensor([wall, float(kv_rank)], dtype=torch.float64, device=dev)
+    if dist:
+        w = t[:1].clone()
+        dist.all_reduce(w, op=dist.ReduceOp.MAX)
+        k = t[1:].clone()
+        dist.all_reduce(k)
+        return float(w.item()), float(k.item())
+    return float(t[0].item()), float(t[1].item())
 
 
 def kernel_name():

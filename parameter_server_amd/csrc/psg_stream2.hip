@@ -119,14 +119,12 @@ __global__ __launch_bounds__(64, WPS) void stream2_kernel(const TileDesc* __rest
   }
   if (lane < 16) dk[kFT + lane] = ~0ull;
 
-  // window of push p at its cursor: W keys (lanes past the end hold ~0)
-  auto load_window = [&](uint64_t& wk, V (&wv)[M], uint32_t& wc, uint32_t& wn, uint32_t p,
-                         uint32_t W) {
+  // window of push p at its cursor: W keys; lanes past the coarse end hold
+  // ~0, which is never below a tile bound
+  auto load_window = [&](uint64_t& wk, V (&wv)[M], uint32_t p, uint32_t W) {
     const uint32_t c = (uint32_t)__builtin_amdgcn_readlane(cur, p);
     const uint32_t e = (uint32_t)__builtin_amdgcn_readlane(cend, p);
     const uint32_t n = e - c < W ? e - c : W;
-    wc = c;
-    wn = n;
     const uint64_t* sk = (const uint64_t*)readlane64(kp, p);
     const bool act = (uint32_t)lane < n;
     wk = act ? G(sk)[c + lane] : ~0ull;
@@ -158,11 +156,10 @@ __global__ __launch_bounds__(64, WPS) void stream2_kernel(const TileDesc* __rest
     const uint64_t bound = last_tile ? ~0ull : G(Dg)[base + kFT];
     uint64_t wk[NPW];
     V wv[NPW][M];
-    uint32_t wc[NPW], wn[NPW];
 #pragma unroll
     for (int q = 0; q < NPW; ++q) {
-      if ((uint32_t)q < np) load_window(wk[q], wv[q], wc[q], wn[q], q, first_w(q));
-      else { wk[q] = ~0ull; wn[q] = 0; wc[q] = 0; }
+      if ((uint32_t)q < np) load_window(wk[q], wv[q], q, first_w(q));
+      else wk[q] = ~0ull;
     }
 
     // ---- install the tile: D, accumulators, bucket table
@@ -210,9 +207,16 @@ __global__ __launch_bounds__(64, WPS) void stream2_kernel(const TileDesc* __rest
 
     // ---- one window of push p: its share of this tile, searched, checked,
     //      folded in arrival order.  Returns the window's in-tile count.
-    auto process = [&](uint64_t key, const V (&val)[M], uint32_t c, uint32_t n, uint32_t p,
-                       int& carry, uint32_t& fails) -> uint32_t {
-      const bool inb = (uint32_t)lane < n && (last_tile || key < bound);
+    auto process = [&](uint64_t key, const V (&val)[M], uint32_t p, uint32_t W, int& carry,
+                       uint32_t& fails) -> uint32_t {
+      bool inb;
+      if (last_tile) {  // the rest of the coarse range: every loaded key
+        const uint32_t c = (uint32_t)__builtin_amdgcn_readlane(cur, p);
+        const uint32_t e = (uint32_t)__builtin_amdgcn_readlane(cend, p);
+        inb = (uint32_t)lane < (e - c < W ? e - c : W);
+      } else {
+        inb = key < bound;
+      }
       const unsigned long long bal = __ballot(inb);
       const uint32_t Lq = (~bal == 0ull) ? 64u : (uint32_t)__builtin_ctzll(~bal);
       const bool act = (uint32_t)lane < Lq;
@@ -261,21 +265,17 @@ __global__ __launch_bounds__(64, WPS) void stream2_kernel(const TileDesc* __rest
       }
       if (Lq > 0) carry = (int)__shfl(pos, (int)Lq - 1, 64);
       fails += (uint32_t)__popcll(__ballot(act && !ok));
-      if (lane == (int)p) cur = c + Lq;
+      if (lane == (int)p) cur += Lq;
       return Lq;
     };
-    // push p after its first window: keep streaming while windows are full
-    // (a window shorter than requested reached the coarse end)
-    auto rest = [&](uint32_t p, uint32_t Lq, uint32_t n, uint32_t W, int& carry,
-                    uint32_t& fails) {
-      while (Lq == n && n == W) {
+    // push p after its first window: keep streaming while a whole window
+    // fell in the tile (a short window -- sentinel lanes -- reached the end)
+    auto rest = [&](uint32_t p, uint32_t Lq, uint32_t W, int& carry, uint32_t& fails) {
+      while (Lq == W) {
         uint64_t k2;
         V v2[M];
-        uint32_t c2, n2;
-        load_window(k2, v2, c2, n2, p, 64u);
-        if (n2 == 0u) break;
-        Lq = process(k2, v2, c2, n2, p, carry, fails);
-        n = n2;
+        load_window(k2, v2, p, 64u);
+        Lq = process(k2, v2, p, 64u, carry, fails);
         W = 64u;
       }
     };
@@ -290,8 +290,8 @@ __global__ __launch_bounds__(64, WPS) void stream2_kernel(const TileDesc* __rest
       if ((uint32_t)q < np) {
         int carry = -1;
         uint32_t fails = 0;
-        const uint32_t Lq = process(wk[q], wv[q], wc[q], wn[q], q, carry, fails);
-        rest(q, Lq, wn[q], first_w(q), carry, fails);
+        const uint32_t Lq = process(wk[q], wv[q], q, first_w(q), carry, fails);
+        rest(q, Lq, first_w(q), carry, fails);
         flush_fails(q, fails);
       }
     }
@@ -299,15 +299,15 @@ __global__ __launch_bounds__(64, WPS) void stream2_kernel(const TileDesc* __rest
     for (uint32_t b0 = NPW; b0 < np; b0 += NPW) {
 #pragma unroll
       for (int q = 0; q < NPW; ++q) {
-        if (b0 + q < np) load_window(wk[q], wv[q], wc[q], wn[q], b0 + q, first_w(b0 + q));
+        if (b0 + q < np) load_window(wk[q], wv[q], b0 + q, first_w(b0 + q));
       }
 #pragma unroll
       for (int q = 0; q < NPW; ++q) {
         if (b0 + q < np) {
           int carry = -1;
           uint32_t fails = 0;
-          const uint32_t Lq = process(wk[q], wv[q], wc[q], wn[q], b0 + q, carry, fails);
-          rest(b0 + q, Lq, wn[q], first_w(b0 + q), carry, fails);
+          const uint32_t Lq = process(wk[q], wv[q], b0 + q, first_w(b0 + q), carry, fails);
+          rest(b0 + q, Lq, first_w(b0 + q), carry, fails);
           flush_fails(b0 + q, fails);
         }
       }
@@ -381,6 +381,8 @@ hipError_t launch_s2m(const TileDesc* t, uint32_t n, hipStream_t s) {
       case 3: return go<V, M, 2, 8, 0, 1, 1>(t, n, s);  // transitions
       case 4: return go<V, M, 4, 8, 0, 0, 1>(t, n, s);
       case 5: return go<V, M, 1, 8, 0, 0, 1>(t, n, s);
+      case 6: return go<V, M, 8, 7, 0, 0, 1>(t, n, s);
+      case 7: return go<V, M, 4, 8, 0, 0, 0>(t, n, s);
       default: break;
     }
   }

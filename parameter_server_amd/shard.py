@@ -79,9 +79,9 @@ def exchange_pieces(pushes, bounds, dist, device=None):
 
 
 def exchange_unsliced(args, rank, world, bounds, dist):
-    """bench.py --ingress unsliced: each rank draws `batch` whole aggregates
-    (keys over the full key space), re-homes their pieces, and returns the
-    per-(source, aggregate) jobs of its own shard."""
+    """bench.py --ingress unsliced: each rank draws its pushes of `batch`
+    aggregates (keys over the full key space), re-homes their pieces, and
+    returns for each aggregate its shard's job (all sources' pieces)."""
     import torch
     from . import synth
     dev = torch.device("cuda", torch.cuda.current_device())
@@ -89,10 +89,9 @@ def exchange_unsliced(args, rank, world, bounds, dist):
     for j in range(args.batch):
         D, pushes = synth.overlap_pushes(1 + j + 1000 * rank, args.npush, args.n, args.overlap)
         per_src = exchange_pieces(pushes, bounds, dist, dev)
-        for pieces in per_src:
-            pieces = [pc for pc in pieces if pc[0].size]
-            if not pieces:
-                continue
+        # one aggregate per j: every source's pieces, in (source, push) order
+        pieces = [pc for src in per_src for pc in src if pc[0].size]
+        if pieces:
             Dsh = np.unique(np.concatenate([k for k, _ in pieces]))
             jobs.append((Dsh, pieces))
     return jobs

@@ -1,0 +1,17 @@
+#!/bin/bash
+# GPU box: the round's committed evidence.  usage: tools/profile_round.sh r01
+#   bench.json   default bench line (N=1, with end-to-end + CPU baseline)
+#   ktrace/      rocprofv3 --kernel-trace --stats of a bench run (same config)
+#   pmc2/k7S/    FETCH_SIZE / WRITE_SIZE / TCC passes (tools/pmc2.sh)
+# Every GPU step has its own time limit; the first failure ends the script.
+set -o pipefail
+export TMPDIR=/tmp
+R=${1:-r01}
+OUT=gpurun_out/$R
+mkdir -p $OUT
+timeout -k 10 600 python3 bench.py > $OUT/bench.json 2> $OUT/bench.err || { echo "bench failed"; tail -5 $OUT/bench.err; exit 1; }
+cat $OUT/bench.json
+timeout -k 10 600 rocprofv3 --kernel-trace --stats --output-format csv -d $OUT/ktrace -o run -- python3 bench.py --no-cpu-baseline > $OUT/ktrace.json 2> $OUT/ktrace.err || { echo "ktrace failed"; tail -5 $OUT/ktrace.err; exit 1; }
+PASSES="1 2 3" ./tools/pmc2.sh "7:S" || exit 1
+rm -rf $OUT/pmc && mv gpurun_out/pmc2/k7S $OUT/pmc
+echo done
