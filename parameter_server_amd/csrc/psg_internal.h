@@ -71,6 +71,10 @@ hipError_t launch_aggregate_stream(int dtype, int m, const TileDesc* d_tiles,
                                    uint32_t ncoarse, hipStream_t stream);
 hipError_t launch_aggregate_stream2(int dtype, int m, const TileDesc* d_tiles,
                                     uint32_t ncoarse, hipStream_t stream);
+hipError_t launch_aggregate_stream3(int dtype, int m, const TileDesc* d_tiles,
+                                    uint32_t ncoarse, hipStream_t stream);
+hipError_t launch_aggregate_stream4(int dtype, int m, const TileDesc* d_tiles,
+                                    uint32_t ncoarse, uint32_t maxnp, hipStream_t stream);
 hipError_t launch_gather(int dtype, const uint64_t* dkeys, uint64_t nd,
                          const void* dvals, const uint64_t* req, uint64_t nreq,
                          void* out, unsigned long long* matched,

@@ -68,7 +68,7 @@ struct JobSpec {
 
 struct JobTable {
   int device = -1;
-  int dtype = 0, m = 1, geo = psg::kGeoS, kernel = 7;
+  int dtype = 0, m = 1, geo = psg::kGeoS, kernel = 9;
   std::vector<JobDev> h;
   std::vector<uint64_t> nslots;
   std::vector<uint32_t*> seg_first;  // device row 0 of each job's seg
@@ -107,7 +107,7 @@ struct JobTable {
     geo = pick_geometry();
     {
       const char* k = getenv("PSG_KERNEL");  // 2 = one-tile-per-workgroup kernel
-      kernel = (k && k[0] >= '2' && k[0] <= '7' && k[0] != '3') ? k[0] - '0' : 7;
+      kernel = (k && k[0] >= '2' && k[0] <= '9' && k[0] != '3') ? k[0] - '0' : 9;
     }
     uint32_t maxnp_all = 0;
     for (const JobSpec& s : jobs) maxnp_all = std::max(maxnp_all, (uint32_t)s.pn.size());
@@ -222,6 +222,10 @@ struct JobTable {
       HIP_TRY(psg::launch_partition(d_jobs, d_item_job, nitems, s));
     else if (kernel == 2)
       HIP_TRY(psg::launch_aggregate(dtype, m, geo, d_tiles, ntiles, maxnp, s));
+    else if (kernel == 9)
+      HIP_TRY(psg::launch_aggregate_stream4(dtype, m, d_tiles, ntiles, maxnp, s));
+    else if (kernel == 8)
+      HIP_TRY(psg::launch_aggregate_stream3(dtype, m, d_tiles, ntiles, s));
     else if (kernel == 7)
       HIP_TRY(psg::launch_aggregate_stream2(dtype, m, d_tiles, ntiles, s));
     else if (kernel == 6)
@@ -239,16 +243,20 @@ struct JobTable {
   }
 
   // matched[p] = (covered elements) - (in-tile failures); stream must be idle.
+  // A job's fail counters and seg rows are adjacent in the blob: one copy.
   int matched(std::vector<uint64_t>& out) const {
     out.clear();
+    std::vector<char> buf;
     for (size_t j = 0; j < h.size(); ++j) {
       const uint32_t np = npush[j];
       if (np == 0) continue;
-      std::vector<uint32_t> first(np), last(np);
-      std::vector<unsigned long long> f(np);
-      HIP_TRY(hipMemcpy(first.data(), seg_first[j], 4 * np, hipMemcpyDeviceToHost));
-      HIP_TRY(hipMemcpy(last.data(), seg_last[j], 4 * np, hipMemcpyDeviceToHost));
-      HIP_TRY(hipMemcpy(f.data(), fails[j], 8 * np, hipMemcpyDeviceToHost));
+      const char* f0 = (const char*)fails[j];
+      const char* end = (const char*)(seg_last[j] + np);
+      buf.resize(end - f0);
+      HIP_TRY(hipMemcpy(buf.data(), f0, buf.size(), hipMemcpyDeviceToHost));
+      const unsigned long long* f = (const unsigned long long*)buf.data();
+      const uint32_t* first = (const uint32_t*)(buf.data() + ((const char*)seg_first[j] - f0));
+      const uint32_t* last = (const uint32_t*)(buf.data() + ((const char*)seg_last[j] - f0));
       for (uint32_t p = 0; p < np; ++p) {
         const uint64_t covered = nslots[j] ? (uint64_t)(last[p] - first[p]) : 0;
         out.push_back(covered >= f[p] ? covered - f[p] : 0);
@@ -286,6 +294,7 @@ struct PendingPush {
   uint64_t* d_keys = nullptr;      // keys then values in one allocation
   void* d_vals[psg::kMaxM] = {};
   uint64_t n = 0;
+  size_t bytes = 0;
 };
 
 struct Aggregate {
@@ -313,6 +322,39 @@ struct psg_ctx {
   void* scratch = nullptr;
   size_t scratch_bytes = 0;
   size_t flush_pushes = psg::kMaxPush;  // pushes per aggregate launch
+  // Freed push-staging and aggregate blocks, by size: a server sees the same
+  // shapes every iteration, so after the first one no push allocates.
+  std::multimap<size_t, void*> pool;
+  size_t pool_bytes = 0;
+  static constexpr size_t kPoolCap = size_t(8) << 30;
+
+  int dev_get(size_t b, void** p) {
+    b = align_up(b ? b : 1, 4096);
+    auto it = pool.lower_bound(b);
+    if (it != pool.end() && it->first <= 2 * b) {
+      *p = it->second;
+      pool_bytes -= it->first;
+      pool.erase(it);
+      return PSG_OK;
+    }
+    HIP_TRY(hipMalloc(p, b));
+    return PSG_OK;
+  }
+  void dev_put(void* p, size_t b) {
+    if (!p) return;
+    b = align_up(b ? b : 1, 4096);
+    if (pool_bytes + b > kPoolCap) {
+      (void)hipFree(p);
+      return;
+    }
+    pool.emplace(b, p);
+    pool_bytes += b;
+  }
+  void pool_release() {
+    for (auto& kv : pool) (void)hipFree(kv.second);
+    pool.clear();
+    pool_bytes = 0;
+  }
 
   int ensure_scratch(size_t b) {
     if (b <= scratch_bytes) return PSG_OK;
@@ -351,7 +393,7 @@ struct psg_ctx {
       for (size_t p = 0; p < take; ++p) {
         a.matched_total += mt[p];
         if (mt[p] != a.pending[p].n) a.unmatched = true;
-        HIP_TRY(hipFree(a.pending[p].d_keys));
+        dev_put(a.pending[p].d_keys, a.pending[p].bytes);
       }
       a.pending.erase(a.pending.begin(), a.pending.begin() + take);
       a.folded += take;
@@ -566,6 +608,7 @@ int psg_destroy(psg_ctx* c) {
     (void)hipFree(kv.second.d_vals);
   }
   c->table.release();
+  c->pool_release();
   (void)hipFree(c->d_counter);
   (void)hipFree(c->scratch);
   (void)hipStreamDestroy(c->stream);
@@ -722,7 +765,8 @@ int psg_push(psg_ctx* c, int chl, int time, uint64_t kb, uint64_t ke,
   PendingPush pp;
   pp.n = n;
   const size_t kbytes = align_up(8 * n, 256), vbytes = align_up(sv * n, 256);
-  HIP_TRY(hipMalloc(&pp.d_keys, kbytes + m * vbytes));
+  pp.bytes = kbytes + m * vbytes;
+  if (int rc = c->dev_get(pp.bytes, (void**)&pp.d_keys)) return rc;
   HIP_TRY(hipMemcpyAsync(pp.d_keys, keys, 8 * n, hipMemcpyHostToDevice, c->stream));
   for (int i = 0; i < m; ++i) {
     pp.d_vals[i] = (char*)pp.d_keys + kbytes + i * vbytes;
@@ -737,7 +781,8 @@ int psg_push(psg_ctx* c, int chl, int time, uint64_t kb, uint64_t ke,
     A.lo = lo;
     A.hi = hi;
     for (int i = 0; i < m; ++i)
-      if (hi > lo) HIP_TRY(hipMalloc(&A.d_out[i], (hi - lo) * sv));
+      if (hi > lo)
+        if (int rc = c->dev_get((hi - lo) * sv, &A.d_out[i])) return rc;
     ait = c->agg.emplace(time, A).first;
   }
   Aggregate& A = ait->second;
@@ -779,8 +824,8 @@ int psg_received(psg_ctx* c, int time, int m, void* const* out) {
   }
   const bool bad = A.unmatched;
   const unsigned long long got = A.matched_total, want = A.expected_total;
-  for (auto& pp : A.pending) (void)hipFree(pp.d_keys);
-  for (int i = 0; i < A.m; ++i) (void)hipFree(A.d_out[i]);
+  for (auto& pp : A.pending) c->dev_put(pp.d_keys, pp.bytes);
+  for (int i = 0; i < A.m; ++i) c->dev_put(A.d_out[i], (A.hi - A.lo) * sv);
   c->agg.erase(it);
   if (rc) return rc;
   if (bad)

@@ -40,7 +40,7 @@ namespace psg {
 namespace {
 
 constexpr int kFT = 256;   // fine tile slots (4 per lane)
-constexpr int kNB = 64;    // buckets per fine tile
+constexpr int kMaxNB = 256;  // buckets per fine tile (template LNB: 64..256)
 
 template <typename T>
 __device__ __forceinline__ const AS1 T* G(const T* p) {
@@ -79,11 +79,19 @@ __device__ __forceinline__ V fold1(V acc, int lp, int p, V v, bool parallel,
   return (p == 0 && !cont) ? v : a1 + v;
 }
 
-// SR: slot search by dependent probes (0) or one round of wide window reads (1)
+// SR: slot search by dependent probes from the bucket start (0), one round
+//     of wide window reads (1), or last-key-<=-k lifting over 8 candidates
+//     with the value carried (2: 3 dependent LDS levels, no re-read)
 // BTT: bucket table by per-bucket searches (0) or slot transitions (1)
 // PR: first window of a push per tile sized by its expected share (1) or 64 (0)
-template <typename V, int M, int NPW, int WPS, int SR = 0, int BTT = 0, int PR = 1>
+// LNB: log2 of the buckets per fine tile
+// DG: diagnostic ablation (benchmarking only, results invalid): 1 = no fold,
+//     2 = no search and no fold
+template <typename V, int M, int NPW, int WPS, int SR = 0, int BTT = 0, int PR = 1, int LNB = 6,
+          int DG = 0>
 __global__ __launch_bounds__(64, WPS) void stream2_kernel(const TileDesc* __restrict__ tiles) {
+  constexpr int kNB = 1 << LNB;
+  static_assert(kNB <= kMaxNB, "bucket table");
   __shared__ __attribute__((aligned(16))) uint64_t dk[kFT + 16];
   __shared__ V acc[M * kFT];
   __shared__ int16_t lastl[kFT];
@@ -118,6 +126,13 @@ __global__ __launch_bounds__(64, WPS) void stream2_kernel(const TileDesc* __rest
     }
   }
   if (lane < 16) dk[kFT + lane] = ~0ull;
+  V* outb[M];
+#pragma unroll
+  for (int mi = 0; mi < M; ++mi) outb[mi] = (V*)G(T.out)[mi] + T.slot0;
+  // Retire the set-up loads here: left pending into the tile loop, they make
+  // the compiler's wait insertion put a vmcnt(0) in front of every window
+  // load (the per-push cursors read by readlane), serialising round trips.
+  __builtin_amdgcn_s_waitcnt(0);
 
   // window of push p at its cursor: W keys; lanes past the coarse end hold
   // ~0, which is never below a tile bound
@@ -141,7 +156,7 @@ __global__ __launch_bounds__(64, WPS) void stream2_kernel(const TileDesc* __rest
     const bool last_tile = ft + 1 == nft;
     V* outp[M];
 #pragma unroll
-    for (int mi = 0; mi < M; ++mi) outp[mi] = (V*)T.out[mi] + T.slot0 + base;
+    for (int mi = 0; mi < M; ++mi) outp[mi] = outb[mi] + base;
 
     auto first_w = [&](uint32_t p) -> uint32_t {
       return PR ? (uint32_t)__builtin_amdgcn_readlane(pred, p) : 64u;
@@ -178,12 +193,15 @@ __global__ __launch_bounds__(64, WPS) void stream2_kernel(const TileDesc* __rest
         ((uint64_t)(uint32_t)__builtin_amdgcn_readfirstlane((uint32_t)(dreg[0] >> 32)) << 32);
     const uint64_t range = dk[nt - 1] - klo;
     const int bits = range ? 64 - __builtin_clzll(range) : 0;
-    const int shift = bits > 6 ? bits - 6 : 0;
+    const int shift = bits > LNB ? bits - LNB : 0;
     if constexpr (BTT == 0) {
-      const uint64_t d = (uint64_t)lane << shift;
-      const uint64_t key = d > ~0ull - klo ? ~0ull : klo + d;
-      const uint32_t sb = lb_pow2<kFT>(dk, 0, key);
-      btab[lane] = sb < (uint32_t)nt ? sb : (uint32_t)nt;
+#pragma unroll
+      for (int r = 0; r < kNB / 64; ++r) {
+        const uint64_t d = (uint64_t)(lane + 64 * r) << shift;
+        const uint64_t key = d > ~0ull - klo ? ~0ull : klo + d;
+        const uint32_t sb = lb_pow2<kFT>(dk, 0, key);
+        btab[lane + 64 * r] = sb < (uint32_t)nt ? sb : (uint32_t)nt;
+      }
       if (lane == 0) btab[kNB] = (uint32_t)nt;
     } else {
       // btab[b] = first slot whose bucket >= b: a slot opens the buckets
@@ -229,7 +247,30 @@ __global__ __launch_bounds__(64, WPS) void stream2_kernel(const TileDesc* __rest
       const uint32_t hi = btab[b < (uint32_t)kNB ? b + 1 : b];
       uint32_t pos;
       bool found;
-      if constexpr (SR == 1) {
+      if constexpr (DG >= 2) {
+        pos = (uint32_t)lane * 4u + (lo & 1u);
+        found = act;
+      } else if constexpr (SR == 2) {
+        // last slot with key <= k among lo..lo+7, its key carried along;
+        // dk is ~0 past the tile, so the candidates never leave the array
+        uint64_t val;
+        if (hi - lo <= 8u) {
+          const uint64_t v0 = dk[lo], v4 = dk[lo + 4];
+          uint32_t j = v4 <= k ? lo + 4 : lo;
+          val = v4 <= k ? v4 : v0;
+          const uint64_t v2 = dk[j + 2];
+          j = v2 <= k ? j + 2 : j;
+          val = v2 <= k ? v2 : val;
+          const uint64_t v1 = dk[j + 1];
+          j = v1 <= k ? j + 1 : j;
+          val = v1 <= k ? v1 : val;
+          pos = j;
+        } else {
+          pos = lb_pow2<kFT>(dk, 0, k);
+          val = dk[pos];
+        }
+        found = val == k;
+      } else if constexpr (SR == 1) {
         if (hi - lo <= 8u) {
           // one round of 5 independent 16-byte reads covers [lo, lo+8]
           const uint32_t w0 = lo & ~1u;
@@ -254,9 +295,9 @@ __global__ __launch_bounds__(64, WPS) void stream2_kernel(const TileDesc* __rest
         found = dk[pos] == k;
       }
       const uint32_t prev_in = __shfl_up(pos, 1, 64);
-      const int prev = lane == 0 ? carry : (int)prev_in;
+      const int prev = DG >= 2 ? -1 : lane == 0 ? carry : (int)prev_in;
       const bool ok = act && (int)pos < nt && found && prev < (int)pos;
-      if (ok) {
+      if (DG == 0 && ok) {
         const int lp = lastl[pos];
 #pragma unroll
         for (int mi = 0; mi < M; ++mi)
@@ -362,9 +403,11 @@ __global__ __launch_bounds__(64, WPS) void stream2_kernel(const TileDesc* __rest
   }
 }
 
-template <typename V, int M, int NPW, int WPS, int SR = 0, int BTT = 0, int PR = 1>
+template <typename V, int M, int NPW, int WPS, int SR = 0, int BTT = 0, int PR = 1, int LNB = 6,
+          int DG = 0>
 hipError_t go(const TileDesc* t, uint32_t n, hipStream_t s) {
-  hipLaunchKernelGGL((stream2_kernel<V, M, NPW, WPS, SR, BTT, PR>), dim3(n), dim3(64), 0, s, t);
+  hipLaunchKernelGGL((stream2_kernel<V, M, NPW, WPS, SR, BTT, PR, LNB, DG>), dim3(n), dim3(64), 0,
+                     s, t);
   return hipGetLastError();
 }
 
@@ -381,8 +424,13 @@ hipError_t launch_s2m(const TileDesc* t, uint32_t n, hipStream_t s) {
       case 3: return go<V, M, 2, 8, 0, 1, 1>(t, n, s);  // transitions
       case 4: return go<V, M, 4, 8, 0, 0, 1>(t, n, s);
       case 5: return go<V, M, 1, 8, 0, 0, 1>(t, n, s);
-      case 6: return go<V, M, 8, 7, 0, 0, 1>(t, n, s);
+      case 6: return go<V, M, 4, 8, 2, 0, 0, 7>(t, n, s);  // last<=k search, 128 buckets
       case 7: return go<V, M, 4, 8, 0, 0, 0>(t, n, s);
+      case 8: return go<V, M, 4, 8, 2, 0, 0, 8>(t, n, s);  // 256 buckets
+      case 9: return go<V, M, 2, 8, 2, 0, 0, 7>(t, n, s);
+      case 10: return go<V, M, 4, 8, 0, 0, 0, 7>(t, n, s);
+      case 21: return go<V, M, 4, 8, 0, 0, 0, 7, 1>(t, n, s);  // ablations of 10
+      case 22: return go<V, M, 4, 8, 0, 0, 0, 7, 2>(t, n, s);
       default: break;
     }
   }
