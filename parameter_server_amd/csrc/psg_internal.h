@@ -51,7 +51,10 @@ struct TileDesc {
   uint32_t nt;                    // slots in this tile (<= tile)
   uint32_t np;                    // pushes of the job
   uint32_t flags;
-  uint32_t pad;
+  // rows kernel: this tile's slot offset inside its partition range (low
+  // 16 bits) and that range's slot count (high 16 bits); the tile's own
+  // push boundaries are searched inside the range's segments
+  uint32_t sub;
 };
 
 // Kernel launchers (psg_kernels.hip).  All enqueue on `stream` only.
@@ -75,6 +78,11 @@ hipError_t launch_aggregate_stream3(int dtype, int m, const TileDesc* d_tiles,
                                     uint32_t ncoarse, hipStream_t stream);
 hipError_t launch_aggregate_stream4(int dtype, int m, const TileDesc* d_tiles,
                                     uint32_t ncoarse, uint32_t maxnp, hipStream_t stream);
+// rows kernel (v10): one wave per coarse tile of rows_tile() slots, np <= 64
+int rows_tile();
+constexpr int kRowsInlineMaxPush = 16;  // above: partition at the rows tile itself
+hipError_t launch_aggregate_rows(int dtype, int m, const TileDesc* d_tiles, uint32_t ncoarse,
+                                 hipStream_t stream);
 hipError_t launch_gather(int dtype, const uint64_t* dkeys, uint64_t nd,
                          const void* dvals, const uint64_t* req, uint64_t nreq,
                          void* out, unsigned long long* matched,

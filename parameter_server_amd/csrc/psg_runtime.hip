@@ -107,13 +107,22 @@ struct JobTable {
     geo = pick_geometry();
     {
       const char* k = getenv("PSG_KERNEL");  // 2 = one-tile-per-workgroup kernel
-      kernel = (k && k[0] >= '2' && k[0] <= '9' && k[0] != '3') ? k[0] - '0' : 9;
+      const int kk = k ? atoi(k) : 0;
+      kernel = (kk >= 2 && kk <= 10 && kk != 3) ? kk : 9;
     }
     uint32_t maxnp_all = 0;
     for (const JobSpec& s : jobs) maxnp_all = std::max(maxnp_all, (uint32_t)s.pn.size());
     if (kernel >= 6 && maxnp_all > (uint32_t)psg::kStreamMaxPush) kernel = 4;  // many pushes
+    // ktile: slots per aggregate-kernel tile; tile: partition granularity.
+    // The rows kernel (10) searches its own tile boundaries inside coarse
+    // partition ranges when the pushes are few enough.
+    const uint32_t ktile = kernel == 10 ? (uint32_t)psg::rows_tile()
+                           : kernel >= 6 ? (uint32_t)psg::kStreamTile
+                                         : (uint32_t)psg::geo_tile(geo);
     const uint32_t tile =
-        kernel >= 6 ? (uint32_t)psg::kStreamTile : (uint32_t)psg::geo_tile(geo);
+        (kernel == 10 && maxnp_all <= (uint32_t)psg::kRowsInlineMaxPush)
+            ? std::max<uint32_t>(ktile, (uint32_t)psg::kStreamTile)
+            : ktile;
     h.clear();
     nslots.clear();
     seg_first.clear();
@@ -133,7 +142,7 @@ struct JobTable {
         if (s.pn[p] >= (1ull << 32))
           return fail(PSG_ERR_ARG, "push of %llu keys >= 2^32", (unsigned long long)s.pn[p]);
       const uint64_t nt = (s.nslots + tile - 1) / tile;
-      tiles += nt;
+      tiles += (s.nslots + ktile - 1) / ktile;
       items += ((nt + 64) / 64) * np;  // partition: one wave per 64 boundaries
       if (tiles >= (1ull << 31) || items >= (1ull << 31))
         return fail(PSG_ERR_ARG, "batch too large (%llu tiles)", (unsigned long long)tiles);
@@ -187,18 +196,23 @@ struct JobTable {
       d.tile = tile;
       h.push_back(d);
       for (uint64_t b = 0; b < ((nt + 64) / 64) * np; ++b) hitems[icur++] = (uint32_t)j;
-      for (uint64_t t = 0; t < nt; ++t) {
+      const uint64_t nkt = (s.nslots + ktile - 1) / ktile;
+      for (uint64_t t = 0; t < nkt; ++t) {
         psg::TileDesc& T = htiles[tcur++];
-        T.dk = s.keys + t * tile;
-        T.seg = d.seg + t * np;
+        const uint64_t slot0 = t * ktile;
+        const uint64_t pt = slot0 / tile;  // partition range holding the tile
+        T.dk = s.keys + slot0;
+        T.seg = d.seg + pt * np;
         T.pkeys = d.pkeys;
         T.pvals = (const void* const*)(base + o.pv);
         T.out = (void* const*)(base + o.out);
         T.fail = d.fail;
-        T.slot0 = t * tile;
-        T.nt = (uint32_t)std::min<uint64_t>(tile, s.nslots - t * tile);
+        T.slot0 = slot0;
+        T.nt = (uint32_t)std::min<uint64_t>(ktile, s.nslots - slot0);
         T.np = np;
         T.flags = s.flags;
+        const uint64_t pslots = std::min<uint64_t>(tile, s.nslots - pt * tile);
+        T.sub = (uint32_t)(slot0 - pt * tile) | ((uint32_t)pslots << 16);
       }
       nslots.push_back(s.nslots);
       seg_first.push_back(d.seg);
@@ -222,6 +236,8 @@ struct JobTable {
       HIP_TRY(psg::launch_partition(d_jobs, d_item_job, nitems, s));
     else if (kernel == 2)
       HIP_TRY(psg::launch_aggregate(dtype, m, geo, d_tiles, ntiles, maxnp, s));
+    else if (kernel == 10)
+      HIP_TRY(psg::launch_aggregate_rows(dtype, m, d_tiles, ntiles, s));
     else if (kernel == 9)
       HIP_TRY(psg::launch_aggregate_stream4(dtype, m, d_tiles, ntiles, maxnp, s));
     else if (kernel == 8)

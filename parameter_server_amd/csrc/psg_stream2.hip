@@ -194,7 +194,9 @@ __global__ __launch_bounds__(64, WPS) void stream2_kernel(const TileDesc* __rest
     const uint64_t range = dk[nt - 1] - klo;
     const int bits = range ? 64 - __builtin_clzll(range) : 0;
     const int shift = bits > LNB ? bits - LNB : 0;
-    if constexpr (BTT == 0) {
+    if constexpr (DG >= 3) {
+      if (lane == 0) btab[kNB] = (uint32_t)nt;
+    } else if constexpr (BTT == 0) {
 #pragma unroll
       for (int r = 0; r < kNB / 64; ++r) {
         const uint64_t d = (uint64_t)(lane + 64 * r) << shift;
@@ -431,6 +433,7 @@ hipError_t launch_s2m(const TileDesc* t, uint32_t n, hipStream_t s) {
       case 10: return go<V, M, 4, 8, 0, 0, 0, 7>(t, n, s);
       case 21: return go<V, M, 4, 8, 0, 0, 0, 7, 1>(t, n, s);  // ablations of 10
       case 22: return go<V, M, 4, 8, 0, 0, 0, 7, 2>(t, n, s);
+      case 23: return go<V, M, 4, 8, 0, 0, 0, 7, 3>(t, n, s);  // + no bucket table
       default: break;
     }
   }
