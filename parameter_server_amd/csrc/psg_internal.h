@@ -80,7 +80,8 @@ hipError_t launch_aggregate_stream4(int dtype, int m, const TileDesc* d_tiles,
                                     uint32_t ncoarse, uint32_t maxnp, hipStream_t stream);
 // rows kernel (v10): one wave per coarse tile of rows_tile() slots, np <= 64
 int rows_tile();
-constexpr int kRowsInlineMaxPush = 16;  // above: partition at the rows tile itself
+constexpr int kRowsInlinePush = 8;  // pushes whose sub-tile boundaries the rows kernel searches
+constexpr int kRowsMaxSub = 4;      // sub-tiles per rows-kernel wave (span)
 hipError_t launch_aggregate_rows(int dtype, int m, const TileDesc* d_tiles, uint32_t ncoarse,
                                  hipStream_t stream);
 hipError_t launch_gather(int dtype, const uint64_t* dkeys, uint64_t nd,

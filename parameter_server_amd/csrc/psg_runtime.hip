@@ -116,13 +116,18 @@ struct JobTable {
     // ktile: slots per aggregate-kernel tile; tile: partition granularity.
     // The rows kernel (10) searches its own tile boundaries inside coarse
     // partition ranges when the pushes are few enough.
-    const uint32_t ktile = kernel == 10 ? (uint32_t)psg::rows_tile()
-                           : kernel >= 6 ? (uint32_t)psg::kStreamTile
-                                         : (uint32_t)psg::geo_tile(geo);
-    const uint32_t tile =
-        (kernel == 10 && maxnp_all <= (uint32_t)psg::kRowsInlineMaxPush)
-            ? std::max<uint32_t>(ktile, (uint32_t)psg::kStreamTile)
-            : ktile;
+    // ktile: slots per aggregate-kernel tile (the rows kernel: a span of
+    // sub-tiles); tile: partition granularity.  With few pushes the rows
+    // kernel searches its sub-tile boundaries inside coarse partition ranges.
+    const bool rows_inline =
+        kernel == 10 && maxnp_all <= (uint32_t)psg::kRowsInlinePush;
+    const uint32_t ktile =
+        kernel == 10 ? (rows_inline ? std::min<uint32_t>((uint32_t)psg::kStreamTile,
+                                                         psg::kRowsMaxSub * psg::rows_tile())
+                                    : (uint32_t)psg::rows_tile())
+        : kernel >= 6 ? (uint32_t)psg::kStreamTile
+                      : (uint32_t)psg::geo_tile(geo);
+    const uint32_t tile = rows_inline ? (uint32_t)psg::kStreamTile : ktile;
     h.clear();
     nslots.clear();
     seg_first.clear();
