@@ -7,8 +7,8 @@
 // SArray::findRange (src/base/shared_array_inl.h:164-171).
 //
 // Two launches per batch of jobs:
-//   partition: one wave per (job, tile boundary, push): 64-ary search of
-//              the tile's first server key in the push (3 rounds at 128 K).
+//   partition: one lane per (job, tile boundary, push): interpolation search
+//              of the tile's first server key in the push.
 //   aggregate: one workgroup per tile of server slots:
 //     1. one scalar round trip for the TileDesc; then the D tile, the
 //        tile's push segments and the push pointers load together;
@@ -36,49 +36,14 @@ namespace {
 
 constexpr uint32_t kInvalid = 0xFFFFFFFFu;
 
-// Two concurrent 32-ary searches (lanes 0-31: key a, lanes 32-63: key b):
-// first index whose key is >= k (or > k when `up`), per half-wave.
-__device__ __forceinline__ void wave_search2(const uint64_t* __restrict__ S,
-                                             uint64_t n, uint64_t ka, bool ua,
-                                             uint64_t kb, bool ub, int lane,
-                                             uint64_t* ra, uint64_t* rb) {
-  const int h = lane >> 5, hl = lane & 31;
-  const uint64_t key = h ? kb : ka;
-  const bool up = h ? ub : ua;
-  uint64_t lo = 0, hi = n;  // answer in [lo, hi]
-  for (;;) {
-    const bool active = hi > lo;
-    if (__ballot(active) == 0ull) break;
-    const uint64_t len = hi - lo;
-    const uint64_t step = (len + 31) >> 5;
-    const uint64_t idx = lo + (uint64_t)(hl + 1) * step - 1;
-    bool pred = true;
-    if (active && idx < hi) {
-      const uint64_t s = S[idx];
-      pred = up ? (s > key) : (s >= key);
-    }
-    const unsigned long long m = __ballot(pred);
-    const uint32_t mh = (uint32_t)(m >> (32 * h));
-    if (active) {
-      if (mh == 0u) {
-        lo = hi;
-      } else {
-        const uint64_t f = (uint64_t)(__ffs(mh) - 1);
-        const uint64_t nhi = lo + (f + 1) * step - 1;
-        lo = lo + f * step;
-        hi = nhi < hi ? nhi : hi;
-      }
-    }
-  }
-  *ra = __shfl(lo, 0, 64);
-  *rb = __shfl(lo, 32, 64);
-}
-
-// partition: one wave per (job, push p, group of 64 consecutive tile
-// boundaries).  The group's first and last boundaries bracket a window of
-// the push (two 32-ary searches); each lane then binary-searches its own
-// boundary inside that window (L2-resident).  Boundary b < ntiles is
-// lower_bound(S_p, D[b*tile]); b == ntiles is upper_bound(S_p, D[nslots-1]).
+// partition: one lane per (job, push p, tile boundary b), 64 consecutive
+// boundaries of one push per wave.  Boundary b < ntiles is
+// lower_bound(S_p, D[b*tile]); b == ntiles is upper_bound(S_p, D[nslots-1])
+// (SArray::findRange, shared_array_inl.h:164-171, restated per tile).
+// Interpolation search: the reference's keys are hashed (murmur,
+// example_parser.cc:205-208), so a push is near-uniform over its key range
+// and about 3 probes bracket the answer in <= 16 keys at 128 K; bisection
+// finishes (and bounds the cost on skewed keys: at most 6 probes first).
 __global__ __launch_bounds__(256) void partition_kernel(
     const JobDev* __restrict__ jobs, const uint32_t* __restrict__ item_job,
     uint32_t nitems) {
@@ -97,29 +62,38 @@ __global__ __launch_bounds__(256) void partition_kernel(
   if (J.nslots > 0) {
     const uint64_t* S = J.pkeys[p];
     const uint64_t n = J.pn[p];
-    auto key_of = [&](uint32_t bb) {
-      return bb == J.ntiles ? J.dkeys[J.nslots - 1] : J.dkeys[(uint64_t)bb * J.tile];
-    };
-    const uint32_t bf = g << 6;
-    const uint32_t bl = bf + 63 < J.ntiles ? bf + 63 : J.ntiles;
-    uint64_t wlo, whi;
-    wave_search2(S, n, key_of(bf), bf == J.ntiles, key_of(bl), bl == J.ntiles, lane,
-                 &wlo, &whi);
-    const uint32_t bc = valid ? b : bl;
-    const uint64_t k = key_of(bc);
+    const uint32_t bc = valid ? b : J.ntiles;
     const bool up = bc == J.ntiles;
-    uint64_t lo = wlo, len = whi - wlo;
-    while (len > 0) {
-      const uint64_t half = len >> 1;
-      const uint64_t s = S[lo + half];
-      if (up ? !(k < s) : (s < k)) {
-        lo += half + 1;
-        len -= half + 1;
-      } else {
-        len = half;
+    const uint64_t x = up ? J.dkeys[J.nslots - 1] : J.dkeys[(uint64_t)bc * J.tile];
+    // upper_bound(x) == lower_bound(x + 1): D never holds 2^64-1
+    const uint64_t xl = up ? x + 1ull : x;
+    const uint64_t k0 = n ? S[0] : 0ull, kn = n ? S[n - 1] : 0ull;
+    if (n == 0 || xl <= k0) {
+      res = 0;
+    } else if (xl > kn) {
+      res = n;
+    } else {
+      // invariant S[a] < xl <= S[c]; interpolation probes, then bisection
+      uint64_t a = 0, c = n - 1, ka = k0, kc = kn;
+      for (int it = 0; it < 6 && c - a > 16u; ++it) {
+        const double f = (double)(xl - ka) / (double)(kc - ka);
+        uint64_t mid = a + 1 + (uint64_t)(f * (double)(c - a - 1));
+        mid = mid < c ? mid : c - 1;
+        const uint64_t km = S[mid];
+        if (km < xl) {
+          a = mid;
+          ka = km;
+        } else {
+          c = mid;
+          kc = km;
+        }
       }
+      while (c - a > 1u) {
+        const uint64_t mid = a + ((c - a) >> 1);
+        if (S[mid] < xl) a = mid; else c = mid;
+      }
+      res = c;
     }
-    res = lo;
   }
   if (valid) {
     J.seg[(size_t)b * J.npush + p] = (uint32_t)res;

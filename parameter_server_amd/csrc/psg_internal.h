@@ -84,6 +84,12 @@ constexpr int kRowsInlinePush = 8;  // pushes whose sub-tile boundaries the rows
 constexpr int kRowsMaxSub = 4;      // sub-tiles per rows-kernel wave (span)
 hipError_t launch_aggregate_rows(int dtype, int m, const TileDesc* d_tiles, uint32_t ncoarse,
                                  hipStream_t stream);
+// tile kernel (v13, psg_tile.hip): one workgroup per tile of `tile` slots
+// (1024 or 2048), any number of pushes; the partition cuts pushes at every tile
+constexpr int kTileSlots = 1024;
+bool tile_size_ok(int tile);
+hipError_t launch_aggregate_tile(int dtype, int m, int tile, const TileDesc* d_tiles,
+                                 uint32_t ntiles, hipStream_t stream);
 hipError_t launch_gather(int dtype, const uint64_t* dkeys, uint64_t nd,
                          const void* dvals, const uint64_t* req, uint64_t nreq,
                          void* out, unsigned long long* matched,

@@ -68,7 +68,7 @@ struct JobSpec {
 
 struct JobTable {
   int device = -1;
-  int dtype = 0, m = 1, geo = psg::kGeoS, kernel = 9;
+  int dtype = 0, m = 1, geo = psg::kGeoS, kernel = 9, tslots = psg::kTileSlots;
   std::vector<JobDev> h;
   std::vector<uint64_t> nslots;
   std::vector<uint32_t*> seg_first;  // device row 0 of each job's seg
@@ -108,11 +108,14 @@ struct JobTable {
     {
       const char* k = getenv("PSG_KERNEL");  // 2 = one-tile-per-workgroup kernel
       const int kk = k ? atoi(k) : 0;
-      kernel = (kk >= 2 && kk <= 10 && kk != 3) ? kk : 9;
+      kernel = (kk >= 2 && kk <= 11 && kk != 3) ? kk : 9;
+      const char* t = getenv("PSG_TILE");  // tile kernel: slots per tile
+      tslots = t && psg::tile_size_ok(atoi(t)) ? atoi(t) : psg::kTileSlots;
     }
     uint32_t maxnp_all = 0;
     for (const JobSpec& s : jobs) maxnp_all = std::max(maxnp_all, (uint32_t)s.pn.size());
-    if (kernel >= 6 && maxnp_all > (uint32_t)psg::kStreamMaxPush) kernel = 4;  // many pushes
+    if (kernel >= 6 && kernel <= 10 && maxnp_all > (uint32_t)psg::kStreamMaxPush)
+      kernel = 4;  // many pushes
     // ktile: slots per aggregate-kernel tile; tile: partition granularity.
     // The rows kernel (10) searches its own tile boundaries inside coarse
     // partition ranges when the pushes are few enough.
@@ -122,7 +125,8 @@ struct JobTable {
     const bool rows_inline =
         kernel == 10 && maxnp_all <= (uint32_t)psg::kRowsInlinePush;
     const uint32_t ktile =
-        kernel == 10 ? (rows_inline ? std::min<uint32_t>((uint32_t)psg::kStreamTile,
+        kernel == 11 ? (uint32_t)tslots
+        : kernel == 10 ? (rows_inline ? std::min<uint32_t>((uint32_t)psg::kStreamTile,
                                                          psg::kRowsMaxSub * psg::rows_tile())
                                     : (uint32_t)psg::rows_tile())
         : kernel >= 6 ? (uint32_t)psg::kStreamTile
@@ -241,6 +245,8 @@ struct JobTable {
       HIP_TRY(psg::launch_partition(d_jobs, d_item_job, nitems, s));
     else if (kernel == 2)
       HIP_TRY(psg::launch_aggregate(dtype, m, geo, d_tiles, ntiles, maxnp, s));
+    else if (kernel == 11)
+      HIP_TRY(psg::launch_aggregate_tile(dtype, m, tslots, d_tiles, ntiles, s));
     else if (kernel == 10)
       HIP_TRY(psg::launch_aggregate_rows(dtype, m, d_tiles, ntiles, s));
     else if (kernel == 9)
