@@ -1,6 +1,5 @@
-// psg_tile.hip -- aggregate kernel v13 ("tile"): one workgroup of TS/4
-// threads per tile of TS server slots; every load of the tile is issued
-// before any of it is used.
+// psg_tile.hip -- aggregate kernel v14 ("tile"): one 256-thread workgroup
+// per tile of kTS server slots, built for instruction efficiency.
 //
 // Reference semantics: KVVector::serialSetValue / parallelSetValue
 // (src/parameter/kv_vector.h:84-204) over oldMatch / match
@@ -12,15 +11,20 @@
 // Shape:
 //   * the partition kernel has cut every push at every tile's first server
 //     key, so push q's keys of this tile are S_q[seg[t][q], seg[t+1][q]);
-//   * thread i takes element i of every push's piece (a "round" of up to
-//     NT elements per push), so all element loads are independent,
-//     coalesced, and in flight together with the tile's D keys;
-//   * D goes to LDS with a bucket table over its key range (2 buckets per
-//     slot): a search is one table read and one or two key reads;
-//   * the fold runs push by push (a barrier between pushes), so each slot
-//     sees its contributions in arrival order without atomics; sums and
-//     "last push holding the slot" live in LDS;
-//   * stores are 256 B per wave instruction;
+//   * the pieces are split into "rounds" of 64 consecutive keys of ONE push,
+//     numbered push-major; each wave takes a contiguous run of rounds, so a
+//     round's push (pointers, bounds) is wave-uniform and every element load
+//     is a coalesced 512 B (keys) / 256 B (f32 values) wave access;
+//   * all of a wave's element loads are issued before the tile's bucket
+//     table is built, so they overlap it;
+//   * D goes to LDS; a bucket table (histogram + scan, 2 buckets per slot,
+//     the tile's key range scaled by one high multiply) turns a search into
+//     one table read and one paired key read;
+//   * the fold runs wave by wave (4 barrier steps): rounds are push-major
+//     and waves hold contiguous runs of them, so every slot sees its
+//     contributions in arrival order with no atomics; sums and "last push
+//     holding the slot" live in LDS;
+//   * thread t owns slots 4t..4t+3: 16-B loads of D and 16-B stores;
 //   * consecutive tiles run on one XCD (blocks b and b+8 share one), so the
 //     cache lines two neighbouring tiles' pieces share are read once.
 // Order check: inside a push's piece the matched positions must increase
@@ -48,17 +52,24 @@ __device__ __forceinline__ AS1 T* GW(T* p) {
   return (AS1 T*)p;
 }
 
-constexpr int kGP = 8;  // pushes per group (elements in flight per thread)
+constexpr int kTS = kTileSlots;  // slots per tile
+constexpr int kNT = 256;         // threads
+constexpr int kNW = kNT / 64;    // waves
+constexpr int kSPT = kTS / kNT;  // slots per thread (contiguous)
+constexpr int kNB = 2 * kTS;     // buckets
+constexpr int kBPT = kNB / kNT;  // bucket-table entries per thread in the scan
+constexpr int kCap = 8;          // rounds a wave holds per pass
+constexpr int kGroup = 64;       // pushes per group (one lane of wave 0 each)
+static_assert(kSPT == 4 && kBPT == 8, "layout");
+static_assert(kTS <= 0x7ffe, "u16 positions");
 
-template <int TS>
-struct Geo {
-  static constexpr int NT = TS / 4;   // threads
-  static constexpr int SPT = 4;       // slots per thread
-  static constexpr int NB = 2 * TS;   // buckets
-  static constexpr int LNB = TS == 512 ? 10 : TS == 1024 ? 11 : TS == 2048 ? 12 : 13;
-  static_assert((1 << LNB) == NB, "bucket count");
-  static_assert(TS <= 0x7ffe, "u16 positions");
-};
+typedef unsigned long long u64x2 __attribute__((ext_vector_type(2)));
+typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
+
+__device__ __forceinline__ uint32_t uni(uint32_t v) { return __builtin_amdgcn_readfirstlane(v); }
+__device__ __forceinline__ uint64_t uni64(uint64_t v) {
+  return ((uint64_t)uni((uint32_t)(v >> 32)) << 32) | uni((uint32_t)v);
+}
 
 // blocks b and b+8 share an XCD (observed dispatch, speed only): give each
 // XCD a contiguous run of tiles
@@ -67,19 +78,22 @@ __device__ __forceinline__ uint32_t xcd_tile(uint32_t b, uint32_t n) {
   return x * q + (x < r ? x : r) + j;
 }
 
-template <typename V, int M, int TS>
-__global__ __launch_bounds__(TS / 4) void tile_kernel(const TileDesc* __restrict__ tiles) {
-  using Gm = Geo<TS>;
-  constexpr int NT = Gm::NT, SPT = Gm::SPT, NB = Gm::NB, LNB = Gm::LNB;
-  __shared__ __attribute__((aligned(16))) uint64_t dk[TS + 8];
-  __shared__ __attribute__((aligned(16))) uint16_t btab[NB + 8];
-  __shared__ __attribute__((aligned(16))) V acc[M][TS];
-  __shared__ __attribute__((aligned(16))) uint16_t lastl[TS];  // last push + 1 holding the slot
-  __shared__ __attribute__((aligned(16))) uint16_t spos[kGP][NT];
-  __shared__ int carry[kGP];
+template <typename V, int M>
+__global__ __launch_bounds__(kNT) void tile_kernel(const TileDesc* __restrict__ tiles) {
+  __shared__ __attribute__((aligned(16))) uint64_t dk[kTS + 8];
+  __shared__ __attribute__((aligned(16))) uint32_t bt[kNB + 8];  // histogram, then bucket starts
+  __shared__ __attribute__((aligned(16))) V acc[M][kTS];
+  __shared__ __attribute__((aligned(16))) uint16_t lastl[kTS];  // last push + 1 holding the slot
+  __shared__ uint32_t rpre[kGroup + 1];  // rounds before push q of the group
+  __shared__ uint32_t pcs[kGroup], pln[kGroup];
+  __shared__ uint64_t pkp[kGroup], pvp[kGroup * M];
+  __shared__ int lastpos[kNW];
+  __shared__ int pcarry;
+  __shared__ uint32_t wsum[kNW];
 
   const int tid = threadIdx.x;
   const int lane = tid & 63;
+  const uint32_t w = uni((uint32_t)tid >> 6);
   const TileDesc& T = tiles[xcd_tile(blockIdx.x, gridDim.x)];
   const uint32_t np = T.np;
   const uint32_t nt = T.nt;
@@ -87,179 +101,244 @@ __global__ __launch_bounds__(TS / 4) void tile_kernel(const TileDesc* __restrict
   const bool cont = (T.flags & kFlagCont) != 0;
   const uint64_t* Dg = T.dk;
 
-  // ---- group 0's element loads first: they are the long pole
-  uint32_t c[kGP], len[kGP];
-  uint64_t ek[kGP];
-  V ev[kGP][M];
-  uint32_t rounds = 0;
-  auto group_bounds = [&](uint32_t g0) {
-    const uint32_t gp = np - g0 < (uint32_t)kGP ? np - g0 : (uint32_t)kGP;
-    uint32_t mx = 0;
-#pragma unroll
-    for (int q = 0; q < kGP; ++q) {
-      c[q] = 0;
-      len[q] = 0;
-      if ((uint32_t)q < gp) {
-        const uint32_t a = G(T.seg)[g0 + q];
-        const uint32_t b = G(T.seg)[np + g0 + q];
-        c[q] = a;
-        len[q] = b > a ? b - a : 0u;
-        if (b < a && tid == 0)  // pieces out of order: the push is unsorted
-          __hip_atomic_fetch_add(GW(T.fail) + g0 + q, 1ull, __ATOMIC_RELAXED,
+  // ---- push tables of a group (wave 0, one lane per push), round prefix
+  auto load_tables = [&](uint32_t g0) {
+    if (w == 0) {
+      const uint32_t gp = np - g0 < (uint32_t)kGroup ? np - g0 : (uint32_t)kGroup;
+      uint32_t nr = 0;
+      if ((uint32_t)lane < gp) {
+        const uint32_t q = g0 + (uint32_t)lane;
+        const uint32_t a = G(T.seg)[q];
+        const uint32_t b = G(T.seg)[np + q];
+        if (b < a)  // pieces out of order: the push is unsorted
+          __hip_atomic_fetch_add(GW(T.fail) + q, 1ull, __ATOMIC_RELAXED,
                                  __HIP_MEMORY_SCOPE_AGENT);
-        mx = len[q] > mx ? len[q] : mx;
-      }
-    }
-    rounds = __builtin_amdgcn_readfirstlane((mx + NT - 1) / NT);
-  };
-  // a pass folds one round of every push of the group (qsel < 0) or, when a
-  // piece spans several rounds, one round of push qsel: the fold order must
-  // stay push-major
-  auto load_round = [&](uint32_t g0, uint32_t r, int qsel) {
-#pragma unroll
-    for (int q = 0; q < kGP; ++q) {
-      const uint32_t i = r * NT + (uint32_t)tid;
-      if ((qsel < 0 || q == qsel) && i < len[q]) {
-        const uint32_t x = c[q] + i;
-        ek[q] = G(T.pkeys[g0 + q])[x];
+        const uint32_t len = b > a ? b - a : 0u;
+        pcs[lane] = a;
+        pln[lane] = len;
+        pkp[lane] = (uint64_t)G(T.pkeys)[q];
 #pragma unroll
         for (int mi = 0; mi < M; ++mi)
-          ev[q][mi] = G((const V*)T.pvals[(size_t)(g0 + q) * M + mi])[x];
+          pvp[lane * M + mi] = (uint64_t)G(T.pvals)[(size_t)q * M + mi];
+        nr = (len + 63u) >> 6;
       }
+      uint32_t x = nr;
+#pragma unroll
+      for (int d = 1; d < 64; d <<= 1) {
+        const uint32_t y = __shfl_up(x, d, 64);
+        if (lane >= d) x += y;
+      }
+      rpre[lane + 1] = x;
+      if (lane == 0) rpre[0] = 0;
     }
   };
-  if (np) {
-    group_bounds(0);
-    if (rounds <= 1) load_round(0, 0, -1);
-  }
+  if (np) load_tables(0);
 
-  // ---- D keys (and continued sums): slot s = tid + NT i
-  uint64_t d[SPT];
+  // ---- D keys, continued sums: thread t owns slots 4t..4t+3
+  const uint32_t s0 = 4u * (uint32_t)tid;
+  uint64_t d[4];
+  if (s0 + 3u < nt && ((uintptr_t)Dg & 15u) == 0u) {
+    const u64x2 x0 = *(const AS1 u64x2*)(Dg + s0);
+    const u64x2 x1 = *(const AS1 u64x2*)(Dg + s0 + 2);
+    d[0] = x0.x; d[1] = x0.y; d[2] = x1.x; d[3] = x1.y;
+  } else {
 #pragma unroll
-  for (int i = 0; i < SPT; ++i) {
-    const uint32_t s = (uint32_t)(tid + i * NT);
-    d[i] = s < nt ? G(Dg)[s] : ~0ull;
+    for (int j = 0; j < 4; ++j) d[j] = s0 + j < nt ? G(Dg)[s0 + j] : ~0ull;
   }
-  V a0[SPT][M];
+  V a0[M][4];
 #pragma unroll
-  for (int i = 0; i < SPT; ++i) {
-    const uint32_t s = (uint32_t)(tid + i * NT);
+  for (int mi = 0; mi < M; ++mi)
 #pragma unroll
-    for (int mi = 0; mi < M; ++mi) {
-      a0[i][mi] = V(0);
-      if (cont && s < nt) a0[i][mi] = G((const V*)T.out[mi] + T.slot0)[s];
-    }
-  }
+    for (int j = 0; j < 4; ++j)
+      a0[mi][j] = (cont && s0 + j < nt) ? G((const V*)T.out[mi] + T.slot0)[s0 + j] : V(0);
 
-  // ---- install D, sums, lastl
-#pragma unroll
-  for (int i = 0; i < SPT; ++i) {
-    const int s = tid + i * NT;
-    dk[s] = d[i];
-#pragma unroll
-    for (int mi = 0; mi < M; ++mi) acc[mi][s] = a0[i][mi];
-    lastl[s] = 0;
-  }
-  if (tid < 8) dk[TS + tid] = ~0ull;
-  if (tid < kGP) carry[tid] = -1;
-
-  // bucket of a key: (k - klo) >> shift, clamped (keys outside the tile's
-  // range land in an end bucket and are not found there)
+  // bucket of a key: the tile's key range [klo, khi] scaled onto [0, kNB) by
+  // one 32x32 high multiply; keys outside the range land in an end bucket
+  // and are not found there
   const uint64_t klo = G(Dg)[0];
   const uint64_t khi = G(Dg)[nt - 1];
   const uint64_t range = khi - klo;
   const int bits = range ? 64 - __builtin_clzll(range) : 0;
-  const int shift = bits > LNB ? bits - LNB : 0;
+  const int s2 = bits > 32 ? bits - 32 : 0;
+  const uint64_t r32 = range >> s2;  // < 2^32
+  const uint64_t mq = ((uint64_t)kNB << 32) / (r32 + 1);
+  const uint32_t mul = mq > 0xffffffffull ? 0xffffffffu : (uint32_t)mq;
   auto bucket = [&](uint64_t k) -> uint32_t {
-    const uint64_t bb = (k - klo) >> shift;
-    return bb < (uint64_t)NB ? (uint32_t)bb : (uint32_t)(NB - 1);
+    const uint64_t x = (k - klo) >> s2;
+    return x > r32 ? (uint32_t)(kNB - 1) : __umulhi((uint32_t)x, mul);
   };
-  __syncthreads();
 
-  // ---- bucket table: btab[b] = first slot whose bucket >= b, btab[NB] = nt
+  // ---- install D, sums, lastl; clear the histogram
 #pragma unroll
-  for (int i = 0; i < SPT; ++i) {
-    const uint32_t s = (uint32_t)(tid + i * NT);
-    if (s < nt) {
-      const int b = (int)bucket(d[i]);
-      const int bp = s ? (int)bucket(dk[s - 1]) : -1;
-      for (int x = bp + 1; x <= b; ++x) btab[x] = (uint16_t)s;
-      if (s == nt - 1)
-        for (int x = b + 1; x <= NB; ++x) btab[x] = (uint16_t)nt;
-    }
+  for (int j = 0; j < 4; ++j) {
+    dk[s0 + j] = d[j];
+#pragma unroll
+    for (int mi = 0; mi < M; ++mi) acc[mi][s0 + j] = a0[mi][j];
+    lastl[s0 + j] = 0;
   }
-  __syncthreads();
+  if (tid < 8) dk[kTS + tid] = ~0ull;
+#pragma unroll
+  for (int j = 0; j < kBPT; ++j) bt[tid * kBPT + j] = 0u;
+  if (tid == 0) pcarry = -1;
+  __syncthreads();  // (1) tables, D, cleared histogram
 
-  // ---- groups of pushes; passes of NT elements per push
-  for (uint32_t g0 = 0; g0 < np; g0 += kGP) {
-    if (g0) {
-      group_bounds(g0);
-      if (tid < kGP) carry[tid] = -1;  // read after the pass's first barrier
+  // ---- a pass: this wave's run of rounds, loaded into registers
+  uint32_t done = 0, U = np ? uni(rpre[np < (uint32_t)kGroup ? np : kGroup]) : 0u;
+  uint32_t g0 = 0;
+  uint32_t nrw = 0, ua = 0, Rw = 0;
+  uint32_t rq[kCap], rch[kCap];
+  uint64_t ek[kCap];
+  V ev[kCap][M];
+  bool ev_ok[kCap];
+  auto load_pass = [&]() {
+    const uint32_t rem = U - done;
+    Rw = (rem + kNW - 1) / kNW;
+    Rw = Rw < (uint32_t)kCap ? Rw : (uint32_t)kCap;
+    ua = done + w * Rw;
+    const uint32_t ub = ua + Rw < U ? ua + Rw : U;
+    nrw = ub > ua ? ub - ua : 0u;
+    // push of the first round: binary search of the round prefix
+    const uint32_t gp = np - g0 < (uint32_t)kGroup ? np - g0 : (uint32_t)kGroup;
+    uint32_t q = 0;
+    if (nrw) {
+      uint32_t lo = 0, hi = gp - 1;  // last q with rpre[q] <= ua
+      while (lo < hi) {
+        const uint32_t mid = (lo + hi + 1) >> 1;
+        if (uni(rpre[mid]) <= ua) lo = mid; else hi = mid - 1;
+      }
+      q = lo;
     }
-    const uint32_t gp = np - g0 < (uint32_t)kGP ? np - g0 : (uint32_t)kGP;
-    const bool wide = rounds <= 1;
-    const uint32_t npass = wide ? 1u : gp * rounds;
-    for (uint32_t ps = 0; ps < npass; ++ps) {
-      const int qsel = wide ? -1 : (int)(ps / rounds);
-      const uint32_t r = wide ? 0u : ps % rounds;
-      if (g0 || !wide) load_round(g0, r, qsel);
-      const uint32_t i = r * NT + (uint32_t)tid;
-      auto act = [&](int q) { return (qsel < 0 || q == qsel) && i < len[q]; };
-      // search
-      uint32_t pos[kGP];
-      bool fnd[kGP];
 #pragma unroll
-      for (int q = 0; q < kGP; ++q) {
-        pos[q] = 0xffffu;
-        fnd[q] = false;
-        if (act(q)) {
-          const uint64_t k = ek[q];
-          const uint32_t b = bucket(k);
-          uint32_t l = btab[b];
-          uint32_t n = (uint32_t)btab[b + 1] - l;
-          while (n > 4u) {
-            const uint32_t half = n >> 1;
-            if (dk[l + half - 1] < k) {
-              l += half;
-              n -= half;
-            } else {
-              n = half;
-            }
-          }
-          const uint64_t k0 = dk[l], k1 = dk[l + 1], k2 = dk[l + 2], k3 = dk[l + 3];
-          const bool l0 = n > 0u && k0 < k, l1 = n > 1u && k1 < k;
-          const bool l2 = n > 2u && k2 < k, l3 = n > 3u && k3 < k;
-          pos[q] = l + (l0 ? 1u : 0u) + (l1 ? 1u : 0u) + (l2 ? 1u : 0u) + (l3 ? 1u : 0u);
-          fnd[q] = (n > 0u && k0 == k) | (n > 1u && k1 == k) | (n > 2u && k2 == k) |
-                   (n > 3u && k3 == k);
-          spos[q][tid] = fnd[q] ? (uint16_t)pos[q] : (uint16_t)0xffffu;
-        }
+    for (int r = 0; r < kCap; ++r) {
+      rq[r] = 0;
+      rch[r] = 0;
+      ev_ok[r] = false;
+      if ((uint32_t)r < nrw) {
+        const uint32_t u = ua + (uint32_t)r;
+        while (uni(rpre[q + 1]) <= u) ++q;  // skips pushes with empty pieces
+        const uint32_t ch = u - uni(rpre[q]);
+        rq[r] = q;
+        rch[r] = ch;
+        const uint32_t i = ch * 64u + (uint32_t)lane;
+        ev_ok[r] = i < uni(pln[q]);
+        const uint32_t x = uni(pcs[q]) + (ev_ok[r] ? i : 0u);
+        ek[r] = G((const uint64_t*)uni64(pkp[q]))[x];
+#pragma unroll
+        for (int mi = 0; mi < M; ++mi) ev[r][mi] = G((const V*)uni64(pvp[q * M + mi]))[x];
       }
+    }
+  };
+  if (U) load_pass();
+
+  // ---- bucket table: histogram, exclusive scan -> bt[b] = first slot of bucket b
+#pragma unroll
+  for (int j = 0; j < 4; ++j)
+    if (s0 + j < nt)
+      __hip_atomic_fetch_add(&bt[bucket(d[j])], 1u, __ATOMIC_RELAXED,
+                             __HIP_MEMORY_SCOPE_WORKGROUP);
+  __syncthreads();  // (2)
+  {
+    const u32x4 h0 = *(const u32x4*)&bt[tid * kBPT];
+    const u32x4 h1 = *(const u32x4*)&bt[tid * kBPT + 4];
+    uint32_t e[kBPT] = {h0.x, h0.y, h0.z, h0.w, h1.x, h1.y, h1.z, h1.w};
+    uint32_t tot = 0;
+#pragma unroll
+    for (int j = 0; j < kBPT; ++j) {
+      const uint32_t c = e[j];
+      e[j] = tot;
+      tot += c;
+    }
+    uint32_t x = tot;
+#pragma unroll
+    for (int dd = 1; dd < 64; dd <<= 1) {
+      const uint32_t y = __shfl_up(x, dd, 64);
+      if (lane >= dd) x += y;
+    }
+    if (lane == 63) wsum[w] = x;
+    __syncthreads();  // (3)
+    uint32_t off = x - tot;
+    for (uint32_t v = 0; v < w; ++v) off += wsum[v];
+    u32x4 o0 = {e[0] + off, e[1] + off, e[2] + off, e[3] + off};
+    u32x4 o1 = {e[4] + off, e[5] + off, e[6] + off, e[7] + off};
+    *(u32x4*)&bt[tid * kBPT] = o0;
+    *(u32x4*)&bt[tid * kBPT + 4] = o1;
+    if (tid == 0) bt[kNB] = nt;
+  }
+  __syncthreads();  // (4)
+
+  for (;;) {
+    if (!U) {  // this group of pushes has no keys in the tile
+      g0 += kGroup;
+      if (g0 >= np) break;
+      load_tables(g0);
       __syncthreads();
-      // order check: strictly increasing positions inside each piece
-      bool ok[kGP];
+      U = uni(rpre[np - g0 < (uint32_t)kGroup ? np - g0 : kGroup]);
+      done = 0;
+      if (U) load_pass();
+      continue;
+    }
+    // ---- search every held round
+    uint32_t pos[kCap];
+    bool fnd[kCap];
 #pragma unroll
-      for (int q = 0; q < kGP; ++q) {
-        ok[q] = false;
-        if ((uint32_t)q < gp && (qsel < 0 || q == qsel)) {
-          const bool a = act(q);
-          if (a) {
-            const int prev = tid ? (int)spos[q][tid - 1] : carry[q];
-            ok[q] = fnd[q] && (int)pos[q] > prev;
+    for (int r = 0; r < kCap; ++r) {
+      pos[r] = 0;
+      fnd[r] = false;
+      if ((uint32_t)r < nrw) {
+        const uint64_t k = ek[r];
+        const uint32_t b = bucket(k);
+        uint32_t l = bt[b];
+        uint32_t n = bt[b + 1] - l;
+        while (n > 2u) {  // crowded bucket
+          const uint32_t half = n >> 1;
+          if (dk[l + half - 1] < k) {
+            l += half;
+            n -= half;
+          } else {
+            n = half;
           }
-          const uint64_t bad = __ballot(a && !ok[q]);
-          if (bad && lane == 0)
-            __hip_atomic_fetch_add(GW(T.fail) + g0 + q, (unsigned long long)__popcll(bad),
-                                   __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         }
+        const uint64_t k0 = dk[l], k1 = dk[l + 1];
+        pos[r] = l + ((n > 0u && k0 < k) ? 1u : 0u) + ((n > 1u && k1 < k) ? 1u : 0u);
+        fnd[r] = (n > 0u && k0 == k) || (n > 1u && k1 == k);
       }
-      // fold, push by push in arrival order
+    }
+    int mylast = 0;  // position held by lane 63 in this wave's last round
 #pragma unroll
-      for (int q = 0; q < kGP; ++q) {
-        if ((uint32_t)q < gp && (qsel < 0 || q == qsel)) {
-          if (ok[q]) {
-            const uint32_t p = g0 + (uint32_t)q;
-            const uint32_t s = pos[q];
+    for (int r = 0; r < kCap; ++r)
+      if ((uint32_t)r + 1u == nrw) mylast = (int)pos[r];
+    if (nrw && lane == 63) lastpos[w] = mylast;
+    __syncthreads();  // (5) lastpos of every wave
+
+    // ---- order check
+    bool ok[kCap];
+#pragma unroll
+    for (int r = 0; r < kCap; ++r) {
+      ok[r] = false;
+      if ((uint32_t)r < nrw) {
+        int prev0;
+        if (rch[r] == 0) prev0 = -1;  // first round of the piece
+        else if (r > 0) prev0 = __builtin_amdgcn_readlane((int)pos[r - 1], 63);
+        else prev0 = w > 0 ? lastpos[w - 1] : pcarry;
+        const int prev = __builtin_amdgcn_update_dpp(prev0, (int)pos[r], 0x138, 0xf, 0xf, false);
+        ok[r] = ev_ok[r] && fnd[r] && (int)pos[r] > prev;
+        const uint64_t bad = __ballot(ev_ok[r] && !ok[r]);
+        if (bad && lane == 0)
+          __hip_atomic_fetch_add(GW(T.fail) + g0 + rq[r], (unsigned long long)__popcll(bad),
+                                 __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      }
+    }
+
+    // ---- fold, wave by wave (rounds are push-major)
+    const uint32_t inpass = (U - done) < kNW * Rw ? U - done : kNW * Rw;
+    const uint32_t wl = (inpass - 1) / Rw;  // wave holding the pass's last round
+    for (uint32_t st = 0; st < (uint32_t)kNW; ++st) {
+      if (st == w) {
+#pragma unroll
+        for (int r = 0; r < kCap; ++r) {
+          if ((uint32_t)r < nrw && ok[r]) {
+            const uint32_t p = g0 + rq[r];
+            const uint32_t s = pos[r];
             const uint32_t l1 = lastl[s];
             const bool first = p == 0u && !cont;
             const bool gap = !parallel && l1 < p;
@@ -267,73 +346,87 @@ __global__ __launch_bounds__(TS / 4) void tile_kernel(const TileDesc* __restrict
             for (int mi = 0; mi < M; ++mi) {
               const V a = acc[mi][s];
               const V ag = gap ? a + V(0) : a;
-              acc[mi][s] = first ? ev[q][mi] : ag + ev[q][mi];
+              acc[mi][s] = first ? ev[r][mi] : ag + ev[r][mi];
             }
             lastl[s] = (uint16_t)(p + 1u);
           }
-          __syncthreads();
         }
-      }
-      // carry: the round's last element of each piece
-#pragma unroll
-      for (int q = 0; q < kGP; ++q) {
-        if (act(q) && (i + 1u == len[q] || tid == NT - 1))
-          carry[q] = fnd[q] ? (int)pos[q] : 0xffff;
+        if (w == wl && lane == 63) pcarry = mylast;
       }
       __syncthreads();
     }
+
+    // ---- next pass, or next group of pushes
+    done += kNW * Rw;
+    if (done < U) {
+      load_pass();
+      continue;
+    }
+    U = 0;  // group finished
+    if (tid == 0) pcarry = -1;
   }
 
   // ---- trailing "+0.0" of absent last pushes (serial), stores
+  V res[M][4];
 #pragma unroll
-  for (int i = 0; i < SPT; ++i) {
-    const uint32_t s = (uint32_t)(tid + i * NT);
-    if (s < nt) {
-      const bool gap = !parallel && (uint32_t)lastl[s] < np;
+  for (int j = 0; j < 4; ++j) {
+    const bool gap = !parallel && (uint32_t)lastl[s0 + j] < np;
 #pragma unroll
-      for (int mi = 0; mi < M; ++mi) {
-        const V a = acc[mi][s];
-        GW((V*)T.out[mi] + T.slot0)[s] = gap ? a + V(0) : a;
+    for (int mi = 0; mi < M; ++mi) {
+      const V a = acc[mi][s0 + j];
+      res[mi][j] = gap ? a + V(0) : a;
+    }
+  }
+#pragma unroll
+  for (int mi = 0; mi < M; ++mi) {
+    V* o = (V*)T.out[mi] + T.slot0 + s0;
+    if (s0 + 3u < nt && ((uintptr_t)o & 15u) == 0u) {
+      if constexpr (sizeof(V) == 4) {
+        typedef float f4 __attribute__((ext_vector_type(4)));
+        const f4 v = {res[mi][0], res[mi][1], res[mi][2], res[mi][3]};
+        *(AS1 f4*)GW(o) = v;
+      } else {
+        typedef double d2 __attribute__((ext_vector_type(2)));
+        const d2 v0 = {res[mi][0], res[mi][1]};
+        const d2 v1 = {res[mi][2], res[mi][3]};
+        ((AS1 d2*)GW(o))[0] = v0;
+        ((AS1 d2*)GW(o))[1] = v1;
       }
+    } else {
+#pragma unroll
+      for (int j = 0; j < 4; ++j)
+        if (s0 + j < nt) GW(o)[j] = res[mi][j];
     }
   }
 }
 
-template <typename V, int M, int TS>
+template <typename V, int M>
 hipError_t go(const TileDesc* t, uint32_t n, hipStream_t s) {
-  hipLaunchKernelGGL((tile_kernel<V, M, TS>), dim3(n), dim3(TS / 4), 0, s, t);
+  hipLaunchKernelGGL((tile_kernel<V, M>), dim3(n), dim3(kNT), 0, s, t);
   return hipGetLastError();
 }
 
-template <typename V, int TS>
+template <typename V>
 hipError_t launch_m(int m, const TileDesc* t, uint32_t n, hipStream_t s) {
   switch (m) {
-    case 1: return go<V, 1, TS>(t, n, s);
-    case 2: return go<V, 2, TS>(t, n, s);
-    case 3: return go<V, 3, TS>(t, n, s);
-    case 4: return go<V, 4, TS>(t, n, s);
-    default: return hipErrorInvalidValue;
-  }
-}
-
-template <typename V>
-hipError_t launch_ts(int tile, int m, const TileDesc* t, uint32_t n, hipStream_t s) {
-  switch (tile) {
-    case 1024: return launch_m<V, 1024>(m, t, n, s);
-    case 2048: return launch_m<V, 2048>(m, t, n, s);
+    case 1: return go<V, 1>(t, n, s);
+    case 2: return go<V, 2>(t, n, s);
+    case 3: return go<V, 3>(t, n, s);
+    case 4: return go<V, 4>(t, n, s);
     default: return hipErrorInvalidValue;
   }
 }
 
 }  // namespace
 
-bool tile_size_ok(int tile) { return tile == 1024 || tile == 2048; }
+bool tile_size_ok(int tile) { return tile == kTS; }
 
 hipError_t launch_aggregate_tile(int dtype, int m, int tile, const TileDesc* d_tiles,
                                  uint32_t ntiles, hipStream_t stream) {
   if (ntiles == 0) return hipSuccess;
-  return dtype == 0 ? launch_ts<float>(tile, m, d_tiles, ntiles, stream)
-                    : launch_ts<double>(tile, m, d_tiles, ntiles, stream);
+  if (tile != kTS) return hipErrorInvalidValue;
+  return dtype == 0 ? launch_m<float>(m, d_tiles, ntiles, stream)
+                    : launch_m<double>(m, d_tiles, ntiles, stream);
 }
 
 }  // namespace psg

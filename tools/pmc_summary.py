@@ -16,7 +16,7 @@ def rows(pattern):
 
 
 def short(name):
-    for k in ("rows_kernel", "stream4_kernel", "stream3_kernel", "stream2_kernel", "stream_kernel", "aggregate_v5_kernel", "aggregate_v4_kernel",
+    for k in ("tile_kernel", "rows_kernel", "stream4_kernel", "stream3_kernel", "stream2_kernel", "stream_kernel", "aggregate_v5_kernel", "aggregate_v4_kernel",
               "aggregate_kernel", "partition_kernel", "gather_kernel", "union", "slice_kernel"):
         if k in name:
             return k
