@@ -58,7 +58,7 @@ constexpr int kNW = kNT / 64;    // waves
 constexpr int kSPT = kTS / kNT;  // slots per thread (contiguous)
 constexpr int kNB = 2 * kTS;     // buckets
 constexpr int kBPT = kNB / kNT;  // bucket-table entries per thread in the scan
-constexpr int kCap = 8;          // rounds a wave holds per pass
+constexpr int kCap = 6;          // rounds a wave holds per pass
 constexpr int kGroup = 64;       // pushes per group (one lane of wave 0 each)
 static_assert(kSPT == 4 && kBPT == 8, "layout");
 static_assert(kTS <= 0x7ffe, "u16 positions");
@@ -79,14 +79,15 @@ __device__ __forceinline__ uint32_t xcd_tile(uint32_t b, uint32_t n) {
 }
 
 template <typename V, int M>
-__global__ __launch_bounds__(kNT) void tile_kernel(const TileDesc* __restrict__ tiles) {
+__global__ __launch_bounds__(kNT, 6) void tile_kernel(const TileDesc* __restrict__ tiles) {
   __shared__ __attribute__((aligned(16))) uint64_t dk[kTS + 8];
   __shared__ __attribute__((aligned(16))) uint32_t bt[kNB + 8];  // histogram, then bucket starts
   __shared__ __attribute__((aligned(16))) V acc[M][kTS];
   __shared__ __attribute__((aligned(16))) uint16_t lastl[kTS];  // last push + 1 holding the slot
-  __shared__ uint32_t rpre[kGroup + 1];  // rounds before push q of the group
-  __shared__ uint32_t pcs[kGroup], pln[kGroup];
-  __shared__ uint64_t pkp[kGroup], pvp[kGroup * M];
+  __shared__ uint32_t rpre[kGroup + 1];             // rounds before push q of the group
+  __shared__ uint16_t rtab[kGroup * (kTS / 64)];    // round -> q << 4 | chunk
+  __shared__ uint32_t pln[kGroup];                  // piece length
+  __shared__ uint64_t pkp[kGroup], pvp[kGroup * M];  // piece starts (keys, values)
   __shared__ int lastpos[kNW];
   __shared__ int pcarry;
   __shared__ uint32_t wsum[kNW];
@@ -110,16 +111,19 @@ __global__ __launch_bounds__(kNT) void tile_kernel(const TileDesc* __restrict__ 
         const uint32_t q = g0 + (uint32_t)lane;
         const uint32_t a = G(T.seg)[q];
         const uint32_t b = G(T.seg)[np + q];
-        if (b < a)  // pieces out of order: the push is unsorted
-          __hip_atomic_fetch_add(GW(T.fail) + q, 1ull, __ATOMIC_RELAXED,
+        // pieces out of order (the push is unsorted) or longer than the tile
+        // (duplicates): those keys cannot all match
+        const uint32_t over = b < a ? 1u : (b - a > (uint32_t)kTS ? b - a - (uint32_t)kTS : 0u);
+        if (over)
+          __hip_atomic_fetch_add(GW(T.fail) + q, (unsigned long long)over, __ATOMIC_RELAXED,
                                  __HIP_MEMORY_SCOPE_AGENT);
-        const uint32_t len = b > a ? b - a : 0u;
-        pcs[lane] = a;
+        // a piece lies inside one tile, so it holds at most kTS keys
+        const uint32_t len = b > a ? (b - a < (uint32_t)kTS ? b - a : (uint32_t)kTS) : 0u;
         pln[lane] = len;
-        pkp[lane] = (uint64_t)G(T.pkeys)[q];
+        pkp[lane] = (uint64_t)(G(T.pkeys)[q] + a);
 #pragma unroll
         for (int mi = 0; mi < M; ++mi)
-          pvp[lane * M + mi] = (uint64_t)G(T.pvals)[(size_t)q * M + mi];
+          pvp[lane * M + mi] = (uint64_t)((const V*)G(T.pvals)[(size_t)q * M + mi] + a);
         nr = (len + 63u) >> 6;
       }
       uint32_t x = nr;
@@ -130,6 +134,7 @@ __global__ __launch_bounds__(kNT) void tile_kernel(const TileDesc* __restrict__ 
       }
       rpre[lane + 1] = x;
       if (lane == 0) rpre[0] = 0;
+      for (uint32_t c = 0; c < nr; ++c) rtab[x - nr + c] = (uint16_t)((uint32_t)lane << 4 | c);
     }
   };
   if (np) load_tables(0);
@@ -186,10 +191,11 @@ __global__ __launch_bounds__(kNT) void tile_kernel(const TileDesc* __restrict__ 
   uint32_t done = 0, U = np ? uni(rpre[np < (uint32_t)kGroup ? np : kGroup]) : 0u;
   uint32_t g0 = 0;
   uint32_t nrw = 0, ua = 0, Rw = 0;
-  uint32_t rq[kCap], rch[kCap];
+  uint32_t re[kCap];  // round: q << 4 | chunk (the same in every lane)
   uint64_t ek[kCap];
   V ev[kCap][M];
-  bool ev_ok[kCap];
+  uint32_t fl = 0;  // per lane: bit r = element of round r exists, bit 8+r = found,
+                    // bit 16+r = found and in order (VGPR bits, not SGPR lane masks)
   auto load_pass = [&]() {
     const uint32_t rem = U - done;
     Rw = (rem + kNW - 1) / kNW;
@@ -197,34 +203,21 @@ __global__ __launch_bounds__(kNT) void tile_kernel(const TileDesc* __restrict__ 
     ua = done + w * Rw;
     const uint32_t ub = ua + Rw < U ? ua + Rw : U;
     nrw = ub > ua ? ub - ua : 0u;
-    // push of the first round: binary search of the round prefix
-    const uint32_t gp = np - g0 < (uint32_t)kGroup ? np - g0 : (uint32_t)kGroup;
-    uint32_t q = 0;
-    if (nrw) {
-      uint32_t lo = 0, hi = gp - 1;  // last q with rpre[q] <= ua
-      while (lo < hi) {
-        const uint32_t mid = (lo + hi + 1) >> 1;
-        if (uni(rpre[mid]) <= ua) lo = mid; else hi = mid - 1;
-      }
-      q = lo;
-    }
+    fl = 0;
 #pragma unroll
     for (int r = 0; r < kCap; ++r) {
-      rq[r] = 0;
-      rch[r] = 0;
-      ev_ok[r] = false;
+      re[r] = 0;
       if ((uint32_t)r < nrw) {
-        const uint32_t u = ua + (uint32_t)r;
-        while (uni(rpre[q + 1]) <= u) ++q;  // skips pushes with empty pieces
-        const uint32_t ch = u - uni(rpre[q]);
-        rq[r] = q;
-        rch[r] = ch;
-        const uint32_t i = ch * 64u + (uint32_t)lane;
-        ev_ok[r] = i < uni(pln[q]);
-        const uint32_t x = uni(pcs[q]) + (ev_ok[r] ? i : 0u);
-        ek[r] = G((const uint64_t*)uni64(pkp[q]))[x];
+        const uint32_t e = rtab[ua + (uint32_t)r];
+        const uint32_t q = e >> 4;
+        const uint32_t i = (e & 15u) * 64u + (uint32_t)lane;
+        re[r] = e;
+        const bool have = i < pln[q];
+        fl |= have ? 1u << r : 0u;
+        const uint32_t x = have ? i : 0u;
+        ek[r] = G((const uint64_t*)pkp[q])[x];
 #pragma unroll
-        for (int mi = 0; mi < M; ++mi) ev[r][mi] = G((const V*)uni64(pvp[q * M + mi]))[x];
+        for (int mi = 0; mi < M; ++mi) ev[r][mi] = G((const V*)pvp[q * M + mi])[x];
       }
     }
   };
@@ -279,11 +272,10 @@ __global__ __launch_bounds__(kNT) void tile_kernel(const TileDesc* __restrict__ 
     }
     // ---- search every held round
     uint32_t pos[kCap];
-    bool fnd[kCap];
+    fl &= 0xffu;
 #pragma unroll
     for (int r = 0; r < kCap; ++r) {
       pos[r] = 0;
-      fnd[r] = false;
       if ((uint32_t)r < nrw) {
         const uint64_t k = ek[r];
         const uint32_t b = bucket(k);
@@ -300,7 +292,7 @@ __global__ __launch_bounds__(kNT) void tile_kernel(const TileDesc* __restrict__ 
         }
         const uint64_t k0 = dk[l], k1 = dk[l + 1];
         pos[r] = l + ((n > 0u && k0 < k) ? 1u : 0u) + ((n > 1u && k1 < k) ? 1u : 0u);
-        fnd[r] = (n > 0u && k0 == k) || (n > 1u && k1 == k);
+        fl |= ((n > 0u && k0 == k) || (n > 1u && k1 == k)) ? 1u << (8 + r) : 0u;
       }
     }
     int mylast = 0;  // position held by lane 63 in this wave's last round
@@ -311,21 +303,22 @@ __global__ __launch_bounds__(kNT) void tile_kernel(const TileDesc* __restrict__ 
     __syncthreads();  // (5) lastpos of every wave
 
     // ---- order check
-    bool ok[kCap];
 #pragma unroll
     for (int r = 0; r < kCap; ++r) {
-      ok[r] = false;
       if ((uint32_t)r < nrw) {
         int prev0;
-        if (rch[r] == 0) prev0 = -1;  // first round of the piece
+        if ((re[r] & 15u) == 0u) prev0 = -1;  // first round of the piece
         else if (r > 0) prev0 = __builtin_amdgcn_readlane((int)pos[r - 1], 63);
         else prev0 = w > 0 ? lastpos[w - 1] : pcarry;
         const int prev = __builtin_amdgcn_update_dpp(prev0, (int)pos[r], 0x138, 0xf, 0xf, false);
-        ok[r] = ev_ok[r] && fnd[r] && (int)pos[r] > prev;
-        const uint64_t bad = __ballot(ev_ok[r] && !ok[r]);
+        const bool have = (fl >> r) & 1u;
+        const bool ok = have && ((fl >> (8 + r)) & 1u) && (int)pos[r] > prev;
+        fl |= ok ? 1u << (16 + r) : 0u;
+        const uint64_t bad = __ballot(have && !ok);
         if (bad && lane == 0)
-          __hip_atomic_fetch_add(GW(T.fail) + g0 + rq[r], (unsigned long long)__popcll(bad),
-                                 __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+          __hip_atomic_fetch_add(GW(T.fail) + g0 + (re[r] >> 4),
+                                 (unsigned long long)__popcll(bad), __ATOMIC_RELAXED,
+                                 __HIP_MEMORY_SCOPE_AGENT);
       }
     }
 
@@ -336,8 +329,8 @@ __global__ __launch_bounds__(kNT) void tile_kernel(const TileDesc* __restrict__ 
       if (st == w) {
 #pragma unroll
         for (int r = 0; r < kCap; ++r) {
-          if ((uint32_t)r < nrw && ok[r]) {
-            const uint32_t p = g0 + rq[r];
+          if ((uint32_t)r < nrw && ((fl >> (16 + r)) & 1u)) {
+            const uint32_t p = g0 + (re[r] >> 4);
             const uint32_t s = pos[r];
             const uint32_t l1 = lastl[s];
             const bool first = p == 0u && !cont;
