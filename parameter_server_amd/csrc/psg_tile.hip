@@ -79,9 +79,11 @@ __device__ __forceinline__ uint32_t xcd_tile(uint32_t b, uint32_t n) {
 }
 
 template <typename V, int M>
-__global__ __launch_bounds__(kNT, 6) void tile_kernel(const TileDesc* __restrict__ tiles) {
+__global__ __launch_bounds__(kNT, 7) void tile_kernel(const TileDesc* __restrict__ tiles) {
   __shared__ __attribute__((aligned(16))) uint64_t dk[kTS + 8];
-  __shared__ __attribute__((aligned(16))) uint32_t bt[kNB + 8];  // histogram, then bucket starts
+  // bucket starts (u16); the histogram counts in it as packed pairs by 32-bit atomics
+  __shared__ __attribute__((aligned(16))) uint32_t bt32[(kNB + 8) / 2];
+  uint16_t* const bt = (uint16_t*)bt32;
   __shared__ __attribute__((aligned(16))) V acc[M][kTS];
   __shared__ __attribute__((aligned(16))) uint16_t lastl[kTS];  // last push + 1 holding the slot
   __shared__ uint32_t rpre[kGroup + 1];             // rounds before push q of the group
@@ -182,8 +184,7 @@ __global__ __launch_bounds__(kNT, 6) void tile_kernel(const TileDesc* __restrict
     lastl[s0 + j] = 0;
   }
   if (tid < 8) dk[kTS + tid] = ~0ull;
-#pragma unroll
-  for (int j = 0; j < kBPT; ++j) bt[tid * kBPT + j] = 0u;
+  *(u32x4*)&bt[tid * kBPT] = u32x4{0u, 0u, 0u, 0u};
   if (tid == 0) pcarry = -1;
   __syncthreads();  // (1) tables, D, cleared histogram
 
@@ -227,13 +228,16 @@ __global__ __launch_bounds__(kNT, 6) void tile_kernel(const TileDesc* __restrict
 #pragma unroll
   for (int j = 0; j < 4; ++j)
     if (s0 + j < nt)
-      __hip_atomic_fetch_add(&bt[bucket(d[j])], 1u, __ATOMIC_RELAXED,
+    {  // counts <= kTS < 2^16: no carry between the packed halves
+      const uint32_t b = bucket(d[j]);
+      __hip_atomic_fetch_add(&bt32[b >> 1], 1u << (16 * (b & 1u)), __ATOMIC_RELAXED,
                              __HIP_MEMORY_SCOPE_WORKGROUP);
+    }
   __syncthreads();  // (2)
   {
-    const u32x4 h0 = *(const u32x4*)&bt[tid * kBPT];
-    const u32x4 h1 = *(const u32x4*)&bt[tid * kBPT + 4];
-    uint32_t e[kBPT] = {h0.x, h0.y, h0.z, h0.w, h1.x, h1.y, h1.z, h1.w};
+    const u32x4 h = *(const u32x4*)&bt[tid * kBPT];
+    uint32_t e[kBPT] = {h.x & 0xffffu, h.x >> 16, h.y & 0xffffu, h.y >> 16,
+                        h.z & 0xffffu, h.z >> 16, h.w & 0xffffu, h.w >> 16};
     uint32_t tot = 0;
 #pragma unroll
     for (int j = 0; j < kBPT; ++j) {
@@ -251,11 +255,10 @@ __global__ __launch_bounds__(kNT, 6) void tile_kernel(const TileDesc* __restrict
     __syncthreads();  // (3)
     uint32_t off = x - tot;
     for (uint32_t v = 0; v < w; ++v) off += wsum[v];
-    u32x4 o0 = {e[0] + off, e[1] + off, e[2] + off, e[3] + off};
-    u32x4 o1 = {e[4] + off, e[5] + off, e[6] + off, e[7] + off};
-    *(u32x4*)&bt[tid * kBPT] = o0;
-    *(u32x4*)&bt[tid * kBPT + 4] = o1;
-    if (tid == 0) bt[kNB] = nt;
+    const u32x4 o = {(e[0] + off) | (e[1] + off) << 16, (e[2] + off) | (e[3] + off) << 16,
+                     (e[4] + off) | (e[5] + off) << 16, (e[6] + off) | (e[7] + off) << 16};
+    *(u32x4*)&bt[tid * kBPT] = o;
+    if (tid == 0) bt[kNB] = (uint16_t)nt;
   }
   __syncthreads();  // (4)
 
@@ -280,7 +283,7 @@ __global__ __launch_bounds__(kNT, 6) void tile_kernel(const TileDesc* __restrict
         const uint64_t k = ek[r];
         const uint32_t b = bucket(k);
         uint32_t l = bt[b];
-        uint32_t n = bt[b + 1] - l;
+        uint32_t n = (uint32_t)bt[b + 1] - l;
         while (n > 2u) {  // crowded bucket
           const uint32_t half = n >> 1;
           if (dk[l + half - 1] < k) {
