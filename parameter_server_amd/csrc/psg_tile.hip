@@ -59,7 +59,7 @@ constexpr int kSPT = kTS / kNT;  // slots per thread (contiguous)
 constexpr int kNB = 2 * kTS;     // buckets
 constexpr int kBPT = kNB / kNT;  // bucket-table entries per thread in the scan
 constexpr int kCap = 6;          // rounds a wave holds per pass
-constexpr int kGroup = 64;       // pushes per group (one lane of wave 0 each)
+constexpr int kGroup = 32;       // pushes per group (one lane of wave 0 each)
 static_assert(kSPT == 4 && kBPT == 8, "layout");
 static_assert(kTS <= 0x7ffe, "u16 positions");
 
@@ -79,13 +79,15 @@ __device__ __forceinline__ uint32_t xcd_tile(uint32_t b, uint32_t n) {
 }
 
 template <typename V, int M>
-__global__ __launch_bounds__(kNT, 7) void tile_kernel(const TileDesc* __restrict__ tiles) {
+__global__ __launch_bounds__(kNT, 8) void tile_kernel(const TileDesc* __restrict__ tiles) {
   __shared__ __attribute__((aligned(16))) uint64_t dk[kTS + 8];
   // bucket starts (u16); the histogram counts in it as packed pairs by 32-bit atomics
   __shared__ __attribute__((aligned(16))) uint32_t bt32[(kNB + 8) / 2];
   uint16_t* const bt = (uint16_t*)bt32;
   __shared__ __attribute__((aligned(16))) V acc[M][kTS];
-  __shared__ __attribute__((aligned(16))) uint16_t lastl[kTS];  // last push + 1 holding the slot
+  // last push holding the slot, relative to the group base g0: last + 2 - g0,
+  // 0 when it precedes g0 - 1 (so the value fits a byte for any push count)
+  __shared__ __attribute__((aligned(16))) uint8_t lastl[kTS];
   __shared__ uint32_t rpre[kGroup + 1];             // rounds before push q of the group
   __shared__ uint16_t rtab[kGroup * (kTS / 64)];    // round -> q << 4 | chunk
   __shared__ uint32_t pln[kGroup];                  // piece length
@@ -134,7 +136,7 @@ __global__ __launch_bounds__(kNT, 7) void tile_kernel(const TileDesc* __restrict
         const uint32_t y = __shfl_up(x, d, 64);
         if (lane >= d) x += y;
       }
-      rpre[lane + 1] = x;
+      if (lane < kGroup) rpre[lane + 1] = x;
       if (lane == 0) rpre[0] = 0;
       for (uint32_t c = 0; c < nr; ++c) rtab[x - nr + c] = (uint16_t)((uint32_t)lane << 4 | c);
     }
@@ -181,7 +183,7 @@ __global__ __launch_bounds__(kNT, 7) void tile_kernel(const TileDesc* __restrict
     dk[s0 + j] = d[j];
 #pragma unroll
     for (int mi = 0; mi < M; ++mi) acc[mi][s0 + j] = a0[mi][j];
-    lastl[s0 + j] = 0;
+    lastl[s0 + j] = 1;  // last = -1 = g0 - 1
   }
   if (tid < 8) dk[kTS + tid] = ~0ull;
   *(u32x4*)&bt[tid * kBPT] = u32x4{0u, 0u, 0u, 0u};
@@ -263,9 +265,12 @@ __global__ __launch_bounds__(kNT, 7) void tile_kernel(const TileDesc* __restrict
   __syncthreads();  // (4)
 
   for (;;) {
-    if (!U) {  // this group of pushes has no keys in the tile
+    if (!U) {  // this group of pushes has no keys in the tile, or is done
       g0 += kGroup;
       if (g0 >= np) break;
+      // rebase lastl on the new group: last == g0 - 1 -> 1, older -> 0
+#pragma unroll
+      for (int j = 0; j < 4; ++j) lastl[s0 + j] = lastl[s0 + j] == kGroup + 1 ? 1 : 0;
       load_tables(g0);
       __syncthreads();
       U = uni(rpre[np - g0 < (uint32_t)kGroup ? np - g0 : kGroup]);
@@ -314,11 +319,17 @@ __global__ __launch_bounds__(kNT, 7) void tile_kernel(const TileDesc* __restrict
         else if (r > 0) prev0 = __builtin_amdgcn_readlane((int)pos[r - 1], 63);
         else prev0 = w > 0 ? lastpos[w - 1] : pcarry;
         const int prev = __builtin_amdgcn_update_dpp(prev0, (int)pos[r], 0x138, 0xf, 0xf, false);
-        const bool have = (fl >> r) & 1u;
-        const bool ok = have && ((fl >> (8 + r)) & 1u) && (int)pos[r] > prev;
+        const bool ok = ((fl >> r) & 1u) && ((fl >> (8 + r)) & 1u) && (int)pos[r] > prev;
         fl |= ok ? 1u << (16 + r) : 0u;
-        const uint64_t bad = __ballot(have && !ok);
-        if (bad && lane == 0)
+      }
+    }
+    // elements that exist but did not match: one ballot per pass, counts per
+    // round only when there are any
+    if (__ballot((fl & ~(fl >> 16) & 0xffu) != 0u)) {
+#pragma unroll
+      for (int r = 0; r < kCap; ++r) {
+        const uint64_t bad = __ballot(((fl >> r) & ~(fl >> (16 + r)) & 1u) != 0u);
+        if ((uint32_t)r < nrw && bad && lane == 0)
           __hip_atomic_fetch_add(GW(T.fail) + g0 + (re[r] >> 4),
                                  (unsigned long long)__popcll(bad), __ATOMIC_RELAXED,
                                  __HIP_MEMORY_SCOPE_AGENT);
@@ -333,18 +344,18 @@ __global__ __launch_bounds__(kNT, 7) void tile_kernel(const TileDesc* __restrict
 #pragma unroll
         for (int r = 0; r < kCap; ++r) {
           if ((uint32_t)r < nrw && ((fl >> (16 + r)) & 1u)) {
-            const uint32_t p = g0 + (re[r] >> 4);
+            const uint32_t q = re[r] >> 4;
             const uint32_t s = pos[r];
             const uint32_t l1 = lastl[s];
-            const bool first = p == 0u && !cont;
-            const bool gap = !parallel && l1 < p;
+            const bool first = g0 + q == 0u && !cont;
+            const bool gap = !parallel && l1 <= q;  // last < g0 + q - 1
 #pragma unroll
             for (int mi = 0; mi < M; ++mi) {
               const V a = acc[mi][s];
               const V ag = gap ? a + V(0) : a;
               acc[mi][s] = first ? ev[r][mi] : ag + ev[r][mi];
             }
-            lastl[s] = (uint16_t)(p + 1u);
+            lastl[s] = (uint8_t)(q + 2u);
           }
         }
         if (w == wl && lane == 63) pcarry = mylast;
@@ -366,7 +377,8 @@ __global__ __launch_bounds__(kNT, 7) void tile_kernel(const TileDesc* __restrict
   V res[M][4];
 #pragma unroll
   for (int j = 0; j < 4; ++j) {
-    const bool gap = !parallel && (uint32_t)lastl[s0 + j] < np;
+    // the last group's base is g0 - kGroup: gap iff last < np - 1
+    const bool gap = !parallel && (uint32_t)lastl[s0 + j] < np - (g0 - kGroup) + 1u;
 #pragma unroll
     for (int mi = 0; mi < M; ++mi) {
       const V a = acc[mi][s0 + j];
