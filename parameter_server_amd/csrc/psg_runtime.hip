@@ -108,7 +108,7 @@ struct JobTable {
     {
       const char* k = getenv("PSG_KERNEL");  // 2 = one-tile-per-workgroup kernel
       const int kk = k ? atoi(k) : 0;
-      kernel = (kk >= 2 && kk <= 11 && kk != 3) ? kk : 9;
+      kernel = (kk >= 2 && kk <= 11 && kk != 3) ? kk : 11;
       const char* t = getenv("PSG_TILE");  // tile kernel: slots per tile
       tslots = t && psg::tile_size_ok(atoi(t)) ? atoi(t) : psg::kTileSlots;
     }

@@ -78,6 +78,20 @@ __device__ __forceinline__ uint32_t xcd_tile(uint32_t b, uint32_t n) {
   return x * q + (x < r ? x : r) + j;
 }
 
+// inclusive 64-lane prefix sum by DPP (row shifts, then row broadcasts):
+// immediate lane controls, so no per-lane shuffle addresses stay live (the
+// __shfl_up form kept six address VGPRs alive across the kernel and spilled
+// them at 8 waves/SIMD)
+__device__ __forceinline__ uint32_t wave_scan_incl(uint32_t x) {
+  x += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x111, 0xf, 0xf, false);  // row_shr:1
+  x += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x112, 0xf, 0xf, false);  // row_shr:2
+  x += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x114, 0xf, 0xf, false);  // row_shr:4
+  x += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x118, 0xf, 0xf, false);  // row_shr:8
+  x += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x142, 0xa, 0xf, false);  // row_bcast:15
+  x += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x143, 0xc, 0xf, false);  // row_bcast:31
+  return x;
+}
+
 template <typename V, int M>
 __global__ __launch_bounds__(kNT, 8) void tile_kernel(const TileDesc* __restrict__ tiles) {
   __shared__ __attribute__((aligned(16))) uint64_t dk[kTS + 8];
@@ -109,6 +123,11 @@ __global__ __launch_bounds__(kNT, 8) void tile_kernel(const TileDesc* __restrict
   // ---- push tables of a group (wave 0, one lane per push), round prefix
   auto load_tables = [&](uint32_t g0) {
     if (w == 0) {
+      // a fresh copy of the lane id per call: otherwise the compiler hoists
+      // the lane-derived LDS addresses out of the push-group loop and, at
+      // 64 VGPRs, spills them to scratch in every workgroup (HBM writes)
+      int lane = tid & 63;
+      asm volatile("" : "+v"(lane));
       const uint32_t gp = np - g0 < (uint32_t)kGroup ? np - g0 : (uint32_t)kGroup;
       uint32_t nr = 0;
       if ((uint32_t)lane < gp) {
@@ -130,14 +149,10 @@ __global__ __launch_bounds__(kNT, 8) void tile_kernel(const TileDesc* __restrict
           pvp[lane * M + mi] = (uint64_t)((const V*)G(T.pvals)[(size_t)q * M + mi] + a);
         nr = (len + 63u) >> 6;
       }
-      uint32_t x = nr;
-#pragma unroll
-      for (int d = 1; d < 64; d <<= 1) {
-        const uint32_t y = __shfl_up(x, d, 64);
-        if (lane >= d) x += y;
-      }
+      const uint32_t x = wave_scan_incl(nr);
       if (lane < kGroup) rpre[lane + 1] = x;
       if (lane == 0) rpre[0] = 0;
+#pragma nounroll
       for (uint32_t c = 0; c < nr; ++c) rtab[x - nr + c] = (uint16_t)((uint32_t)lane << 4 | c);
     }
   };
@@ -227,11 +242,16 @@ __global__ __launch_bounds__(kNT, 8) void tile_kernel(const TileDesc* __restrict
   if (U) load_pass();
 
   // ---- bucket table: histogram, exclusive scan -> bt[b] = first slot of bucket b
+  // D keys back from LDS: the registers that held them are free during the
+  // pass's element loads (8 waves/SIMD leave 64 VGPRs)
+  const u64x2 y0 = *(const u64x2*)&dk[s0];
+  const u64x2 y1 = *(const u64x2*)&dk[s0 + 2];
+  const uint64_t dd[4] = {y0.x, y0.y, y1.x, y1.y};
 #pragma unroll
   for (int j = 0; j < 4; ++j)
     if (s0 + j < nt)
     {  // counts <= kTS < 2^16: no carry between the packed halves
-      const uint32_t b = bucket(d[j]);
+      const uint32_t b = bucket(dd[j]);
       __hip_atomic_fetch_add(&bt32[b >> 1], 1u << (16 * (b & 1u)), __ATOMIC_RELAXED,
                              __HIP_MEMORY_SCOPE_WORKGROUP);
     }
@@ -247,12 +267,7 @@ __global__ __launch_bounds__(kNT, 8) void tile_kernel(const TileDesc* __restrict
       e[j] = tot;
       tot += c;
     }
-    uint32_t x = tot;
-#pragma unroll
-    for (int dd = 1; dd < 64; dd <<= 1) {
-      const uint32_t y = __shfl_up(x, dd, 64);
-      if (lane >= dd) x += y;
-    }
+    const uint32_t x = wave_scan_incl(tot);
     if (lane == 63) wsum[w] = x;
     __syncthreads();  // (3)
     uint32_t off = x - tot;
