@@ -43,7 +43,8 @@ constexpr uint32_t kInvalid = 0xFFFFFFFFu;
 // Interpolation search: the reference's keys are hashed (murmur,
 // example_parser.cc:205-208), so a push is near-uniform over its key range
 // and about 3 probes bracket the answer in <= 16 keys at 128 K; bisection
-// finishes (and bounds the cost on skewed keys: at most 6 probes first).
+// narrows skewed cases to 16 (at most 6 interpolation probes first) and one
+// batch of 15 independent loads finishes.
 __global__ __launch_bounds__(256) void partition_kernel(
     const JobDev* __restrict__ jobs, const uint32_t* __restrict__ item_job,
     uint32_t nitems) {
@@ -88,11 +89,19 @@ __global__ __launch_bounds__(256) void partition_kernel(
           kc = km;
         }
       }
-      while (c - a > 1u) {
+      while (c - a > 16u) {
         const uint64_t mid = a + ((c - a) >> 1);
         if (S[mid] < xl) a = mid; else c = mid;
       }
-      res = c;
+      // the last <= 15 candidates in one round trip: independent loads of
+      // S[a+1 .. c-1] (indices clamped to c, where S[c] >= xl counts 0)
+      uint32_t below = 0;
+#pragma unroll
+      for (uint32_t i = 1; i < 16u; ++i) {
+        const uint64_t idx = a + i < c ? a + i : c;
+        below += S[idx] < xl ? 1u : 0u;
+      }
+      res = a + 1u + below;
     }
   }
   if (valid) {
