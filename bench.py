@@ -5,8 +5,10 @@ Headline workload (BASELINE.json configs[1], "cfg2"): one (channel, time)
 aggregate = 8 worker pushes x 131,072 sorted unique uint64 keys with f32
 values, 10 % of the keys shared by all pushes, U = 956,827 server keys.
 A step is one pass of the hot path (partition + aggregate kernels) over a
-batch of --batch such aggregates per GPU (default 32: 770 MB of distinct
-inputs/outputs, 3x the 256 MB Infinity Cache, so the rate is an HBM rate).
+batch of --batch such aggregates per GPU (default 64: 1.54 GB of distinct
+inputs/outputs, 6x the 256 MB Infinity Cache, so the rate is an HBM rate;
+SURVEY 8d sizes one merge at ~4 us at the target, so a launch should carry
+>= 64 of them to amortise launch and tail).
 
 Multi-GPU (one process per GPU, torchrun): the key space is range-
 partitioned with Range<uint64>::all().evenDivide(N, rank) (reference
@@ -41,7 +43,7 @@ def parse():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=20)
     ap.add_argument("--warmup", type=int, default=5)
-    ap.add_argument("--batch", type=int, default=32, help="cfg2 aggregates per GPU per step")
+    ap.add_argument("--batch", type=int, default=64, help="cfg2 aggregates per GPU per step")
     ap.add_argument("--npush", type=int, default=8)
     ap.add_argument("--n", type=int, default=131072)
     ap.add_argument("--overlap", type=float, default=0.1)
