@@ -33,6 +33,7 @@
 // unique, inside the range.
 #include <hip/hip_runtime.h>
 #include <stdint.h>
+#include <stdlib.h>
 
 #include "psg_device.h"
 #include "psg_internal.h"
@@ -92,8 +93,19 @@ __device__ __forceinline__ uint32_t wave_scan_incl(uint32_t x) {
   return x;
 }
 
-template <typename V, int M>
-__global__ __launch_bounds__(kNT, 8) void tile_kernel(const TileDesc* __restrict__ tiles) {
+// persistent order (P): the blocks of one XCD (b, b+8, ...) walk that XCD's
+// contiguous run of tiles together, block j taking tiles j, j + J, j + 2J ...
+// of the run (J = blocks per XCD), so neighbouring tiles still run at once
+__device__ __forceinline__ uint32_t persist_tile(uint32_t b, uint32_t G, uint32_t n, uint32_t k) {
+  const uint32_t x = b & 7u, j = b >> 3, J = G >> 3, q = n >> 3, r = n & 7u;
+  const uint32_t base = x * q + (x < r ? x : r), cnt = q + (x < r ? 1u : 0u);
+  const uint32_t i = j + k * J;
+  return i < cnt ? base + i : 0xffffffffu;
+}
+
+template <typename V, int M, bool P>
+__global__ __launch_bounds__(kNT, 8) void tile_kernel(const TileDesc* __restrict__ tiles,
+                                                      uint32_t ntiles) {
   __shared__ __attribute__((aligned(16))) uint64_t dk[kTS + 8];
   // bucket starts (u16); the histogram counts in it as packed pairs by 32-bit atomics
   __shared__ __attribute__((aligned(16))) uint32_t bt32[(kNB + 8) / 2];
@@ -110,10 +122,29 @@ __global__ __launch_bounds__(kNT, 8) void tile_kernel(const TileDesc* __restrict
   __shared__ int pcarry;
   __shared__ uint32_t wsum[kNW];
 
-  const int tid = threadIdx.x;
+  // P: the next tile's push tables (group 0), staged by LDS-DMA from wave 1
+  // while this tile is in flight: piece bounds and push pointers (lo, hi)
+  __shared__ uint32_t stA[kGroup], stB[kGroup], stK[2][kGroup], stV[2 * M][kGroup];
+
+  bool staged = false;
+  const uint32_t w = uni((uint32_t)threadIdx.x >> 6);
+  for (uint32_t it = 0;; ++it) {
+  // P: the thread id afresh per tile from the lane count and the (scalar)
+  // wave index, so values derived from it are recomputed rather than hoisted
+  // out of the tile loop, and threadIdx itself is not spilled (its scratch
+  // reload's vmcnt(0) would wait for the previous tile's stores)
+  int tid = threadIdx.x;
+  if (P) {
+    uint32_t z = 0;  // opaque per tile, so the lane count is not hoisted
+    asm volatile("" : "+v"(z));
+    tid = (int)((w << 6) + __builtin_amdgcn_mbcnt_hi(~0u, __builtin_amdgcn_mbcnt_lo(~0u, z)));
+  }
   const int lane = tid & 63;
-  const uint32_t w = uni((uint32_t)tid >> 6);
-  const TileDesc& T = tiles[xcd_tile(blockIdx.x, gridDim.x)];
+  const uint32_t ti = P ? persist_tile(blockIdx.x, gridDim.x, ntiles, it)
+                        : (it ? 0xffffffffu : xcd_tile(blockIdx.x, gridDim.x));
+  if (ti >= ntiles) break;
+  const uint32_t tn = P ? persist_tile(blockIdx.x, gridDim.x, ntiles, it + 1) : 0xffffffffu;
+  const TileDesc& T = tiles[ti];
   const uint32_t np = T.np;
   const uint32_t nt = T.nt;
   const bool parallel = (T.flags & kFlagParallel) != 0;
@@ -132,8 +163,9 @@ __global__ __launch_bounds__(kNT, 8) void tile_kernel(const TileDesc* __restrict
       uint32_t nr = 0;
       if ((uint32_t)lane < gp) {
         const uint32_t q = g0 + (uint32_t)lane;
-        const uint32_t a = G(T.seg)[q];
-        const uint32_t b = G(T.seg)[np + q];
+        const bool st = P && staged && g0 == 0;
+        const uint32_t a = st ? stA[lane] : G(T.seg)[q];
+        const uint32_t b = st ? stB[lane] : G(T.seg)[np + q];
         // pieces out of order (the push is unsorted) or longer than the tile
         // (duplicates): those keys cannot all match
         const uint32_t over = b < a ? 1u : (b - a > (uint32_t)kTS ? b - a - (uint32_t)kTS : 0u);
@@ -143,10 +175,15 @@ __global__ __launch_bounds__(kNT, 8) void tile_kernel(const TileDesc* __restrict
         // a piece lies inside one tile, so it holds at most kTS keys
         const uint32_t len = b > a ? (b - a < (uint32_t)kTS ? b - a : (uint32_t)kTS) : 0u;
         pln[lane] = len;
-        pkp[lane] = (uint64_t)(G(T.pkeys)[q] + a);
+        const uint64_t* kp = st ? (const uint64_t*)((uint64_t)stK[1][lane] << 32 | stK[0][lane])
+                                : G(T.pkeys)[q];
+        pkp[lane] = (uint64_t)(kp + a);
 #pragma unroll
-        for (int mi = 0; mi < M; ++mi)
-          pvp[lane * M + mi] = (uint64_t)((const V*)G(T.pvals)[(size_t)q * M + mi] + a);
+        for (int mi = 0; mi < M; ++mi) {
+          const V* vp = st ? (const V*)((uint64_t)stV[2 * mi + 1][lane] << 32 | stV[2 * mi][lane])
+                           : (const V*)G(T.pvals)[(size_t)q * M + mi];
+          pvp[lane * M + mi] = (uint64_t)(vp + a);
+        }
         nr = (len + 63u) >> 6;
       }
       const uint32_t x = wave_scan_incl(nr);
@@ -201,7 +238,11 @@ __global__ __launch_bounds__(kNT, 8) void tile_kernel(const TileDesc* __restrict
     lastl[s0 + j] = 1;  // last = -1 = g0 - 1
   }
   if (tid < 8) dk[kTS + tid] = ~0ull;
-  *(u32x4*)&bt[tid * kBPT] = u32x4{0u, 0u, 0u, 0u};
+  {
+    uint32_t z = 0;  // opaque zero: not a hoisted (and spilled) constant vector
+    if (P) asm volatile("" : "+v"(z));
+    *(u32x4*)&bt[tid * kBPT] = u32x4{z, z, z, z};
+  }
   if (tid == 0) pcarry = -1;
   __syncthreads();  // (1) tables, D, cleared histogram
 
@@ -231,7 +272,7 @@ __global__ __launch_bounds__(kNT, 8) void tile_kernel(const TileDesc* __restrict
         const uint32_t i = (e & 15u) * 64u + (uint32_t)lane;
         re[r] = e;
         const bool have = i < pln[q];
-        fl |= have ? 1u << r : 0u;
+        fl |= (uint32_t)have << r;  // shift of a 0/1: no literal masks held in VGPRs
         const uint32_t x = have ? i : 0u;
         ek[r] = G((const uint64_t*)pkp[q])[x];
 #pragma unroll
@@ -240,6 +281,30 @@ __global__ __launch_bounds__(kNT, 8) void tile_kernel(const TileDesc* __restrict
     }
   };
   if (U) load_pass();
+
+  // ---- P: stage the next tile's group-0 tables (wave 1, one lane per push)
+  // by LDS-DMA behind this tile's element loads; the table build of the next
+  // iteration reads them after this tile's barriers (which retire the DMA)
+  if (P && w == 1 && tn < ntiles) {
+    const TileDesc& Tn = tiles[tn];
+    const uint32_t npn = Tn.np;
+    if ((uint32_t)lane < (npn < (uint32_t)kGroup ? npn : (uint32_t)kGroup)) {
+      typedef __attribute__((address_space(3))) void* LP;
+      const uint32_t* sg = Tn.seg;
+      const uint32_t* pk = (const uint32_t*)Tn.pkeys;
+      const uint32_t* pv = (const uint32_t*)Tn.pvals;
+      __builtin_amdgcn_global_load_lds(G(sg + lane), (LP)stA, 4, 0, 0);
+      __builtin_amdgcn_global_load_lds(G(sg + npn + lane), (LP)stB, 4, 0, 0);
+      __builtin_amdgcn_global_load_lds(G(pk + 2 * lane), (LP)stK[0], 4, 0, 0);
+      __builtin_amdgcn_global_load_lds(G(pk + 2 * lane + 1), (LP)stK[1], 4, 0, 0);
+#pragma unroll
+      for (int mi = 0; mi < M; ++mi) {
+        __builtin_amdgcn_global_load_lds(G(pv + 2 * (lane * M + mi)), (LP)stV[2 * mi], 4, 0, 0);
+        __builtin_amdgcn_global_load_lds(G(pv + 2 * (lane * M + mi) + 1), (LP)stV[2 * mi + 1], 4,
+                                         0, 0);
+      }
+    }
+  }
 
   // ---- bucket table: histogram, exclusive scan -> bt[b] = first slot of bucket b
   // D keys back from LDS: the registers that held them are free during the
@@ -271,7 +336,8 @@ __global__ __launch_bounds__(kNT, 8) void tile_kernel(const TileDesc* __restrict
     if (lane == 63) wsum[w] = x;
     __syncthreads();  // (3)
     uint32_t off = x - tot;
-    for (uint32_t v = 0; v < w; ++v) off += wsum[v];
+#pragma unroll
+    for (uint32_t v = 0; v < (uint32_t)kNW - 1u; ++v) off += v < w ? wsum[v] : 0u;
     const u32x4 o = {(e[0] + off) | (e[1] + off) << 16, (e[2] + off) | (e[3] + off) << 16,
                      (e[4] + off) | (e[5] + off) << 16, (e[6] + off) | (e[7] + off) << 16};
     *(u32x4*)&bt[tid * kBPT] = o;
@@ -315,7 +381,7 @@ __global__ __launch_bounds__(kNT, 8) void tile_kernel(const TileDesc* __restrict
         }
         const uint64_t k0 = dk[l], k1 = dk[l + 1];
         pos[r] = l + ((n > 0u && k0 < k) ? 1u : 0u) + ((n > 1u && k1 < k) ? 1u : 0u);
-        fl |= ((n > 0u && k0 == k) || (n > 1u && k1 == k)) ? 1u << (8 + r) : 0u;
+        fl |= (uint32_t)((n > 0u && k0 == k) || (n > 1u && k1 == k)) << (8 + r);
       }
     }
     int mylast = 0;  // position held by lane 63 in this wave's last round
@@ -335,7 +401,7 @@ __global__ __launch_bounds__(kNT, 8) void tile_kernel(const TileDesc* __restrict
         else prev0 = w > 0 ? lastpos[w - 1] : pcarry;
         const int prev = __builtin_amdgcn_update_dpp(prev0, (int)pos[r], 0x138, 0xf, 0xf, false);
         const bool ok = ((fl >> r) & 1u) && ((fl >> (8 + r)) & 1u) && (int)pos[r] > prev;
-        fl |= ok ? 1u << (16 + r) : 0u;
+        fl |= (uint32_t)ok << (16 + r);
       }
     }
     // elements that exist but did not match: one ballot per pass, counts per
@@ -421,11 +487,32 @@ __global__ __launch_bounds__(kNT, 8) void tile_kernel(const TileDesc* __restrict
         if (s0 + j < nt) GW(o)[j] = res[mi][j];
     }
   }
+  staged = P;
+  if (!P) break;
+  __syncthreads();  // LDS reuse by the next tile
+  }
 }
+
+// persistent grid: 8 workgroups per CU (the occupancy limit), a multiple of 8
+constexpr uint32_t kPersistBlocks = 256u * 8u;
 
 template <typename V, int M>
 hipError_t go(const TileDesc* t, uint32_t n, hipStream_t s) {
-  hipLaunchKernelGGL((tile_kernel<V, M>), dim3(n), dim3(kNT), 0, s, t);
+  static const bool persist = [] {
+    const char* e = getenv("PSG_PERSIST");
+    return e && e[0] == '1';
+  }();
+  // PSG_PERSIST_BLOCKS (testing aid, a multiple of 8): a smaller persistent
+  // grid, so small parity cases run many tiles per workgroup
+  static const uint32_t blocks = [] {
+    const char* e = getenv("PSG_PERSIST_BLOCKS");
+    const long v = e ? atol(e) : 0;
+    return v >= 8 && v % 8 == 0 && v <= (long)kPersistBlocks ? (uint32_t)v : kPersistBlocks;
+  }();
+  if (persist && n > blocks)
+    hipLaunchKernelGGL((tile_kernel<V, M, true>), dim3(blocks), dim3(kNT), 0, s, t, n);
+  else
+    hipLaunchKernelGGL((tile_kernel<V, M, false>), dim3(n), dim3(kNT), 0, s, t, n);
   return hipGetLastError();
 }
 
