@@ -47,12 +47,26 @@ def parse():
     ap.add_argument("--npush", type=int, default=8)
     ap.add_argument("--n", type=int, default=131072)
     ap.add_argument("--overlap", type=float, default=0.1)
+    ap.add_argument("--workload", choices=["cfg2", "cfg3", "cfg4"], default="cfg2",
+                    help="cfg2 (default, the headline); cfg3 CTR shape (64 Zipf(1.1) "
+                         "murmur-keyed pushes x 131072) and cfg4 dense (8 x 16 M contiguous "
+                         "keys) are single-GPU side lines (BASELINE.json configs[2], [3])")
     ap.add_argument("--ingress", choices=["sliced", "unsliced"], default="sliced")
     ap.add_argument("--cpu-seconds", type=float, default=10.0)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--profile-steps", type=int, default=0,
                     help="only run warmup+steps (for rocprofv3); skip baselines")
     return ap.parse_args()
+
+
+WORKLOADS = {
+    "cfg2": ("cfg2: {a.npush} pushes x {a.n} sorted unique uint64 keys + f32 values, 10% shared "
+             "keys (U={U:,}); {a.batch} such (channel,time) aggregates per GPU per step"),
+    "cfg3": ("cfg3 (CTR shape): 64 pushes x 131072 unique murmur-shuffled Zipf(1.1) ranks in "
+             "[1,1e9] + f32 values (U={U:,}); {a.batch} such aggregates per step"),
+    "cfg4": ("cfg4 (dense-bucket limit): 8 pushes of all keys [0,16777216) + f32 values "
+             "(U={U:,}); {a.batch} such aggregates per step"),
+}
 
 
 def log(msg):
@@ -82,7 +96,12 @@ def main():
 
     # ---- synthetic inputs (each rank: its shard of `batch` aggregates) ----
     t0 = time.time()
-    if args.ingress == "sliced" or world == 1:
+    if args.workload != "cfg2":
+        if world > 1:
+            raise SystemExit("--workload cfg3/cfg4 are single-GPU side lines")
+        insts = [synth.zipf_pushes(seed=3 + j) if args.workload == "cfg3"
+                 else synth.dense_pushes(seed=4 + j) for j in range(args.batch)]
+    elif args.ingress == "sliced" or world == 1:
         insts = [synth.shard_instance(seed=1 + j + 1000 * rank, lo=lo, hi=hi,
                                       npush=args.npush, n=args.n, overlap=args.overlap)
                  for j in range(args.batch)]
@@ -187,9 +206,7 @@ def main():
         "dtype": "f32",
         "data": "synthetic",
         "config": {
-            "workload": (f"cfg2: {args.npush} pushes x {args.n} sorted unique uint64 keys + f32 "
-                         f"values, {int(args.overlap * 100)}% shared keys (U=956,827 at the "
-                         f"defaults); {args.batch} such (channel,time) aggregates per GPU per step"),
+            "workload": WORKLOADS[args.workload].format(a=args, U=insts[0][0].size),
             "global_batch": args.batch * world,
             "kv_per_step": kv_all,
             "parallelism": (f"key-range shards evenDivide({world}); "
