@@ -498,17 +498,15 @@ constexpr uint32_t kPersistBlocks = 256u * 8u;
 
 template <typename V, int M>
 hipError_t go(const TileDesc* t, uint32_t n, hipStream_t s) {
-  static const bool persist = [] {
-    const char* e = getenv("PSG_PERSIST");
-    return e && e[0] == '1';
-  }();
+  // read per launch (an ablation knob; tests switch it inside one process)
+  const char* pe = getenv("PSG_PERSIST");
+  const bool persist = pe && pe[0] == '1';
   // PSG_PERSIST_BLOCKS (testing aid, a multiple of 8): a smaller persistent
   // grid, so small parity cases run many tiles per workgroup
-  static const uint32_t blocks = [] {
-    const char* e = getenv("PSG_PERSIST_BLOCKS");
-    const long v = e ? atol(e) : 0;
-    return v >= 8 && v % 8 == 0 && v <= (long)kPersistBlocks ? (uint32_t)v : kPersistBlocks;
-  }();
+  const char* be = getenv("PSG_PERSIST_BLOCKS");
+  const long bv = be ? atol(be) : 0;
+  const uint32_t blocks =
+      bv >= 8 && bv % 8 == 0 && bv <= (long)kPersistBlocks ? (uint32_t)bv : kPersistBlocks;
   if (persist && n > blocks)
     hipLaunchKernelGGL((tile_kernel<V, M, true>), dim3(blocks), dim3(kNT), 0, s, t, n);
   else

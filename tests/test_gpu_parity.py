@@ -306,3 +306,24 @@ def test_plan_cfg4_full_dense(torch_cuda):
     assert plan.matched().tolist() == [1 << 24] * 8
     _, _, _, want, _ = O.aggregate(D, *ALL, pushes)
     assert_bitexact(keep[3][0].cpu().numpy(), want[0])
+
+
+def test_plan_persistent_tile_variant(torch_cuda, monkeypatch):
+    """The persistent tile-kernel variant (PSG_PERSIST=1, DESIGN.md 4.2: next
+    tile's push tables staged by LDS-DMA) on a grid of 8 workgroups, so every
+    workgroup walks many tiles, across jobs, push groups (40 pushes) and a
+    dense job: bit-exact against the oracle like the default kernel."""
+    torch = torch_cuda
+    from parameter_server_amd import synth
+    monkeypatch.setenv("PSG_PERSIST", "1")
+    monkeypatch.setenv("PSG_PERSIST_BLOCKS", "8")
+    cases = [synth.overlap_pushes(5, npush=8, n=30000),
+             synth.dense_pushes(npush=3, n=1 << 18),
+             synth.overlap_pushes(6, npush=40, n=3000, overlap=0.5)]
+    for parallel in (False, True):
+        plan, keep = plan_for(torch, cases, parallel=parallel)
+        plan.run()
+        assert plan.matched().tolist() == [k.size for _, ps in cases for k, _ in ps]
+        for (D, pushes), out in zip(cases, keep[3::4]):
+            _, _, _, want, _ = O.aggregate(D, *ALL, pushes, parallel=parallel)
+            assert_bitexact(out[0].cpu().numpy()[: D.size], want[0])
