@@ -55,8 +55,12 @@ __global__ __launch_bounds__(256) void partition_kernel(
   const JobDev& J = jobs[j];
   const uint32_t local = item - J.part_begin;
   const uint32_t ng = (J.ntiles + 64u) >> 6;  // ceil((ntiles + 1) / 64)
-  const uint32_t p = local / ng;
-  const uint32_t g = local - p * ng;
+  // group-major: the waves of one boundary group (all pushes) are adjacent,
+  // so they share workgroups/XCDs (the group's D keys hit in L2) and their
+  // interleaved seg[b * npush + p] writes land close together in time
+  const uint32_t g = local / J.npush;
+  const uint32_t p = local - g * J.npush;
+  (void)ng;
   const uint32_t b = (g << 6) + (uint32_t)lane;
   const bool valid = b <= J.ntiles;
   uint64_t res = 0;
