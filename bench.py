@@ -101,14 +101,17 @@ def main():
             raise SystemExit("--workload cfg3/cfg4 are single-GPU side lines")
         insts = [synth.zipf_pushes(seed=3 + j) if args.workload == "cfg3"
                  else synth.dense_pushes(seed=4 + j) for j in range(args.batch)]
-    elif args.ingress == "sliced" or world == 1:
+    elif args.ingress == "sliced":
         insts = [synth.shard_instance(seed=1 + j + 1000 * rank, lo=lo, hi=hi,
                                       npush=args.npush, n=args.n, overlap=args.overlap)
                  for j in range(args.batch)]
     else:
-        from parameter_server_amd import shard as S
-        insts = S.exchange_unsliced(args, rank, world, bounds, dist)
-    log(f"rank {rank}: generated {len(insts)} aggregates in {time.time() - t0:.1f}s")
+        # mode B: this rank's workers push whole pushes; they are re-homed by
+        # an all-to-all inside every timed step (shard.UnslicedExchange)
+        aggs = [synth.overlap_pushes(1 + j + 1000 * rank, args.npush, args.n, args.overlap)[1]
+                for j in range(args.batch)]
+        insts = None
+    log(f"rank {rank}: generated {args.batch} aggregates in {time.time() - t0:.1f}s")
 
     dev = torch.device("cuda", local)
 
@@ -117,7 +120,28 @@ def main():
         return torch.from_numpy(a.view(np.int64) if a.dtype == np.uint64 else a).to(dev)
 
     keep, jobs = [], []
-    for D, pushes in insts:
+    ex = None
+    if insts is None:
+        from parameter_server_amd import shard as S
+        ex = S.UnslicedExchange(aggs, bounds, dist, dev)
+        ex.run()
+        torch.cuda.synchronize()
+        rk = ex.recv_keys.cpu().numpy().view(np.uint64)
+        for j in range(args.batch):
+            pcs = ex.pieces(j)
+            if not pcs:
+                continue
+            D = np.unique(np.concatenate([rk[o:o + c] for o, c in pcs]))
+            dD = to_dev(D)
+            out = torch.empty(max(1, D.size), dtype=torch.float32, device=dev)
+            keep.append((dD, out))
+            jobs.append({"keys": dD.data_ptr(), "nslots": int(D.size),
+                         "push_keys": [ex.recv_keys.data_ptr() + 8 * o for o, _ in pcs],
+                         "push_vals": [[ex.recv_vals[0].data_ptr() + 4 * o] for o, _ in pcs],
+                         "push_n": [c for _, c in pcs],
+                         "out": [out.data_ptr()]})
+        del rk
+    for D, pushes in insts or []:
         dD = to_dev(D)
         pk = [to_dev(k) for k, _ in pushes]
         pv = [[to_dev(v) for v in vs] for _, vs in pushes]
@@ -135,10 +159,12 @@ def main():
     # correctness guard: every pushed key matched
     plan.run(sh)
     mt = plan.matched()
-    want = np.array([int(k.size) for _, ps in insts for k, _ in ps], np.uint64)
+    want = np.array([n for jb in jobs for n in jb["push_n"]], np.uint64)
     assert np.array_equal(mt, want), "unmatched keys in the bench workload"
 
     for _ in range(args.warmup):
+        if ex is not None:
+            ex.run()
         plan.run(sh)
     torch.cuda.synchronize()
     if dist:
@@ -146,9 +172,12 @@ def main():
     torch.cuda.synchronize()
 
     K = args.steps
-    ev = [[torch.cuda.Event(enable_timing=True) for _ in range(3)] for _ in range(K)]
+    ev = [[torch.cuda.Event(enable_timing=True) for _ in range(4)] for _ in range(K)]
     t_start = time.perf_counter()
     for s in range(K):
+        ev[s][3].record(stream)
+        if ex is not None:
+            ex.run()  # mode B: the RCCL all-to-all re-homing is part of the step
         ev[s][0].record(stream)
         plan.run_stage(0, sh)
         ev[s][1].record(stream)
@@ -162,6 +191,7 @@ def main():
 
     part_ms = float(np.mean([ev[s][0].elapsed_time(ev[s][1]) for s in range(K)]))
     agg_ms = float(np.mean([ev[s][1].elapsed_time(ev[s][2]) for s in range(K)]))
+    xchg_ms = float(np.mean([ev[s][3].elapsed_time(ev[s][0]) for s in range(K)]))
 
     wall_max, kv_all = reduce_over_ranks(wall, plan.kv_pairs, dist, dev)
     value = kv_all * K / wall_max
@@ -206,13 +236,13 @@ def main():
         "dtype": "f32",
         "data": "synthetic",
         "config": {
-            "workload": WORKLOADS[args.workload].format(a=args, U=insts[0][0].size),
+            "workload": WORKLOADS[args.workload].format(a=args, U=jobs[0]["nslots"] if jobs else 0),
             "global_batch": args.batch * world,
             "kv_per_step": kv_all,
             "parallelism": (f"key-range shards evenDivide({world}); "
                             + ("worker-sliced ingress, no data-path collective"
-                               if args.ingress == "sliced" or world == 1 else
-                               "unsliced ingress, RCCL all-to-all re-homing")),
+                               if ex is None else
+                               "unsliced ingress, RCCL all-to-all re-homing in every step")),
         },
         "roofline": {
             "bound": "hbm",
@@ -230,7 +260,11 @@ def main():
             "frac_of_measured_copy": achieved / copy_gbps,
         },
     }
-    if rank == 0 and world == 1 and not args.no_cpu_baseline:
+    if ex is not None:
+        result["exchange"] = {"ms": xchg_ms, "bytes_sent_per_rank": ex.sent_bytes,
+                              "scope": "gather into destination order + all-to-all of keys "
+                                       "and values (RCCL), per step, rank 0's HIP events"}
+    if rank == 0 and world == 1 and not args.no_cpu_baseline and ex is None:
         result["end_to_end"] = end_to_end(insts[0], local)
         result["cpu_baseline"] = cpu_baseline(insts[0], args.cpu_seconds)
     if rank == 0:

@@ -95,3 +95,95 @@ def exchange_unsliced(args, rank, world, bounds, dist):
             Dsh = np.unique(np.concatenate([k for k, _ in pieces]))
             jobs.append((Dsh, pieces))
     return jobs
+
+
+class UnslicedExchange:
+    """Mode B inside the timed step (bench.py --ingress unsliced).
+
+    The rank holds whole pushes of `len(aggs)` aggregates on its device
+    (aggs[j] = [(keys, [vals])] per push).  A step re-homes them: one gather
+    into destination-major order (shard s's pieces of every push are the
+    contiguous runs [pos_s, pos_s+1) of the sorted push, message.h:96-99),
+    then one all-to-all for the keys and one per value array (RCCL over
+    xGMI on GPUs; gloo in the CPU tests; a plain copy at world size 1).
+    The slice positions are computed once at set-up (a sorted push's cut
+    is data-dependent but costs S binary searches, the partition kernel's
+    work class).  After a step, `recv_keys`/`recv_vals` hold, for source
+    rank src, aggregate j and push p, the piece at `recv_off[src, j, p]`
+    with `recv_cnt[src, j, p]` keys: the layout the merge plan points at.
+    """
+
+    def __init__(self, aggs, bounds, dist, device):
+        import torch
+        self.dist = dist
+        world = dist.get_world_size() if dist is not None else 1
+        J, P = len(aggs), len(aggs[0])
+        m = len(aggs[0][0][1])
+        vdt = aggs[0][0][1][0].dtype
+        flat_k, flat_v, perm_parts = [], [[] for _ in range(m)], []
+        cnt = np.zeros((world, J, P), np.int64)  # send counts [dest, j, p]
+        base = 0
+        starts = np.zeros((J, P), np.int64)
+        pos = {}
+        for j in range(J):
+            for p in range(P):
+                k, vs = aggs[j][p]
+                pos[j, p] = slice_positions(k, bounds)
+                cnt[:, j, p] = np.diff(pos[j, p])
+                starts[j, p] = base
+                base += k.size
+                flat_k.append(k.view(np.int64))
+                for i in range(m):
+                    flat_v[i].append(vs[i])
+        for s in range(world):
+            for j in range(J):
+                for p in range(P):
+                    a, e = int(pos[j, p][s]), int(pos[j, p][s + 1])
+                    perm_parts.append(np.arange(starts[j, p] + a, starts[j, p] + e, dtype=np.int64))
+        perm = np.concatenate(perm_parts) if perm_parts else np.zeros(0, np.int64)
+        self.send_split = cnt.sum(axis=(1, 2)).tolist()
+        send_cnt = torch.from_numpy(cnt.reshape(-1).copy()).to(device)
+        if world > 1:
+            recv_cnt = torch.empty_like(send_cnt)
+            dist.all_to_all_single(recv_cnt, send_cnt)
+        else:
+            recv_cnt = send_cnt.clone()
+        self.recv_cnt = recv_cnt.cpu().numpy().reshape(world, J, P)
+        self.recv_split = self.recv_cnt.sum(axis=(1, 2)).tolist()
+        self.recv_off = (np.cumsum(self.recv_cnt.reshape(-1)) - self.recv_cnt.reshape(-1)).reshape(
+            world, J, P)
+        self.world, self.J, self.P, self.m = world, J, P, m
+        self.flat_keys = torch.from_numpy(np.concatenate(flat_k)).to(device)
+        self.flat_vals = [torch.from_numpy(np.concatenate(v).astype(vdt, copy=False)).to(device)
+                          for v in flat_v]
+        # int32 gather indices when they fit (half the index traffic)
+        self.perm = torch.from_numpy(perm.astype(np.int32) if base < 2 ** 31 else perm).to(device)
+        nrecv = int(sum(self.recv_split))
+        self.send_keys = torch.empty_like(self.flat_keys)
+        self.send_vals = [torch.empty_like(v) for v in self.flat_vals]
+        self.recv_keys = torch.empty(nrecv, dtype=torch.int64, device=device)
+        self.recv_vals = [torch.empty(nrecv, dtype=v.dtype, device=device) for v in self.flat_vals]
+        self.sent_bytes = int(self.flat_keys.numel()) * (8 + sum(v.element_size() for v in self.flat_vals))
+
+    def run(self):
+        """One step's re-homing (enqueued on the current stream)."""
+        import torch
+        if self.world == 1:  # one shard: the pushes are already in send order
+            pairs = [(self.recv_keys, self.flat_keys)] + list(zip(self.recv_vals, self.flat_vals))
+        else:
+            torch.index_select(self.flat_keys, 0, self.perm, out=self.send_keys)
+            for src, dst in zip(self.flat_vals, self.send_vals):
+                torch.index_select(src, 0, self.perm, out=dst)
+            pairs = [(self.recv_keys, self.send_keys)] + list(zip(self.recv_vals, self.send_vals))
+        for out, inp in pairs:
+            if self.world > 1:
+                self.dist.all_to_all_single(out, inp, output_split_sizes=self.recv_split,
+                                            input_split_sizes=self.send_split)
+            else:
+                out.copy_(inp)
+
+    def pieces(self, j):
+        """Aggregate j's received pieces in (source, push) arrival order:
+        [(offset, count)] into recv_keys / recv_vals (empty pieces dropped)."""
+        return [(int(self.recv_off[s, j, p]), int(self.recv_cnt[s, j, p]))
+                for s in range(self.world) for p in range(self.P) if self.recv_cnt[s, j, p]]

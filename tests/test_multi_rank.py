@@ -128,3 +128,54 @@ def test_mode_b_exchange_gloo(world):
     for p in procs:
         p.join(timeout=60)
     assert res == {r: "ok" for r in range(world)}, res
+
+
+def _timed_exchange_worker(rank, world, port, q):
+    """UnslicedExchange (the timed mode-B step of bench.py): after run(),
+    aggregate j's pieces for this shard are every source's pushes of j cut
+    at the shard bounds, in (source, push) order, bit for bit."""
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        b = shard_bounds(world)
+        J = 3
+        aggs = {r: [_pushes(200 + 10 * r + j)[1] for j in range(J)] for r in range(world)}
+        ex = S.UnslicedExchange(aggs[rank], b, dist, torch.device("cpu"))
+        ex.run()
+        ex.run()  # a second step lands in the same buffers
+        rk = ex.recv_keys.numpy().view(np.uint64)
+        rv = ex.recv_vals[0].numpy()
+        for j in range(J):
+            want = []
+            for src in range(world):
+                for k, vs in aggs[src][j]:
+                    pos = S.slice_positions(k, b)
+                    a, e = int(pos[rank]), int(pos[rank + 1])
+                    if e > a:
+                        want.append((k[a:e], vs[0][a:e]))
+            got = ex.pieces(j)
+            assert len(got) == len(want)
+            for (off, c), (wk, wv) in zip(got, want):
+                assert np.array_equal(rk[off:off + c], wk)
+                assert rv[off:off + c].tobytes() == wv.tobytes()
+        q.put((rank, "ok"))
+    except Exception as e:  # pragma: no cover - reported to the parent
+        q.put((rank, repr(e)))
+        raise
+    finally:
+        dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("world", [2])
+def test_mode_b_timed_exchange_gloo(world):
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_timed_exchange_worker, args=(r, world, port, q))
+             for r in range(world)]
+    for p in procs:
+        p.start()
+    res = dict(q.get(timeout=180) for _ in range(world))
+    for p in procs:
+        p.join(timeout=60)
+    assert res == {r: "ok" for r in range(world)}, res
