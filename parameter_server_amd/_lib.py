@@ -16,7 +16,8 @@ import ctypes as C
 import os
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(_HERE, "libpsg.so")
+# PSG_LIB_PATH: benchmarking aid (an A/B build of the same sources)
+LIB_PATH = os.environ.get("PSG_LIB_PATH") or os.path.join(_HERE, "libpsg.so")
 
 PSG_OK = 0
 PSG_ERR_ARG = -1

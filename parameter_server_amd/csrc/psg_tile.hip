@@ -103,8 +103,12 @@ __device__ __forceinline__ uint32_t persist_tile(uint32_t b, uint32_t G, uint32_
   return i < cnt ? base + i : 0xffffffffu;
 }
 
+#ifndef PSG_TILE_WAVES  // waves per SIMD (A/B builds only)
+#define PSG_TILE_WAVES 8
+#endif
+
 template <typename V, int M, bool P>
-__global__ __launch_bounds__(kNT, 8) void tile_kernel(const TileDesc* __restrict__ tiles,
+__global__ __launch_bounds__(kNT, PSG_TILE_WAVES) void tile_kernel(const TileDesc* __restrict__ tiles,
                                                       uint32_t ntiles) {
   __shared__ __attribute__((aligned(16))) uint64_t dk[kTS + 8];
   // bucket starts (u16); the histogram counts in it as packed pairs by 32-bit atomics
@@ -141,7 +145,11 @@ __global__ __launch_bounds__(kNT, 8) void tile_kernel(const TileDesc* __restrict
   }
   const int lane = tid & 63;
   const uint32_t ti = P ? persist_tile(blockIdx.x, gridDim.x, ntiles, it)
+#ifdef PSG_NO_XCD  // A/B builds only: plain block order
+                        : (it ? 0xffffffffu : blockIdx.x);
+#else
                         : (it ? 0xffffffffu : xcd_tile(blockIdx.x, gridDim.x));
+#endif
   if (ti >= ntiles) break;
   const uint32_t tn = P ? persist_tile(blockIdx.x, gridDim.x, ntiles, it + 1) : 0xffffffffu;
   const TileDesc& T = tiles[ti];
