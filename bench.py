@@ -288,11 +288,8 @@ def reduce_over_ranks(wall, kv_rank, dist, dev):
 
 
 def kernel_name():
-    """The aggregate kernel the runtime selects (psg_runtime.hip JobTable)."""
-    k = os.environ.get("PSG_KERNEL", "11")
-    return {"11": "tile_kernel<float,1>", "10": "rows_kernel", "9": "stream4_kernel<float,1,2,7,7,0>", "8": "stream3_kernel<float,1,2,8,7,0>", "7": "stream2_kernel<float,1,2,8,0,0,1>",
-            "6": "stream_kernel<float,1>",
-            "4": "aggregate4_kernel<float,1>", "2": "aggregate_kernel<float,1>"}.get(k, k)
+    """The aggregate kernel (psg_tile.hip)."""
+    return "tile_kernel<float,1>"
 
 
 def end_to_end(inst, device, reps=5):

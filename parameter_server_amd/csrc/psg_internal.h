@@ -1,5 +1,5 @@
-// psg_internal.h -- shared between the gfx950 kernels (psg_kernels.hip) and
-// the host runtime behind the C ABI (psg_runtime.hip).  Not installed.
+// psg_internal.h -- shared between the gfx950 kernels and the host runtime
+// behind the C ABI (psg_runtime.hip).  Not installed.
 #pragma once
 
 #include <hip/hip_runtime.h>
@@ -7,89 +7,68 @@
 
 namespace psg {
 
-// ---- aggregate kernel geometry (see DESIGN.md "Kernels") ----
-constexpr int kEPT = 8;          // push elements per thread per chunk
-constexpr int kGroup = 64;       // pushes per chunk (one mask bit each)
-constexpr int kMaxPush = 4096;   // pushes per job per launch
-constexpr int kMaxM = 4;         // value arrays per push
-
-// Tile geometries: server slots per workgroup tile / threads per workgroup
-// (4 slots per thread in every geometry).
-enum Geometry { kGeoS = 0, kGeoM = 1, kGeoL = 2, kNumGeo = 3 };
-constexpr int geo_tile(int g) { return g == kGeoS ? 512 : g == kGeoM ? 1024 : 2048; }
-constexpr int geo_threads(int g) { return geo_tile(g) / 4; }
+constexpr int kMaxPush = 4096;  // pushes per job per launch
+constexpr int kMaxM = 4;        // value arrays per push
+constexpr int kTileSlots = 1024;  // server slots per aggregate-kernel tile
 
 constexpr uint32_t kFlagParallel = 1u;  // PSG_PARALLEL_MATCH
 constexpr uint32_t kFlagCont = 2u;      // continue an aggregate of an earlier launch
 
-// One (channel, time) aggregate as the partition kernel sees it.  All
-// pointers are device pointers.  seg[b*npush + p] = first index of push p
-// whose key is >= D[b*tile] (b < ntiles) or > D[nslots-1] (b == ntiles).
+// How the partition finds a job's (push, tile) pieces:
+// kSearch: one lane per (push, tile boundary), interpolation search -- cost
+//          per boundary, right when pieces are long (cfg2: ~140 keys);
+// kStream: every push key read once and mapped to its tile through the
+//          job's splitter array -- cost per key, right when pieces are
+//          short (many sparse pushes: cfg3 ~29 keys, cfg5 ~4).
+enum PartMode : uint32_t { kSearch = 0, kStream = 1 };
+constexpr uint32_t kStreamChunk = 256;  // push keys per streaming-partition wave
+
+// One (channel, time) aggregate as the partition kernels see it.  All
+// pointers are device pointers.  seg is push-major: seg[p*(ntiles+1) + b] =
+// first index of push p whose key is >= D[b*tile] (b < ntiles) or
+// > D[nslots-1] (b == ntiles): SArray::findRange restated per tile.
 struct JobDev {
   const uint64_t* dkeys;          // D + lo
   uint64_t nslots;                // hi - lo
   const uint64_t* const* pkeys;   // [npush]
   const uint64_t* pn;             // [npush]
-  uint32_t* seg;                  // [(ntiles + 1) * npush]
-  unsigned long long* fail;       // [npush] in-tile match failures
+  uint32_t* seg;                  // [npush * (ntiles + 1)]
+  unsigned long long* fail;       // [npush] match failures
+  uint64_t* split;                // kStream: [ntiles + 1] tile splitters
   uint32_t npush;
   uint32_t ntiles;
-  uint32_t part_begin;            // first global partition item of this job
+  uint32_t split_begin;           // kStream: first splitter item of this job
+  uint32_t mode;                  // PartMode
   uint32_t tile;                  // slots per tile
+  uint32_t pad;
 };
 
-// One workgroup tile of the aggregate kernel: everything it needs is one
-// scalar-load round trip away.
+// One workgroup tile of the aggregate kernel.
 struct TileDesc {
   const uint64_t* dk;             // D + lo + slot0
-  const uint32_t* seg;            // &job.seg[t * npush]; row t+1 follows
+  const uint32_t* seg;            // &job.seg[t]; push q's bounds: seg[q*stride], seg[q*stride+1]
   const uint64_t* const* pkeys;   // job push key pointers [npush]
   const void* const* pvals;       // job push value pointers [npush * m]
+  const uint64_t* pn;             // job push lengths [npush]
   void* const* out;               // job output pointers [m]
   unsigned long long* fail;       // job fail counters [npush]
   uint64_t slot0;                 // first slot of the tile in the job
-  uint32_t nt;                    // slots in this tile (<= tile)
+  uint32_t nt;                    // slots in this tile (<= kTileSlots)
   uint32_t np;                    // pushes of the job
+  uint32_t stride;                // ntiles + 1
   uint32_t flags;
-  // rows kernel: this tile's slot offset inside its partition range (low
-  // 16 bits) and that range's slot count (high 16 bits); the tile's own
-  // push boundaries are searched inside the range's segments
-  uint32_t sub;
 };
 
-// Kernel launchers (psg_kernels.hip).  All enqueue on `stream` only.
-hipError_t launch_partition(const JobDev* d_jobs, const uint32_t* d_item_job,
+// ---- kernel launchers; all enqueue on `stream` only ----
+// partition: splitters + fail reset of kStream jobs (one block of 256
+// splitters per split item; entry = job index), then the search / stream
+// items (u64: job << 37 | push << 24 | boundary group or chunk)
+hipError_t launch_partition(const JobDev* d_jobs, const uint32_t* d_split_item_job,
+                            uint32_t nsplit_items, const uint64_t* d_items,
                             uint32_t nitems, hipStream_t stream);
-size_t aggregate_lds_bytes(int geo, int dtype, int m, uint32_t maxnp);
-hipError_t launch_aggregate(int dtype, int m, int geo, const TileDesc* d_tiles,
-                            uint32_t ntiles, uint32_t maxnp, hipStream_t stream);
-hipError_t launch_aggregate_v4(int dtype, int m, int geo, const TileDesc* d_tiles,
-                               uint32_t ntiles, uint32_t maxnp, hipStream_t stream);
-hipError_t launch_aggregate_v5(int dtype, int m, int geo, const TileDesc* d_tiles,
-                               uint32_t ntiles, uint32_t maxnp, hipStream_t stream);
-// streaming kernel: one wave per coarse tile of kStreamTile slots, np <= 64
-constexpr int kStreamTile = 4096;
-constexpr int kStreamMaxPush = 64;
-hipError_t launch_aggregate_stream(int dtype, int m, const TileDesc* d_tiles,
-                                   uint32_t ncoarse, hipStream_t stream);
-hipError_t launch_aggregate_stream2(int dtype, int m, const TileDesc* d_tiles,
-                                    uint32_t ncoarse, hipStream_t stream);
-hipError_t launch_aggregate_stream3(int dtype, int m, const TileDesc* d_tiles,
-                                    uint32_t ncoarse, hipStream_t stream);
-hipError_t launch_aggregate_stream4(int dtype, int m, const TileDesc* d_tiles,
-                                    uint32_t ncoarse, uint32_t maxnp, hipStream_t stream);
-// rows kernel (v10): one wave per coarse tile of rows_tile() slots, np <= 64
-int rows_tile();
-constexpr int kRowsInlinePush = 8;  // pushes whose sub-tile boundaries the rows kernel searches
-constexpr int kRowsMaxSub = 4;      // sub-tiles per rows-kernel wave (span)
-hipError_t launch_aggregate_rows(int dtype, int m, const TileDesc* d_tiles, uint32_t ncoarse,
+// aggregate (psg_tile.hip): one workgroup per tile of kTileSlots slots
+hipError_t launch_aggregate_tile(int dtype, int m, const TileDesc* d_tiles, uint32_t ntiles,
                                  hipStream_t stream);
-// tile kernel (v13, psg_tile.hip): one workgroup per tile of `tile` slots
-// (1024 or 2048), any number of pushes; the partition cuts pushes at every tile
-constexpr int kTileSlots = 1024;
-bool tile_size_ok(int tile);
-hipError_t launch_aggregate_tile(int dtype, int m, int tile, const TileDesc* d_tiles,
-                                 uint32_t ntiles, hipStream_t stream);
 hipError_t launch_gather(int dtype, const uint64_t* dkeys, uint64_t nd,
                          const void* dvals, const uint64_t* req, uint64_t nreq,
                          void* out, unsigned long long* matched,

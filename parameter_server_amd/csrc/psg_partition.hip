@@ -1,0 +1,224 @@
+// psg_partition.hip -- where every push of a (channel, time) aggregate is
+// cut at every tile of server slots: SArray::findRange restated per tile
+// (reference src/base/shared_array_inl.h:164-171, and the per-separator
+// lower_bound of sliceKeyOrderedMsg, src/system/message.h:96-99).
+//
+// Output, per job, push-major: seg[p*(ntiles+1) + b] = first index of push p
+// whose key is >= D[b*tile] (b < ntiles), or > D[nslots-1] (b == ntiles).
+// The aggregate kernel (psg_tile.hip) reads push p's piece of tile t as
+// [seg[p][t], seg[p][t+1]).
+//
+// Two ways to fill it (JobDev::mode, chosen per job by the host from the
+// mean piece length):
+//   kSearch: one lane per (push, boundary); interpolation probes (pushes of
+//            murmur-hashed keys are near-uniform over their range), then a
+//            bisection, then one batch of 15 independent loads.  Costs a few
+//            random lines per boundary: the right choice for long pieces.
+//   kStream: one wave per 256 consecutive keys of one push; every key is
+//            mapped to its tile through the job's splitter array
+//            split[t] = D[t*tile] (split[ntiles] = D[nslots-1] + 1), and the
+//            tile transitions between consecutive keys write seg.  Costs
+//            8 B per pushed key: the right choice for many short pieces.
+// Items are u64: job << 37 | push << 24 | (boundary group or chunk).
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include "psg_device.h"
+#include "psg_internal.h"
+
+namespace psg {
+
+namespace {
+
+__device__ __forceinline__ uint32_t uni(uint32_t v) { return __builtin_amdgcn_readfirstlane(v); }
+__device__ __forceinline__ uint64_t uni64(uint64_t v) {
+  return ((uint64_t)uni((uint32_t)(v >> 32)) << 32) | uni((uint32_t)v);
+}
+
+// ---- kStream jobs: splitters and the reset of the job's fail counters ----
+__global__ __launch_bounds__(256) void splitter_kernel(const JobDev* __restrict__ jobs,
+                                                       const uint32_t* __restrict__ item_job,
+                                                       uint32_t nitems) {
+  const uint32_t item = blockIdx.x;
+  if (item >= nitems) return;
+  const uint32_t j = uni(item_job[item]);
+  const JobDev& J = jobs[j];
+  // this job's splitter blocks are consecutive items
+  const uint32_t first = uni(J.split_begin);
+  const uint64_t t = (uint64_t)(item - first) * 256u + threadIdx.x;
+  if (t < J.ntiles) J.split[t] = J.dkeys[t * J.tile];
+  if (t == J.ntiles) J.split[t] = J.dkeys[J.nslots - 1] + 1ull;  // D never holds 2^64-1
+  if (t < J.npush) J.fail[t] = 0ull;
+}
+
+// ---- kSearch: one lane per (push, tile boundary) ----
+__device__ __forceinline__ void search_item(const JobDev& J, uint32_t p, uint32_t g, int lane) {
+  const uint32_t b = (g << 6) + (uint32_t)lane;
+  const bool valid = b <= J.ntiles;
+  uint64_t res = 0;
+  const uint64_t* S = J.pkeys[p];
+  const uint64_t n = J.pn[p];
+  const uint32_t bc = valid ? b : J.ntiles;
+  const bool up = bc == J.ntiles;
+  const uint64_t x = up ? J.dkeys[J.nslots - 1] : J.dkeys[(uint64_t)bc * J.tile];
+  // upper_bound(x) == lower_bound(x + 1): D never holds 2^64-1
+  const uint64_t xl = up ? x + 1ull : x;
+  const uint64_t k0 = S[0], kn = S[n - 1];
+  if (xl <= k0) {
+    res = 0;
+  } else if (xl > kn) {
+    res = n;
+  } else {
+    // invariant S[a] < xl <= S[c]; interpolation probes, then bisection
+    uint64_t a = 0, c = n - 1, ka = k0, kc = kn;
+    for (int it = 0; it < 6 && c - a > 16u; ++it) {
+      const double f = (double)(xl - ka) / (double)(kc - ka);
+      uint64_t mid = a + 1 + (uint64_t)(f * (double)(c - a - 1));
+      mid = mid < c ? mid : c - 1;
+      const uint64_t km = S[mid];
+      if (km < xl) {
+        a = mid;
+        ka = km;
+      } else {
+        c = mid;
+        kc = km;
+      }
+    }
+    while (c - a > 16u) {
+      const uint64_t mid = a + ((c - a) >> 1);
+      if (S[mid] < xl) a = mid; else c = mid;
+    }
+    // the last <= 15 candidates in one round trip: independent loads of
+    // S[a+1 .. c-1] (indices clamped to c, where S[c] >= xl counts 0)
+    uint32_t below = 0;
+#pragma unroll
+    for (uint32_t i = 1; i < 16u; ++i) {
+      const uint64_t idx = a + i < c ? a + i : c;
+      below += S[idx] < xl ? 1u : 0u;
+    }
+    res = a + 1u + below;
+  }
+  if (valid) {
+    J.seg[(size_t)p * (J.ntiles + 1u) + b] = (uint32_t)res;
+    if (b == 0) J.fail[p] = 0ull;  // the aggregate launch follows in-stream
+  }
+}
+
+// ---- kStream: one wave per kStreamChunk consecutive keys of one push ----
+// T(k) = (number of splitters <= k) - 1, in [-1, ntiles]; seg[p][t] = number
+// of keys with T < t, written where T steps up between consecutive keys.
+__device__ __forceinline__ void stream_item(const JobDev& J, uint32_t p, uint32_t c, int lane) {
+  const uint64_t* S = J.pkeys[p];
+  const uint64_t n = J.pn[p];
+  const uint32_t nt = J.ntiles;
+  const uint64_t* sp = J.split;
+  uint32_t* seg = J.seg + (size_t)p * (nt + 1u);
+  const uint64_t i0 = (uint64_t)c * kStreamChunk;
+  // this lane's keys i0 + 4*lane + j
+  const uint64_t ib = i0 + 4u * (uint32_t)lane;
+  uint64_t k[4];
+#pragma unroll
+  for (int j = 0; j < 4; ++j) k[j] = ib + j < n ? S[ib + j] : ~0ull;
+  // T0: tile of the key before the chunk (-1 for the push's first chunk);
+  // every key of a sorted chunk lies in a tile >= T0
+  int64_t T0 = -1;
+  const uint64_t kp = i0 > 0 ? uni64(S[i0 - 1]) : 0ull;
+  if (i0 > 0) {
+    // upper_bound over split[0 .. nt] by 64-ary wave search
+    T0 = (int64_t)dev::wave_search(sp, (uint64_t)nt + 1u, kp, true, lane) - 1;
+  }
+  // window: the 64 splitters after T0, one per lane (past split[nt]: +inf)
+  const uint64_t w = T0 + 1 + lane <= (int64_t)nt ? sp[T0 + 1 + lane] : ~0ull;
+  const uint64_t wlast = uni64((uint64_t)__shfl((long long)w, 63, 64));
+  const bool wfull = T0 + 64 <= (int64_t)nt;  // the window's last entry is a real splitter
+  int64_t T[4];
+#pragma unroll
+  for (int j = 0; j < 4; ++j) {
+    const uint64_t key = k[j];
+    // splitters of the window <= key: a binary search over the lanes' window
+    // entries, by every lane (a shuffle reads nothing from an inactive lane)
+    int cnt = 0;
+#pragma unroll
+    for (int step = 32; step > 0; step >>= 1) {
+      const uint64_t wv = (uint64_t)__shfl((long long)w, cnt + step - 1, 64);
+      if (wv <= key) cnt += step;
+    }
+    int64_t t = T0 + (int64_t)cnt;
+    if (wfull && key >= wlast) {
+      // beyond the window (a very sparse push): search the rest
+      uint64_t lo = (uint64_t)(T0 + 65), len = (uint64_t)nt + 1u - lo;
+      while (len > 0) {
+        const uint64_t half = len >> 1;
+        if (sp[lo + half] <= key) {
+          lo += half + 1;
+          len -= half + 1;
+        } else {
+          len = half;
+        }
+      }
+      t = (int64_t)lo - 1;
+    }
+    T[j] = t > (int64_t)nt ? (int64_t)nt : t;
+  }
+  // predecessor of this lane's first key: lane-1's last key / tile; lane 0
+  // takes the key before the chunk (T0)
+  const int64_t Tp_l = (int64_t)__shfl_up((long long)T[3], 1, 64);
+  const uint64_t kp_l = (uint64_t)__shfl_up((long long)k[3], 1, 64);
+  int64_t Tp = lane == 0 ? T0 : Tp_l;
+  uint64_t kprev = lane == 0 ? kp : kp_l;
+  bool hasprev = lane > 0 || i0 > 0;
+  uint32_t bad = 0;
+#pragma unroll
+  for (int j = 0; j < 4; ++j) {
+    const uint64_t i = ib + j;
+    if (i < n) {
+      if (hasprev && !(kprev < k[j])) ++bad;  // not strictly increasing
+      for (int64_t t = Tp + 1; t <= T[j]; ++t) seg[t] = (uint32_t)i;
+      if (T[j] > Tp) Tp = T[j];
+      kprev = k[j];
+      hasprev = true;
+      if (i == n - 1)  // past the push's last key: every later boundary is n
+        for (int64_t t = Tp + 1; t <= (int64_t)nt; ++t) seg[t] = (uint32_t)n;
+    }
+  }
+  const unsigned long long bm = __ballot(bad != 0);
+  if (bm) {
+    // a later key not above its predecessor: the push cannot match fully
+    if (bad)
+      __hip_atomic_fetch_add(J.fail + p, (unsigned long long)bad, __ATOMIC_RELAXED,
+                             __HIP_MEMORY_SCOPE_AGENT);
+  }
+}
+
+__global__ __launch_bounds__(256) void partition_kernel(const JobDev* __restrict__ jobs,
+                                                        const uint64_t* __restrict__ items,
+                                                        uint32_t nitems) {
+  const uint32_t item = uni((blockIdx.x * 256u + threadIdx.x) >> 6);
+  const int lane = threadIdx.x & 63;
+  if (item >= nitems) return;
+  const uint64_t it = uni64(items[item]);
+  const uint32_t j = (uint32_t)(it >> 37);
+  const uint32_t p = (uint32_t)(it >> 24) & 0x1fffu;
+  const uint32_t x = (uint32_t)it & 0xffffffu;
+  const JobDev& J = jobs[j];
+  if (J.mode == kStream)
+    stream_item(J, p, x, lane);
+  else
+    search_item(J, p, x, lane);
+}
+
+}  // namespace
+
+hipError_t launch_partition(const JobDev* d_jobs, const uint32_t* d_split_item_job,
+                            uint32_t nsplit_items, const uint64_t* d_items, uint32_t nitems,
+                            hipStream_t stream) {
+  if (nsplit_items)
+    hipLaunchKernelGGL(splitter_kernel, dim3(nsplit_items), dim3(256), 0, stream, d_jobs,
+                       d_split_item_job, nsplit_items);
+  if (nitems)
+    hipLaunchKernelGGL(partition_kernel, dim3((nitems + 3) / 4), dim3(256), 0, stream, d_jobs,
+                       d_items, nitems);
+  return hipGetLastError();
+}
+
+}  // namespace psg

@@ -66,21 +66,43 @@ struct JobSpec {
   uint32_t flags;
 };
 
+// Mean piece length (keys per push per tile) below which a job's partition
+// streams the push keys instead of searching every tile boundary
+// (DESIGN.md 4.1): a boundary search reads ~5 random lines (~600 B), the
+// stream 8 B per key.
+constexpr double kStreamBelow = 64.0;
+
+// PSG_PART_MODE=search|stream forces the partition mode (A/B measurements);
+// read once per job-table build, never inside a launch.
+int forced_part_mode() {
+  const char* e = getenv("PSG_PART_MODE");
+  if (!e) return -1;
+  if (!strcmp(e, "search")) return psg::kSearch;
+  if (!strcmp(e, "stream")) return psg::kStream;
+  return -1;
+}
+
 struct JobTable {
   int device = -1;
-  int dtype = 0, m = 1, geo = psg::kGeoS, kernel = 9, tslots = psg::kTileSlots;
+  int dtype = 0, m = 1;
   std::vector<JobDev> h;
-  std::vector<uint64_t> nslots;
-  std::vector<uint32_t*> seg_first;  // device row 0 of each job's seg
-  std::vector<uint32_t*> seg_last;   // device row ntiles
-  std::vector<unsigned long long*> fails;
-  std::vector<uint32_t> npush;
-  uint32_t ntiles = 0, nitems = 0, maxnp = 0;
+  // per job (host): pushes kept (non-empty) and where their matched counts go
+  struct JobInfo {
+    uint32_t np = 0, ntiles = 0;
+    std::vector<uint64_t> pn;          // kept pushes
+    std::vector<uint32_t> slot;        // kept push -> index in the caller's push list
+    uint32_t ncaller = 0;              // caller's push count (empties included)
+    uint32_t* seg = nullptr;
+    unsigned long long* fail = nullptr;
+  };
+  std::vector<JobInfo> info;
+  uint32_t ntiles = 0, nitems = 0, nsplit = 0;
   void* blob = nullptr;
   size_t blob_bytes = 0;
   JobDev* d_jobs = nullptr;
   psg::TileDesc* d_tiles = nullptr;
-  uint32_t* d_item_job = nullptr;
+  uint32_t* d_split_items = nullptr;
+  uint64_t* d_items = nullptr;
   std::vector<char> host_img;
 
   void release() {
@@ -89,82 +111,70 @@ struct JobTable {
     blob_bytes = 0;
   }
 
-  static int pick_geometry() {
-    const char* g = getenv("PSG_GEOMETRY");  // S / M / L (benchmarking aid)
-    if (g && (g[0] == 'S' || g[0] == 's')) return psg::kGeoS;
-    if (g && (g[0] == 'L' || g[0] == 'l')) return psg::kGeoL;
-    if (g && (g[0] == 'M' || g[0] == 'm')) return psg::kGeoM;
-    return psg::kGeoS;
-  }
-
   // Builds (or rebuilds, reusing the allocation when it fits) the device image:
-  // [JobDev x njobs][TileDesc x ntiles][item->job x nitems] then per job:
-  // pkeys, pvals, pn, out, fail, seg.
+  // [JobDev x njobs][TileDesc x ntiles][split items u32][items u64] then per
+  // job: pkeys, pvals, pn, out, fail, seg, split.
   int build(int dev, int dt, int mm, const std::vector<JobSpec>& jobs) {
     device = dev;
     dtype = dt;
     m = mm;
-    geo = pick_geometry();
-    {
-      const char* k = getenv("PSG_KERNEL");  // 2 = one-tile-per-workgroup kernel
-      const int kk = k ? atoi(k) : 0;
-      kernel = (kk >= 2 && kk <= 11 && kk != 3) ? kk : 11;
-      const char* t = getenv("PSG_TILE");  // tile kernel: slots per tile
-      tslots = t && psg::tile_size_ok(atoi(t)) ? atoi(t) : psg::kTileSlots;
-    }
-    uint32_t maxnp_all = 0;
-    for (const JobSpec& s : jobs) maxnp_all = std::max(maxnp_all, (uint32_t)s.pn.size());
-    if (kernel >= 6 && kernel <= 10 && maxnp_all > (uint32_t)psg::kStreamMaxPush)
-      kernel = 4;  // many pushes
-    // ktile: slots per aggregate-kernel tile; tile: partition granularity.
-    // The rows kernel (10) searches its own tile boundaries inside coarse
-    // partition ranges when the pushes are few enough.
-    // ktile: slots per aggregate-kernel tile (the rows kernel: a span of
-    // sub-tiles); tile: partition granularity.  With few pushes the rows
-    // kernel searches its sub-tile boundaries inside coarse partition ranges.
-    const bool rows_inline =
-        kernel == 10 && maxnp_all <= (uint32_t)psg::kRowsInlinePush;
-    const uint32_t ktile =
-        kernel == 11 ? (uint32_t)tslots
-        : kernel == 10 ? (rows_inline ? std::min<uint32_t>((uint32_t)psg::kStreamTile,
-                                                         psg::kRowsMaxSub * psg::rows_tile())
-                                    : (uint32_t)psg::rows_tile())
-        : kernel >= 6 ? (uint32_t)psg::kStreamTile
-                      : (uint32_t)psg::geo_tile(geo);
-    const uint32_t tile = rows_inline ? (uint32_t)psg::kStreamTile : ktile;
-    h.clear();
-    nslots.clear();
-    seg_first.clear();
-    seg_last.clear();
-    fails.clear();
-    npush.clear();
-    ntiles = nitems = maxnp = 0;
-    struct Offs { size_t pk, pv, pn, out, fail, seg; };
+    const uint32_t tile = psg::kTileSlots;
+    const int forced = forced_part_mode();
+    h.assign(jobs.size(), JobDev{});
+    info.assign(jobs.size(), JobInfo{});
+    struct Offs { size_t pk, pv, pn, out, fail, seg, split; };
     std::vector<Offs> offs(jobs.size());
-    uint64_t tiles = 0, items = 0;
+    uint64_t tiles = 0, items = 0, sitems = 0;
     for (size_t j = 0; j < jobs.size(); ++j) {
       const JobSpec& s = jobs[j];
-      const size_t np = s.pn.size();
-      if (np > (size_t)psg::kMaxPush)
-        return fail(PSG_ERR_ARG, "job %zu: %zu pushes > max %d", j, np, psg::kMaxPush);
-      for (size_t p = 0; p < np; ++p)
+      JobInfo& I = info[j];
+      I.ncaller = (uint32_t)s.pn.size();
+      if (s.pn.size() > (size_t)psg::kMaxPush)
+        return fail(PSG_ERR_ARG, "job %zu: %zu pushes > max %d", j, s.pn.size(), psg::kMaxPush);
+      uint64_t kv = 0;
+      for (size_t p = 0; p < s.pn.size(); ++p) {
         if (s.pn[p] >= (1ull << 32))
           return fail(PSG_ERR_ARG, "push of %llu keys >= 2^32", (unsigned long long)s.pn[p]);
-      const uint64_t nt = (s.nslots + tile - 1) / tile;
-      tiles += (s.nslots + ktile - 1) / ktile;
-      items += ((nt + 64) / 64) * np;  // partition: one wave per 64 boundaries
-      if (tiles >= (1ull << 31) || items >= (1ull << 31))
+        // an empty push is ignored (kv_vector.h:90,177): the first NON-empty
+        // push is the one that assigns
+        if (s.pn[p] == 0) continue;
+        I.pn.push_back(s.pn[p]);
+        I.slot.push_back((uint32_t)p);
+        kv += s.pn[p];
+      }
+      I.np = (uint32_t)I.pn.size();
+      // no server keys: nothing can match (every pushed key is reported unmatched)
+      I.ntiles = s.nslots ? (uint32_t)((s.nslots + tile - 1) / tile) : 0u;
+      JobDev& d = h[j];
+      d.nslots = s.nslots;
+      d.npush = I.np;
+      d.ntiles = I.ntiles;
+      d.tile = tile;
+      const double piece = I.np && I.ntiles ? (double)kv / ((double)I.np * I.ntiles) : 1e9;
+      d.mode = forced >= 0 ? (uint32_t)forced : (piece < kStreamBelow ? psg::kStream : psg::kSearch);
+      tiles += I.ntiles;
+      if (I.ntiles && I.np) {
+        if (d.mode == psg::kSearch) {
+          items += (uint64_t)((I.ntiles + 64) / 64) * I.np;
+        } else {
+          d.split_begin = (uint32_t)sitems;
+          sitems += (std::max<uint64_t>(I.ntiles + 1, I.np) + 255) / 256;
+          for (uint64_t n : I.pn) items += (n + psg::kStreamChunk - 1) / psg::kStreamChunk;
+        }
+      }
+      if (tiles >= (1ull << 31) || items >= (1ull << 31) || sitems >= (1ull << 31))
         return fail(PSG_ERR_ARG, "batch too large (%llu tiles)", (unsigned long long)tiles);
-      maxnp = std::max(maxnp, (uint32_t)np);
+      if (j >= (1ull << 27)) return fail(PSG_ERR_ARG, "too many jobs");
     }
     size_t off = align_up(sizeof(JobDev) * jobs.size(), 256);
     const size_t tiles_off = off;
     off = align_up(off + sizeof(psg::TileDesc) * tiles, 256);
+    const size_t sitems_off = off;
+    off = align_up(off + 4 * sitems, 256);
     const size_t items_off = off;
-    off = align_up(off + 4 * items, 256);
+    off = align_up(off + 8 * items, 256);
     for (size_t j = 0; j < jobs.size(); ++j) {
-      const size_t np = jobs[j].pn.size();
-      const uint64_t nt = (jobs[j].nslots + tile - 1) / tile;
+      const size_t np = info[j].np, nt = info[j].ntiles;
       Offs& o = offs[j];
       o.pk = off; off = align_up(off + 8 * np, 64);
       o.pv = off; off = align_up(off + 8 * np * m, 64);
@@ -172,6 +182,8 @@ struct JobTable {
       o.out = off; off = align_up(off + 8 * m, 64);
       o.fail = off; off = align_up(off + 8 * np, 64);
       o.seg = off; off = align_up(off + 4 * (nt + 1) * np, 256);
+      o.split = off;
+      if (h[j].mode == psg::kStream) off = align_up(off + 8 * (nt + 1), 256);
     }
     if (off > blob_bytes) {
       release();
@@ -181,60 +193,73 @@ struct JobTable {
     char* base = (char*)blob;
     host_img.assign(off, 0);
     psg::TileDesc* htiles = (psg::TileDesc*)&host_img[tiles_off];
-    uint32_t* hitems = (uint32_t*)&host_img[items_off];
-    uint32_t tcur = 0, icur = 0;
+    uint32_t* hsitems = (uint32_t*)&host_img[sitems_off];
+    uint64_t* hitems = (uint64_t*)&host_img[items_off];
+    uint64_t tcur = 0, icur = 0, scur = 0;
     for (size_t j = 0; j < jobs.size(); ++j) {
       const JobSpec& s = jobs[j];
+      JobInfo& I = info[j];
       const Offs& o = offs[j];
-      const uint32_t np = (uint32_t)s.pn.size();
-      const uint64_t nt = (s.nslots + tile - 1) / tile;
-      memcpy(&host_img[o.pk], s.pkeys.data(), 8 * np);
-      memcpy(&host_img[o.pv], s.pvals.data(), 8 * np * m);
-      memcpy(&host_img[o.pn], s.pn.data(), 8 * np);
+      const uint32_t np = I.np, nt = I.ntiles;
+      uint64_t* hk = (uint64_t*)&host_img[o.pk];
+      uint64_t* hv = (uint64_t*)&host_img[o.pv];
+      for (uint32_t p = 0; p < np; ++p) {
+        const uint32_t c = I.slot[p];
+        hk[p] = (uint64_t)s.pkeys[c];
+        for (int i = 0; i < m; ++i) hv[(size_t)p * m + i] = (uint64_t)s.pvals[(size_t)c * m + i];
+      }
+      memcpy(&host_img[o.pn], I.pn.data(), 8 * np);
       memcpy(&host_img[o.out], s.out.data(), 8 * m);
-      JobDev d{};
+      JobDev& d = h[j];
       d.dkeys = s.keys;
-      d.nslots = s.nslots;
       d.pkeys = (const uint64_t* const*)(base + o.pk);
       d.pn = (const uint64_t*)(base + o.pn);
       d.seg = (uint32_t*)(base + o.seg);
       d.fail = (unsigned long long*)(base + o.fail);
-      d.npush = np;
-      d.ntiles = (uint32_t)nt;
-      d.part_begin = icur;
-      d.tile = tile;
-      h.push_back(d);
-      for (uint64_t b = 0; b < ((nt + 64) / 64) * np; ++b) hitems[icur++] = (uint32_t)j;
-      const uint64_t nkt = (s.nslots + ktile - 1) / ktile;
-      for (uint64_t t = 0; t < nkt; ++t) {
+      d.split = d.mode == psg::kStream ? (uint64_t*)(base + o.split) : nullptr;
+      I.seg = d.seg;
+      I.fail = d.fail;
+      if (nt && np) {
+        if (d.mode == psg::kSearch) {
+          const uint64_t ng = (nt + 64) / 64;
+          for (uint64_t g = 0; g < ng; ++g)  // group-major: a boundary group's pushes adjacent
+            for (uint32_t p = 0; p < np; ++p)
+              hitems[icur++] = (uint64_t)j << 37 | (uint64_t)p << 24 | g;
+        } else {
+          const uint64_t ns = (std::max<uint64_t>(nt + 1, np) + 255) / 256;
+          for (uint64_t b = 0; b < ns; ++b) hsitems[scur++] = (uint32_t)j;
+          for (uint32_t p = 0; p < np; ++p) {
+            const uint64_t nc = (I.pn[p] + psg::kStreamChunk - 1) / psg::kStreamChunk;
+            for (uint64_t c = 0; c < nc; ++c)
+              hitems[icur++] = (uint64_t)j << 37 | (uint64_t)p << 24 | c;
+          }
+        }
+      }
+      for (uint32_t t = 0; t < nt; ++t) {
         psg::TileDesc& T = htiles[tcur++];
-        const uint64_t slot0 = t * ktile;
-        const uint64_t pt = slot0 / tile;  // partition range holding the tile
+        const uint64_t slot0 = (uint64_t)t * tile;
         T.dk = s.keys + slot0;
-        T.seg = d.seg + pt * np;
+        T.seg = d.seg + t;
         T.pkeys = d.pkeys;
         T.pvals = (const void* const*)(base + o.pv);
+        T.pn = d.pn;
         T.out = (void* const*)(base + o.out);
         T.fail = d.fail;
         T.slot0 = slot0;
-        T.nt = (uint32_t)std::min<uint64_t>(ktile, s.nslots - slot0);
+        T.nt = (uint32_t)std::min<uint64_t>(tile, s.nslots - slot0);
         T.np = np;
+        T.stride = nt + 1;
         T.flags = s.flags;
-        const uint64_t pslots = std::min<uint64_t>(tile, s.nslots - pt * tile);
-        T.sub = (uint32_t)(slot0 - pt * tile) | ((uint32_t)pslots << 16);
       }
-      nslots.push_back(s.nslots);
-      seg_first.push_back(d.seg);
-      seg_last.push_back(d.seg + nt * np);
-      fails.push_back(d.fail);
-      npush.push_back(np);
     }
     memcpy(host_img.data(), h.data(), sizeof(JobDev) * h.size());
     ntiles = (uint32_t)tiles;
     nitems = (uint32_t)items;
+    nsplit = (uint32_t)scur;
     d_jobs = (JobDev*)blob;
     d_tiles = (psg::TileDesc*)(base + tiles_off);
-    d_item_job = (uint32_t*)(base + items_off);
+    d_split_items = (uint32_t*)(base + sitems_off);
+    d_items = (uint64_t*)(base + items_off);
     HIP_TRY(hipMemcpy(blob, host_img.data(), off, hipMemcpyHostToDevice));
     return PSG_OK;
   }
@@ -242,25 +267,9 @@ struct JobTable {
   int run_stage(int stage, hipStream_t s) const {
     if (h.empty()) return PSG_OK;
     if (stage == 0)
-      HIP_TRY(psg::launch_partition(d_jobs, d_item_job, nitems, s));
-    else if (kernel == 2)
-      HIP_TRY(psg::launch_aggregate(dtype, m, geo, d_tiles, ntiles, maxnp, s));
-    else if (kernel == 11)
-      HIP_TRY(psg::launch_aggregate_tile(dtype, m, tslots, d_tiles, ntiles, s));
-    else if (kernel == 10)
-      HIP_TRY(psg::launch_aggregate_rows(dtype, m, d_tiles, ntiles, s));
-    else if (kernel == 9)
-      HIP_TRY(psg::launch_aggregate_stream4(dtype, m, d_tiles, ntiles, maxnp, s));
-    else if (kernel == 8)
-      HIP_TRY(psg::launch_aggregate_stream3(dtype, m, d_tiles, ntiles, s));
-    else if (kernel == 7)
-      HIP_TRY(psg::launch_aggregate_stream2(dtype, m, d_tiles, ntiles, s));
-    else if (kernel == 6)
-      HIP_TRY(psg::launch_aggregate_stream(dtype, m, d_tiles, ntiles, s));
-    else if (kernel == 4)
-      HIP_TRY(psg::launch_aggregate_v4(dtype, m, geo, d_tiles, ntiles, maxnp, s));
+      HIP_TRY(psg::launch_partition(d_jobs, d_split_items, nsplit, d_items, nitems, s));
     else
-      HIP_TRY(psg::launch_aggregate_v5(dtype, m, geo, d_tiles, ntiles, maxnp, s));
+      HIP_TRY(psg::launch_aggregate_tile(dtype, m, d_tiles, ntiles, s));
     return PSG_OK;
   }
 
@@ -269,25 +278,27 @@ struct JobTable {
     return run_stage(1, s);
   }
 
-  // matched[p] = (covered elements) - (in-tile failures); stream must be idle.
-  // A job's fail counters and seg rows are adjacent in the blob: one copy.
+  // matched[p] per caller push (empty pushes 0): covered elements minus
+  // match failures; the stream must be idle.
   int matched(std::vector<uint64_t>& out) const {
     out.clear();
-    std::vector<char> buf;
     for (size_t j = 0; j < h.size(); ++j) {
-      const uint32_t np = npush[j];
-      if (np == 0) continue;
-      const char* f0 = (const char*)fails[j];
-      const char* end = (const char*)(seg_last[j] + np);
-      buf.resize(end - f0);
-      HIP_TRY(hipMemcpy(buf.data(), f0, buf.size(), hipMemcpyDeviceToHost));
-      const unsigned long long* f = (const unsigned long long*)buf.data();
-      const uint32_t* first = (const uint32_t*)(buf.data() + ((const char*)seg_first[j] - f0));
-      const uint32_t* last = (const uint32_t*)(buf.data() + ((const char*)seg_last[j] - f0));
-      for (uint32_t p = 0; p < np; ++p) {
-        const uint64_t covered = nslots[j] ? (uint64_t)(last[p] - first[p]) : 0;
-        out.push_back(covered >= f[p] ? covered - f[p] : 0);
+      const JobInfo& I = info[j];
+      std::vector<uint64_t> mt(I.ncaller, 0);
+      const uint32_t np = I.np, nt = I.ntiles;
+      if (np && nt) {
+        std::vector<unsigned long long> f(np);
+        std::vector<uint32_t> first(np), last(np);
+        const size_t pitch = 4 * (size_t)(nt + 1);
+        HIP_TRY(hipMemcpy(f.data(), I.fail, 8 * np, hipMemcpyDeviceToHost));
+        HIP_TRY(hipMemcpy2D(first.data(), 4, I.seg, pitch, 4, np, hipMemcpyDeviceToHost));
+        HIP_TRY(hipMemcpy2D(last.data(), 4, I.seg + nt, pitch, 4, np, hipMemcpyDeviceToHost));
+        for (uint32_t p = 0; p < np; ++p) {
+          const uint64_t covered = last[p] >= first[p] ? (uint64_t)(last[p] - first[p]) : 0;
+          mt[I.slot[p]] = covered >= f[p] ? covered - f[p] : 0;
+        }
       }
+      out.insert(out.end(), mt.begin(), mt.end());
     }
     return PSG_OK;
   }
@@ -656,6 +667,13 @@ int psg_key_union(psg_ctx* c, int chl, const uint64_t* keys, size_t n) {
   if (n == 0) return PSG_OK;  // kv_vector.h:177: empty key list is ignored
   if (int rc = set_dev(c->device)) return rc;
   Channel& C = c->ch[chl];
+  // Pending value pushes of this channel were matched against the current
+  // key_[chl] in the reference (setValue matches at arrival,
+  // kv_vector.h:171-204): merge them before the key set (and so every
+  // position) changes.
+  for (auto& kv : c->agg)
+    if (kv.second.chl == chl && !kv.second.pending.empty())
+      if (int rc = c->flush(kv.second)) return rc;
   const size_t sb = psg::union_scratch_bytes(n);
   if (int rc = c->ensure_scratch(align_up(sb, 256) + 8 * n)) return rc;
   uint64_t* d_new = (uint64_t*)((char*)c->scratch + align_up(sb, 256));

@@ -164,11 +164,11 @@ def dense_pushes(npush: int = 8, n: int = 16777216, seed: int = 4,
 
 
 def uniform_pushes(seed: int = 5, npush: int = 256, n: int = 262144,
-                   rank_max: int = 10 ** 9, dtype=np.float32, m: int = 1):
-    """cfg5: unique uniform ranks in [0, rank_max), murmur-shuffled."""
+                   rank_max: int = 10 ** 9, dtype=np.float32, m: int = 1, union: bool = True):
+    """cfg5: unique uniform ranks in [0, rank_max), murmur-shuffled.
+    Returns (D, pushes); D (the union) is None when ``union`` is False."""
     rng = np.random.default_rng(seed)
     pushes = []
-    allk = []
     for p in range(npush):
         r = np.unique(rng.integers(0, rank_max, size=n + n // 8, dtype=np.uint64))
         while r.size < n:
@@ -177,5 +177,30 @@ def uniform_pushes(seed: int = 5, npush: int = 256, n: int = 262144,
         k = np.unique(murmur_shuffle(r))
         vals = [uniform_values(seed * 1000003 + p * 17 + i, k.size, dtype) for i in range(m)]
         pushes.append((k, vals))
-        allk.append(k)
-    return np.unique(np.concatenate(allk)), pushes
+    D = np.unique(np.concatenate([k for k, _ in pushes])) if union else None
+    return D, pushes
+
+
+def shard_pieces(pushes, bounds, shard: int):
+    """Each push's piece for server shard [bounds[shard], bounds[shard+1]):
+    the lower_bound cut of sliceKeyOrderedMsg (reference message.h:96-99)
+    at Range::all().evenDivide bounds (range.h:85-98).  Zero-copy views."""
+    lo, hi = np.uint64(bounds[shard]), np.uint64(bounds[shard + 1])
+    out = []
+    for k, vs in pushes:
+        a, b = np.searchsorted(k, [lo, hi], side="left")
+        out.append((k[a:b], [v[a:b] for v in vs]))
+    return out
+
+
+def cfg5_shard(shard: int = 0, nshards: int = 8, seed: int = 5, npush: int = 256,
+               n: int = 262144, dtype=np.float32, m: int = 1):
+    """cfg5 as server shard `shard` of `nshards` receives it when workers
+    slice their pushes (mode A): (D_shard, [piece per push]), D_shard = the
+    union of the pieces = the shard's slice of the global key set."""
+    from .kv_vector import shard_bounds
+    b = shard_bounds(nshards)
+    _, pushes = uniform_pushes(seed, npush, n, dtype=dtype, m=m, union=False)
+    pieces = shard_pieces(pushes, b, shard)
+    D = np.unique(np.concatenate([k for k, _ in pieces]))
+    return D, pieces

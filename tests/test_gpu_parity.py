@@ -308,22 +308,173 @@ def test_plan_cfg4_full_dense(torch_cuda):
     assert_bitexact(keep[3][0].cpu().numpy(), want[0])
 
 
-def test_plan_persistent_tile_variant(torch_cuda, monkeypatch):
-    """The persistent tile-kernel variant (PSG_PERSIST=1, DESIGN.md 4.2: next
-    tile's push tables staged by LDS-DMA) on a grid of 8 workgroups, so every
-    workgroup walks many tiles, across jobs, push groups (40 pushes) and a
-    dense job: bit-exact against the oracle like the default kernel."""
+@pytest.mark.parametrize("mode", ["search", "stream"])
+def test_plan_partition_modes_agree(torch_cuda, mode, monkeypatch):
+    """Both partition modes on dense and sparse jobs, forced
+    with PSG_PART_MODE (read at plan creation): every (push, tile) piece must
+    come out the same, so the merge is bit-exact either way, including
+    pushes much sparser than the tiles (window fallback of the stream mode)
+    and pushes with keys below D[0] or above D[-1] only in other tiles."""
     torch = torch_cuda
     from parameter_server_amd import synth
-    monkeypatch.setenv("PSG_PERSIST", "1")
-    monkeypatch.setenv("PSG_PERSIST_BLOCKS", "8")
-    cases = [synth.overlap_pushes(5, npush=8, n=30000),
-             synth.dense_pushes(npush=3, n=1 << 18),
-             synth.overlap_pushes(6, npush=40, n=3000, overlap=0.5)]
+    monkeypatch.setenv("PSG_PART_MODE", mode)
+    rng = np.random.default_rng(77)
+    D = np.unique(rng.integers(0, 1 << 60, 300000, dtype=np.uint64))
+    sparse = [(np.sort(rng.choice(D, n, replace=False)),
+               [rng.standard_normal(n).astype(np.float32)]) for n in (3, 40, 700, 5000, 1)]
+    cases = [synth.overlap_pushes(21, npush=8, n=30000),
+             (D, sparse),
+             synth.zipf_pushes(22, npush=20, n=4000)]
     for parallel in (False, True):
         plan, keep = plan_for(torch, cases, parallel=parallel)
         plan.run()
         assert plan.matched().tolist() == [k.size for _, ps in cases for k, _ in ps]
-        for (D, pushes), out in zip(cases, keep[3::4]):
-            _, _, _, want, _ = O.aggregate(D, *ALL, pushes, parallel=parallel)
-            assert_bitexact(out[0].cpu().numpy()[: D.size], want[0])
+        for (Dj, pushes), out in zip(cases, keep[3::4]):
+            _, _, _, want, _ = O.aggregate(Dj, *ALL, pushes, parallel=parallel)
+            assert_bitexact(out[0].cpu().numpy()[: Dj.size], want[0])
+
+
+def test_plan_cfg3_full_size(torch_cuda):
+    """cfg3 at its configured shape (BASELINE.json configs[2]): 64 pushes x
+    131,072 unique murmur-shuffled Zipf(1.1) ranks in [1, 1e9]
+    (synth.zipf_pushes defaults), f32, both match modes."""
+    torch = torch_cuda
+    from parameter_server_amd import synth
+    D, pushes = synth.zipf_pushes()
+    assert len(pushes) == 64 and all(k.size == 131072 for k, _ in pushes)
+    for parallel in (False, True):
+        plan, keep = plan_for(torch, [(D, pushes)], parallel=parallel)
+        plan.run()
+        assert plan.matched().tolist() == [131072] * 64
+        _, _, _, want, _ = O.aggregate(D, *ALL, pushes, parallel=parallel)
+        assert_bitexact(keep[3][0].cpu().numpy()[: D.size], want[0])
+
+
+def test_plan_cfg5_shard(torch_cuda):
+    """cfg5 (BASELINE.json configs[4]) as one GPU's shard: 256 pushes x
+    262,144 unique murmur-shuffled uniform ranks in [0, 1e9), cut at the
+    8-shard evenDivide bounds (range.h:85-98) by sliceKeyOrderedMsg's
+    lower_bound rule (message.h:96-99); shard 0's pieces merged on the GPU
+    against the oracle's merge of the same pieces over the shard's keys."""
+    torch = torch_cuda
+    from parameter_server_amd import synth
+    from parameter_server_amd.kv_vector import shard_bounds
+    b = shard_bounds(8)
+    D, pieces = synth.cfg5_shard(0, 8)
+    assert len(pieces) == 256
+    assert D.size > 0 and int(D[-1]) < int(b[1])
+    plan, keep = plan_for(torch, [(D, pieces)])
+    plan.run()
+    assert plan.matched().tolist() == [k.size for k, _ in pieces]
+    _, _, _, want, _ = O.aggregate(D, int(b[0]), int(b[1]), pieces)
+    assert_bitexact(keep[3][0].cpu().numpy()[: D.size], want[0])
+
+
+def test_rcv1_shape_blocks(torch_cuda):
+    """cfg1 (rcv1 L1-LR via Darling) shape through the host API: 47,236
+    server keys in [1, 47237), feature blocks as key ranges, 2 workers
+    pushing ~150 keys each per block with m = 2 f64 arrays (G and U,
+    darling.cc:196-220); received(t) per block against the oracle, serial
+    and parallel (the data itself cannot be fetched)."""
+    rng = np.random.default_rng(1)
+    D = np.arange(1, 47237, dtype=np.uint64)
+    edges = np.linspace(1, 47237, 298).astype(np.uint64)  # 297 blocks per pass
+    for parallel in (False, True):
+        v = kvv(np.float64, parallel)
+        v.setValue(msg(D))
+        for t, blk in enumerate(range(0, 297, 15)):
+            kb, ke = int(edges[blk]), int(edges[blk + 1])
+            inr = D[(D >= kb) & (D < ke)]
+            pushes = []
+            for wkr in range(2):
+                k = np.sort(rng.choice(inr, min(inr.size, 150), replace=False))
+                pushes.append((k, [rng.standard_normal(k.size), rng.standard_normal(k.size)]))
+                v.setValue(msg(k, pushes[-1][1], t=t, rng=(kb, ke)))
+            out = v.received(t)
+            rc, lo, hi, want, _ = O.aggregate(D, kb, ke, pushes, parallel, 1, np.float64)
+            assert rc == 0 and len(out) == 2
+            for i in range(2):
+                assert tuple(out[i][0]) == (lo, hi)
+                assert_bitexact(out[i][1], want[i])
+        v.close()
+
+
+def test_plan_empty_first_push_keeps_negative_zero(torch_cuda):
+    """An empty push is ignored (kv_vector.h:90,177): when the caller's first
+    push is empty, the first NON-empty push assigns, so its -0.0 stays -0.0
+    where no later push holds the key (parallel), and the serial path's
+    trailing +0.0 canonicalises it exactly as the reference's dense += does."""
+    torch = torch_cuda
+    D = np.array([2, 4, 6, 8], np.uint64)
+    pushes = [(np.zeros(0, np.uint64), [np.zeros(0, np.float32)]),
+              (np.array([2, 4], np.uint64), [np.array([-0.0, 1.5], np.float32)]),
+              (np.array([4, 8], np.uint64), [np.array([2.0, -0.0], np.float32)])]
+    for parallel in (False, True):
+        plan, keep = plan_for(torch, [(D, pushes)], parallel=parallel)
+        plan.run()
+        assert plan.matched().tolist() == [0, 2, 2]
+        _, _, _, want, _ = O.aggregate(D, *ALL, pushes[1:], parallel=parallel)
+        got = keep[3][0].cpu().numpy()
+        assert_bitexact(got, want[0])
+        assert np.signbit(got[0]) == (parallel is True)  # -0.0 kept only by parallel
+
+
+def test_key_union_between_push_and_received(torch_cuda):
+    """A key-only push that lands between a value push at time t and
+    received(t) (keys added below and inside the range): the pending push
+    was matched against the key set it arrived with (kv_vector.h:171-204),
+    so received(t) equals the oracle over the OLD keys and positions."""
+    D = np.array([10, 20, 30, 40, 50], np.uint64)
+    v = kvv()
+    v.setValue(msg(D))
+    k = np.array([20, 40], np.uint64)
+    v.setValue(msg(k, [np.array([1.0, 2.0], np.float32)], t=3))
+    v.setValue(msg(np.array([5, 25, 45], np.uint64)))  # union changes every position
+    (rng, got), = v.received(3)
+    _, lo, hi, want, _ = O.aggregate(D, *ALL, [(k, [np.array([1.0, 2.0], np.float32)])])
+    assert tuple(rng) == (lo, hi) and got.tolist() == want[0].tolist()
+    assert v.key(0).tolist() == [5, 10, 20, 25, 30, 40, 45, 50]
+    v.close()
+
+
+def test_device_entry_points(torch_cuda):
+    """psg_gather_dev, psg_key_union_dev and psg_slice_dev on device buffers
+    against the oracle's gather / setUnion / sliceKeyOrderedMsg."""
+    torch = torch_cuda
+    import ctypes as C
+    from parameter_server_amd import _lib
+    from parameter_server_amd.kv_vector import shard_bounds
+    L = _lib.lib()
+    rng = np.random.default_rng(9)
+    D = np.unique(rng.integers(0, 1 << 62, 50000, dtype=np.uint64))
+    W = rng.standard_normal(D.size).astype(np.float32)
+    req = np.sort(np.concatenate([rng.choice(D, 4000, replace=False),
+                                  rng.integers(0, 1 << 62, 500, dtype=np.uint64)]))
+    dD, dW, dR = to_dev(torch, D), to_dev(torch, W), to_dev(torch, req)
+    dout = torch.empty(req.size, dtype=torch.float32, device="cuda")
+    dm = torch.zeros(1, dtype=torch.int64, device="cuda")
+    _lib.check(L.psg_gather_dev(_lib.PSG_F32, dD.data_ptr(), D.size, dW.data_ptr(), dR.data_ptr(),
+                                req.size, dout.data_ptr(), dm.data_ptr(), None))
+    want, wm = O.gather(D, W, req)
+    assert int(dm.item()) == wm
+    assert_bitexact(dout.cpu().numpy(), want)
+    a = np.unique(rng.integers(0, 1 << 40, 30000, dtype=np.uint64))
+    bb = np.unique(rng.integers(0, 1 << 40, 20000, dtype=np.uint64))
+    da, db = to_dev(torch, a), to_dev(torch, bb)
+    du = torch.empty(a.size + bb.size, dtype=torch.int64, device="cuda")
+    nout = C.c_uint64()
+    _lib.check(L.psg_key_union_dev(da.data_ptr(), a.size, db.data_ptr(), bb.size, du.data_ptr(),
+                                   C.byref(nout), None))
+    assert np.array_equal(du.cpu().numpy().view(np.uint64)[: nout.value], O.set_union(a, bb))
+    bad = to_dev(torch, np.array([5, 3], np.uint64))
+    assert L.psg_key_union_dev(da.data_ptr(), a.size, bad.data_ptr(), 2, du.data_ptr(),
+                               C.byref(nout), None) == _lib.PSG_ERR_UNSORTED
+    sep = shard_bounds(8)
+    for kb, ke in ((0, (1 << 64) - 1), (int(D[100]), int(D[-100]))):
+        dsep = to_dev(torch, sep)
+        dpos = torch.empty(sep.size, dtype=torch.int64, device="cuda")
+        _lib.check(L.psg_slice_dev(dD.data_ptr(), D.size, kb, ke, dsep.data_ptr(), sep.size,
+                                   dpos.data_ptr(), None))
+        torch.cuda.synchronize()
+        pos, _ = O.slice_key_ordered(D, kb, ke, sep)
+        assert np.array_equal(dpos.cpu().numpy().view(np.uint64), pos)
