@@ -6,24 +6,31 @@ aggregate = 8 worker pushes x 131,072 sorted unique uint64 keys with f32
 values, 10 % of the keys shared by all pushes, U = 956,827 server keys.
 A step is one pass of the hot path (partition + aggregate kernels) over a
 batch of --batch such aggregates per GPU (default 64: 1.54 GB of distinct
-inputs/outputs, 6x the 256 MB Infinity Cache, so the rate is an HBM rate;
-SURVEY 8d sizes one merge at ~4 us at the target, so a launch should carry
->= 64 of them to amortise launch and tail).
+inputs/outputs, 6x the 256 MB Infinity Cache, so the rate is an HBM rate).
 
 Multi-GPU (one process per GPU, torchrun): the key space is range-
 partitioned with Range<uint64>::all().evenDivide(N, rank) (reference
-linear_method.cc:137-145); each rank holds the shard of every aggregate
-that its key range owns, exactly what the reference's worker-side
-sliceKeyOrderedMsg delivers (message.h:89-123), so the data path has no
-collective and per-GPU work is fixed ("scaling": "weak").  --ingress
-unsliced instead hands every rank whole pushes and re-homes the pieces with
-an RCCL all-to-all before merging (SURVEY 8e mode B).
+linear_method.cc:137-145).  The headline line shards the units (aggregates'
+key ranges) across ranks with no data-path collective: each rank holds the
+shard of --batch aggregates that its key range owns, exactly what the
+reference's worker-side sliceKeyOrderedMsg delivers (message.h:89-123);
+per-GPU work is fixed ("scaling": "weak").
+
+The line also carries a "cfg5" block (BASELINE.json configs[4], the
+north star's 8-GPU target): ONE fixed global workload -- 256 worker pushes
+x 262,144 murmur-shuffled uniform keys over a 1e9-rank (1 B-key) space --
+range-partitioned over the N ranks (strong scaling), timed on all ranks
+together, plus the same whole workload on ONE GPU (rank 0) in the same job,
+so "speedup_vs_1gpu" is measured, not inferred.
+
+--workload cfg3|cfg4|cfg5 runs a single-GPU side line of that config.
 
 Prints ONE JSON line on rank 0.
 """
 from __future__ import annotations
 
 import argparse
+import ctypes
 import json
 import os
 import sys
@@ -37,40 +44,108 @@ sys.path.insert(0, ROOT)
 HBM_PEAK_GBPS = 8000.0  # MI355X_MICROARCH.md: HBM3E 8.0 TB/s spec
 METRIC = "aggregated kv-pairs/s (device-resident), N-way sparse push merge at 1/2/4/8 GPU"
 
+WORKLOADS = {
+    "cfg2": dict(batch=64, desc=(
+        "cfg2: {a.npush} pushes x {a.n} sorted unique uint64 keys + f32 values, 10% shared "
+        "keys (U={U:,}); {batch} such (channel,time) aggregates per GPU per step")),
+    "cfg3": dict(batch=2, desc=(
+        "cfg3 (CTR shape): 64 pushes x 131072 unique murmur-shuffled Zipf(1.1) ranks in "
+        "[1,1e9] + f32 values (U={U:,}); {batch} such aggregates per step")),
+    "cfg4": dict(batch=1, desc=(
+        "cfg4 (dense-bucket limit): 8 pushes of all keys [0,16777216) + f32 values "
+        "(U={U:,}); {batch} such aggregate per step")),
+    "cfg5": dict(batch=1, desc=(
+        "cfg5: 256 pushes x 262144 unique murmur-shuffled uniform ranks in [0,1e9) + f32 "
+        "values (U={U:,}), the whole 1 B-key-space aggregate on one GPU")),
+}
+
 
 def parse():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=20)
     ap.add_argument("--warmup", type=int, default=5)
-    ap.add_argument("--batch", type=int, default=64, help="cfg2 aggregates per GPU per step")
+    ap.add_argument("--batch", type=int, default=0,
+                    help="aggregates per GPU per step (default: 64 for cfg2, else 1-2)")
     ap.add_argument("--npush", type=int, default=8)
     ap.add_argument("--n", type=int, default=131072)
     ap.add_argument("--overlap", type=float, default=0.1)
-    ap.add_argument("--workload", choices=["cfg2", "cfg3", "cfg4"], default="cfg2",
-                    help="cfg2 (default, the headline); cfg3 CTR shape (64 Zipf(1.1) "
-                         "murmur-keyed pushes x 131072) and cfg4 dense (8 x 16 M contiguous "
-                         "keys) are single-GPU side lines (BASELINE.json configs[2], [3])")
-    ap.add_argument("--ingress", choices=["sliced", "unsliced"], default="sliced")
+    ap.add_argument("--workload", choices=sorted(WORKLOADS), default="cfg2")
+    ap.add_argument("--no-cfg5", action="store_true",
+                    help="skip the cfg5 strong-scaling block of the default line")
+    ap.add_argument("--cfg5-steps", type=int, default=10)
     ap.add_argument("--cpu-seconds", type=float, default=10.0)
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--no-check", action="store_true",
+                    help="skip the matched-count guard (ablation builds via PSG_LIB_PATH only)")
     ap.add_argument("--profile-steps", type=int, default=0,
-                    help="only run warmup+steps (for rocprofv3); skip baselines")
-    return ap.parse_args()
-
-
-WORKLOADS = {
-    "cfg2": ("cfg2: {a.npush} pushes x {a.n} sorted unique uint64 keys + f32 values, 10% shared "
-             "keys (U={U:,}); {a.batch} such (channel,time) aggregates per GPU per step"),
-    "cfg3": ("cfg3 (CTR shape): 64 pushes x 131072 unique murmur-shuffled Zipf(1.1) ranks in "
-             "[1,1e9] + f32 values (U={U:,}); {a.batch} such aggregates per step"),
-    "cfg4": ("cfg4 (dense-bucket limit): 8 pushes of all keys [0,16777216) + f32 values "
-             "(U={U:,}); {a.batch} such aggregates per step"),
-}
+                    help="only run warmup+steps (for rocprofv3); skip baselines and blocks")
+    a = ap.parse_args()
+    if not a.batch:
+        a.batch = WORKLOADS[a.workload]["batch"]
+    return a
 
 
 def log(msg):
     print(f"[bench] {msg}", file=sys.stderr, flush=True)
+
+
+def to_dev(a, dev):
+    import torch
+    a = np.ascontiguousarray(a)
+    return torch.from_numpy(a.view(np.int64) if a.dtype == np.uint64 else a).to(dev)
+
+
+def make_plan(insts, dev, local):
+    """MergePlan over [(D, pushes)] resident on `dev`; returns (plan, keep, jobs)."""
+    import torch
+    from parameter_server_amd.kv_vector import MergePlan
+    from parameter_server_amd._lib import PSG_F32
+    keep, jobs = [], []
+    for D, pushes in insts:
+        dD = to_dev(D, dev)
+        pk = [to_dev(k, dev) for k, _ in pushes]
+        pv = [[to_dev(v, dev) for v in vs] for _, vs in pushes]
+        out = torch.empty(max(1, D.size), dtype=torch.float32, device=dev)
+        keep.append((dD, pk, pv, out))
+        jobs.append({"keys": dD.data_ptr(), "nslots": int(D.size),
+                     "push_keys": [t.data_ptr() for t in pk],
+                     "push_vals": [[t.data_ptr() for t in vs] for vs in pv],
+                     "push_n": [int(k.size) for k, _ in pushes],
+                     "out": [out.data_ptr()]})
+    plan = MergePlan(local, PSG_F32, 1, jobs)
+    return plan, keep, jobs
+
+
+def timed_steps(plan, K, W, stream, dist):
+    """W untimed warm-up steps, then exactly K timed steps bracketed by a
+    barrier + device synchronize on both sides.  Returns (wall s, mean
+    partition ms, mean aggregate ms); the stage times are HIP events on the
+    launch stream."""
+    import torch
+    sh = stream.cuda_stream
+    for _ in range(W):
+        plan.run(sh)
+    torch.cuda.synchronize()
+    if dist:
+        dist.barrier()
+    torch.cuda.synchronize()
+    ev = [[torch.cuda.Event(enable_timing=True) for _ in range(3)] for _ in range(K)]
+    t0 = time.perf_counter()
+    for s in range(K):
+        ev[s][0].record(stream)
+        plan.run_stage(0, sh)
+        ev[s][1].record(stream)
+        plan.run_stage(1, sh)
+        ev[s][2].record(stream)
+    torch.cuda.synchronize()
+    if dist:
+        dist.barrier()
+    torch.cuda.synchronize()
+    wall = time.perf_counter() - t0
+    part = float(np.mean([ev[s][0].elapsed_time(ev[s][1]) for s in range(K)]))
+    agg = float(np.mean([ev[s][1].elapsed_time(ev[s][2]) for s in range(K)]))
+    return wall, part, agg
 
 
 def main():
@@ -88,139 +163,66 @@ def main():
         dist.init_process_group("nccl", device_id=torch.device("cuda", local))
 
     from parameter_server_amd import synth
-    from parameter_server_amd.kv_vector import MergePlan, shard_bounds
-    from parameter_server_amd._lib import PSG_F32
+    from parameter_server_amd.kv_vector import shard_bounds
 
     bounds = shard_bounds(world)
     lo, hi = int(bounds[rank]), int(bounds[rank + 1])
+    dev = torch.device("cuda", local)
+    wl = args.workload
 
     # ---- synthetic inputs (each rank: its shard of `batch` aggregates) ----
     t0 = time.time()
-    if args.workload != "cfg2":
-        if world > 1:
-            raise SystemExit("--workload cfg3/cfg4 are single-GPU side lines")
-        insts = [synth.zipf_pushes(seed=3 + j) if args.workload == "cfg3"
-                 else synth.dense_pushes(seed=4 + j) for j in range(args.batch)]
-    elif args.ingress == "sliced":
+    if wl != "cfg2" and world > 1:
+        raise SystemExit("--workload cfg3/cfg4/cfg5 are single-GPU side lines; the default "
+                         "line carries cfg5's multi-GPU strong-scaling block")
+    if wl == "cfg2":
         insts = [synth.shard_instance(seed=1 + j + 1000 * rank, lo=lo, hi=hi,
                                       npush=args.npush, n=args.n, overlap=args.overlap)
                  for j in range(args.batch)]
+    elif wl == "cfg3":
+        insts = [synth.zipf_pushes(seed=3 + j) for j in range(args.batch)]
+    elif wl == "cfg4":
+        insts = [synth.dense_pushes(seed=4 + j) for j in range(args.batch)]
     else:
-        # mode B: this rank's workers push whole pushes; they are re-homed by
-        # an all-to-all inside every timed step (shard.UnslicedExchange)
-        aggs = [synth.overlap_pushes(1 + j + 1000 * rank, args.npush, args.n, args.overlap)[1]
-                for j in range(args.batch)]
-        insts = None
-    log(f"rank {rank}: generated {args.batch} aggregates in {time.time() - t0:.1f}s")
+        insts = [synth.uniform_pushes(seed=5 + j) for j in range(args.batch)]
+    log(f"rank {rank}: generated {args.batch} {wl} aggregates in {time.time() - t0:.1f}s")
 
-    dev = torch.device("cuda", local)
-
-    def to_dev(a):
-        a = np.ascontiguousarray(a)
-        return torch.from_numpy(a.view(np.int64) if a.dtype == np.uint64 else a).to(dev)
-
-    keep, jobs = [], []
-    ex = None
-    if insts is None:
-        from parameter_server_amd import shard as S
-        ex = S.UnslicedExchange(aggs, bounds, dist, dev)
-        ex.run()
-        torch.cuda.synchronize()
-        rk = ex.recv_keys.cpu().numpy().view(np.uint64)
-        for j in range(args.batch):
-            pcs = ex.pieces(j)
-            if not pcs:
-                continue
-            D = np.unique(np.concatenate([rk[o:o + c] for o, c in pcs]))
-            dD = to_dev(D)
-            out = torch.empty(max(1, D.size), dtype=torch.float32, device=dev)
-            keep.append((dD, out))
-            jobs.append({"keys": dD.data_ptr(), "nslots": int(D.size),
-                         "push_keys": [ex.recv_keys.data_ptr() + 8 * o for o, _ in pcs],
-                         "push_vals": [[ex.recv_vals[0].data_ptr() + 4 * o] for o, _ in pcs],
-                         "push_n": [c for _, c in pcs],
-                         "out": [out.data_ptr()]})
-        del rk
-    for D, pushes in insts or []:
-        dD = to_dev(D)
-        pk = [to_dev(k) for k, _ in pushes]
-        pv = [[to_dev(v) for v in vs] for _, vs in pushes]
-        out = torch.empty(max(1, D.size), dtype=torch.float32, device=dev)
-        keep.append((dD, pk, pv, out))
-        jobs.append({"keys": dD.data_ptr(), "nslots": int(D.size),
-                     "push_keys": [t.data_ptr() for t in pk],
-                     "push_vals": [[t.data_ptr() for t in vs] for vs in pv],
-                     "push_n": [int(k.size) for k, _ in pushes],
-                     "out": [out.data_ptr()]})
-    plan = MergePlan(local, PSG_F32, 1, jobs)
+    plan, keep, jobs = make_plan(insts, dev, local)
     stream = torch.cuda.current_stream()
-    sh = stream.cuda_stream
 
     # correctness guard: every pushed key matched
-    plan.run(sh)
-    mt = plan.matched()
+    plan.run(stream.cuda_stream)
     want = np.array([n for jb in jobs for n in jb["push_n"]], np.uint64)
-    assert np.array_equal(mt, want), "unmatched keys in the bench workload"
-
-    for _ in range(args.warmup):
-        if ex is not None:
-            ex.run()
-        plan.run(sh)
-    torch.cuda.synchronize()
-    if dist:
-        dist.barrier()
-    torch.cuda.synchronize()
+    assert args.no_check or np.array_equal(plan.matched(), want), \
+        "unmatched keys in the bench workload"
 
     K = args.steps
-    ev = [[torch.cuda.Event(enable_timing=True) for _ in range(4)] for _ in range(K)]
-    t_start = time.perf_counter()
-    for s in range(K):
-        ev[s][3].record(stream)
-        if ex is not None:
-            ex.run()  # mode B: the RCCL all-to-all re-homing is part of the step
-        ev[s][0].record(stream)
-        plan.run_stage(0, sh)
-        ev[s][1].record(stream)
-        plan.run_stage(1, sh)
-        ev[s][2].record(stream)
-    torch.cuda.synchronize()
-    if dist:
-        dist.barrier()
-    torch.cuda.synchronize()
-    wall = time.perf_counter() - t_start
-
-    part_ms = float(np.mean([ev[s][0].elapsed_time(ev[s][1]) for s in range(K)]))
-    agg_ms = float(np.mean([ev[s][1].elapsed_time(ev[s][2]) for s in range(K)]))
-    xchg_ms = float(np.mean([ev[s][3].elapsed_time(ev[s][0]) for s in range(K)]))
-
+    wall, part_ms, agg_ms = timed_steps(plan, K, args.warmup, stream, dist)
     wall_max, kv_all = reduce_over_ranks(wall, plan.kv_pairs, dist, dev)
     value = kv_all * K / wall_max
     ms_per_step = wall_max / K * 1e3
 
     if args.profile_steps:
         if rank == 0:
-            log(f"profile run: {ms_per_step:.3f} ms/step, aggregate {agg_ms:.3f} ms")
+            log(f"profile run: {ms_per_step:.3f} ms/step, aggregate {agg_ms:.3f} ms, "
+                f"partition {part_ms:.3f} ms")
         if dist:
             dist.destroy_process_group()
         return
 
-    # copy-kernel bandwidth in the same run (read + write bytes / time)
-    nbytes = 1 << 30
-    src = torch.empty(nbytes // 4, dtype=torch.float32, device=dev)
-    dst = torch.empty_like(src)
-    for _ in range(3):
-        dst.copy_(src)
-    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-    e0.record(stream)
-    for _ in range(10):
-        dst.copy_(src)
-    e1.record(stream)
-    torch.cuda.synchronize()
-    copy_gbps = 2 * nbytes * 10 / (e0.elapsed_time(e1) * 1e-3) / 1e9
-    del src, dst
-
-    achieved = plan.bytes / (agg_ms * 1e-3) / 1e9
-    traffic = load_traffic(args, plan.bytes)
+    # roofline of the aggregate kernel: ALGORITHMIC bytes per launch (SURVEY
+    # 8d) / its mean HIP-event duration; cfg4 is priced in the dense form
+    U = sum(int(jb["nslots"]) for jb in jobs)
+    if wl == "cfg4":
+        nbytes = int(plan.kv_pairs) * 4 + U * 4
+        formula = "dense form: sum_p n_p*4 [push values] + U*4 [sums] (keys implied, SURVEY 8d)"
+    else:
+        nbytes = int(plan.bytes)
+        formula = "sum_p n_p*(8+4) [pushes] + U*(8+4) [server keys + sums] (SURVEY 8d)"
+    achieved = nbytes / (agg_ms * 1e-3) / 1e9
+    step_gbps = nbytes / (ms_per_step * 1e-3) / 1e9
+    copy_gbps = copy_bandwidth(dev, stream)
+    traffic = load_traffic(nbytes, wl)
 
     result = {
         "metric": METRIC,
@@ -236,13 +238,12 @@ def main():
         "dtype": "f32",
         "data": "synthetic",
         "config": {
-            "workload": WORKLOADS[args.workload].format(a=args, U=jobs[0]["nslots"] if jobs else 0),
+            "workload": WORKLOADS[wl]["desc"].format(a=args, U=jobs[0]["nslots"] if jobs else 0,
+                                                     batch=args.batch),
             "global_batch": args.batch * world,
             "kv_per_step": kv_all,
-            "parallelism": (f"key-range shards evenDivide({world}); "
-                            + ("worker-sliced ingress, no data-path collective"
-                               if ex is None else
-                               "unsliced ingress, RCCL all-to-all re-homing in every step")),
+            "parallelism": (f"key-range shards evenDivide({world}); worker-sliced ingress, "
+                            "no data-path collective"),
         },
         "roofline": {
             "bound": "hbm",
@@ -250,27 +251,89 @@ def main():
             "peak": HBM_PEAK_GBPS,
             "unit": "GB/s",
             "frac": achieved / HBM_PEAK_GBPS,
-            "traffic": traffic,
-            "kernel": kernel_name(),
-            "bytes_per_launch": plan.bytes,
-            "bytes_formula": "sum_p n_p*(8+4) [pushes] + U*(8+4) [server keys + sums]",
+            "traffic": traffic.get("tile") if traffic else None,
+            "kernel": "tile_kernel<float,1>",
+            "bytes_per_launch": nbytes,
+            "bytes_formula": formula,
             "kernel_ms": agg_ms,
             "partition_ms": part_ms,
+            "step_achieved": step_gbps,
+            "step_frac": step_gbps / HBM_PEAK_GBPS,
+            "traffic_partition": traffic.get("partition") if traffic else None,
+            "traffic_source": traffic.get("source") if traffic else None,
             "measured_copy_GBps": copy_gbps,
-            "frac_of_measured_copy": achieved / copy_gbps,
+            "frac_of_measured_copy": achieved / copy_gbps if copy_gbps else None,
         },
     }
-    if ex is not None:
-        result["exchange"] = {"ms": xchg_ms, "bytes_sent_per_rank": ex.sent_bytes,
-                              "scope": "gather into destination order + all-to-all of keys "
-                                       "and values (RCCL), per step, rank 0's HIP events"}
-    if rank == 0 and world == 1 and not args.no_cpu_baseline and ex is None:
+    if wl == "cfg2" and not args.no_cfg5:
+        del plan, keep
+        torch.cuda.empty_cache()
+        result["cfg5"] = cfg5_block(args, rank, world, bounds, dist, dev, local, stream)
+    if rank == 0 and world == 1 and not args.no_cpu_baseline and wl == "cfg2":
         result["end_to_end"] = end_to_end(insts[0], local)
         result["cpu_baseline"] = cpu_baseline(insts[0], args.cpu_seconds)
     if rank == 0:
         print(json.dumps(result), flush=True)
     if dist:
         dist.destroy_process_group()
+
+
+def cfg5_block(args, rank, world, bounds, dist, dev, local, stream):
+    """BASELINE.json configs[4]: one fixed global workload (256 pushes x
+    262,144 keys over a 1 B-key space), range-partitioned over the N ranks
+    with worker-sliced ingress (each rank merges its shard's pieces of all
+    256 pushes; no data-path collective), and the same whole workload on
+    rank 0's GPU alone in the same job."""
+    import torch
+    from parameter_server_amd import synth
+    t0 = time.time()
+    _, pushes = synth.uniform_pushes(seed=5, union=False)
+    kv_total = sum(int(k.size) for k, _ in pushes)
+    pieces = synth.shard_pieces(pushes, bounds, rank)
+    D = np.unique(np.concatenate([k for k, _ in pieces]))
+    log(f"rank {rank}: cfg5 shard {D.size:,} keys generated in {time.time() - t0:.1f}s")
+    plan, keep, jobs = make_plan([(D, pieces)], dev, local)
+    plan.run(stream.cuda_stream)
+    assert args.no_check or np.array_equal(plan.matched(),
+                                            np.array([k.size for k, _ in pieces], np.uint64))
+    K = args.cfg5_steps
+    wall, part_ms, agg_ms = timed_steps(plan, K, 2, stream, dist)
+    wall_max, kv_all = reduce_over_ranks(wall, plan.kv_pairs, dist, dev)
+    assert int(kv_all) == kv_total
+    nbytes = int(plan.bytes)
+    out = {
+        "workload": ("256 pushes x 262144 murmur-shuffled uniform keys (1e9-rank space), "
+                     f"f32; fixed global workload split by evenDivide({world})"),
+        "scaling": "strong",
+        "n_gpus": world,
+        "value": kv_total * K / wall_max,
+        "unit": "kv-pairs/s",
+        "ms_per_step": wall_max / K * 1e3,
+        "rank0": {"slots": int(D.size), "kernel_ms": agg_ms, "partition_ms": part_ms,
+                  "bytes_per_launch": nbytes,
+                  "frac": nbytes / (agg_ms * 1e-3) / 1e9 / HBM_PEAK_GBPS,
+                  "step_frac": nbytes / (wall / K) / 1e9 / HBM_PEAK_GBPS},
+    }
+    del plan, keep
+    torch.cuda.empty_cache()
+    if world > 1:
+        # the same whole workload on ONE GPU (rank 0), the others waiting
+        t1 = None
+        if rank == 0:
+            Dall = np.unique(np.concatenate([k for k, _ in pushes]))
+            p1, k1, _ = make_plan([(Dall, pushes)], dev, local)
+            w1, _, _ = timed_steps(p1, K, 2, stream, None)
+            t1 = w1 / K
+            del p1, k1
+            torch.cuda.empty_cache()
+        dist.barrier()
+        if rank == 0:
+            out["one_gpu_ms_per_step"] = t1 * 1e3
+            out["speedup_vs_1gpu"] = t1 / (wall_max / K)
+    else:
+        out["one_gpu_ms_per_step"] = out["ms_per_step"]
+        out["speedup_vs_1gpu"] = 1.0
+    return out
 
 
 def reduce_over_ranks(wall, kv_rank, dist, dev):
@@ -287,9 +350,31 @@ def reduce_over_ranks(wall, kv_rank, dist, dev):
     return float(t[0].item()), float(t[1].item())
 
 
-def kernel_name():
-    """The aggregate kernel (psg_tile.hip)."""
-    return "tile_kernel<float,1>"
+def copy_bandwidth(dev, stream):
+    """HBM copy ceiling in the same run: tools/copybw (a hand-written 16-B
+    per lane copy kernel), 1 GiB -> 1 GiB, read + write bytes / time."""
+    import torch
+    path = os.path.join(ROOT, "tools", "copybw", "libcopybw.so")
+    if not os.path.exists(path):
+        return None
+    L = ctypes.CDLL(path)
+    L.copybw_copy.restype = ctypes.c_int
+    L.copybw_copy.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_size_t, ctypes.c_void_p]
+    nbytes = 1 << 30
+    src = torch.empty(nbytes // 4, dtype=torch.float32, device=dev)
+    dst = torch.empty_like(src)
+    sh = stream.cuda_stream
+    for _ in range(3):
+        L.copybw_copy(dst.data_ptr(), src.data_ptr(), nbytes, sh)
+    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    e0.record(stream)
+    for _ in range(10):
+        L.copybw_copy(dst.data_ptr(), src.data_ptr(), nbytes, sh)
+    e1.record(stream)
+    torch.cuda.synchronize()
+    gbps = 2 * nbytes * 10 / (e0.elapsed_time(e1) * 1e-3) / 1e9
+    del src, dst
+    return gbps
 
 
 def end_to_end(inst, device, reps=5):
@@ -297,7 +382,6 @@ def end_to_end(inst, device, reps=5):
     (KVVector.setValue per push from pageable host memory + received(t)
     D2H), the reference's own call pattern.  Reported beside `value`,
     never as it."""
-    import ctypes
     from parameter_server_amd.kv_vector import KVVector, Message
     D, pushes = inst
     kv = sum(int(k.size) for k, _ in pushes)
@@ -321,18 +405,21 @@ def end_to_end(inst, device, reps=5):
                       f"median of {reps}")}
 
 
-def load_traffic(args, bytes_per_launch):
-    """HBM bytes per aggregate launch from the committed rocprofv3 PMC
-    summary (profiles/pmc_summary.json, written by tools/pmc_traffic.py),
-    when it was collected on this same workload; else null."""
+def load_traffic(bytes_per_launch, workload):
+    """HBM bytes per launch of the aggregate and partition kernels from the
+    committed rocprofv3 PMC summary (profiles/pmc_summary.json, written by
+    tools/pmc_traffic.py), when it was collected on this same workload; else
+    null."""
     p = os.path.join(ROOT, "profiles", "pmc_summary.json")
     try:
         d = json.load(open(p))
     except Exception:
         return None
-    if d.get("bytes_per_launch") != bytes_per_launch:
+    if d.get("bytes_per_launch") != bytes_per_launch or d.get("workload", "cfg2") != workload:
         return None
-    return d.get("hbm_bytes_per_launch")
+    return {"tile": d.get("hbm_bytes_per_launch"),
+            "partition": d.get("partition_hbm_bytes_per_launch"),
+            "source": d.get("source")}
 
 
 def cpu_baseline(inst, seconds):
@@ -376,8 +463,10 @@ def cpu_baseline(inst, seconds):
         pass
     return {
         "value": v, "unit": "kv-pairs/s", "cores": 1, "kind": "port",
-        "sample": (f"{reps} x one cfg2 aggregate (8 x 131072 kv, U={D.size}) through "
-                   f"oracle serialSetValue restatement in {el:.1f}s, 1 thread, {model}"),
+        "sample": (f"{reps} x one cfg2 aggregate (8 x 131072 kv, U={D.size}) through the "
+                   f"oracle's serialSetValue restatement in {el:.1f}s on 1 thread of {model} "
+                   f"(host: nproc {os.cpu_count()}, this job's affinity {share} CPUs); the "
+                   "same 24 MB aggregate is re-run, so its inputs are warm in the host's L3"),
         "parallel_match_by_threads": par,
     }
 

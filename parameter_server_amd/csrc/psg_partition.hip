@@ -105,94 +105,98 @@ __device__ __forceinline__ void search_item(const JobDev& J, uint32_t p, uint32_
 }
 
 // ---- kStream: one wave per kStreamChunk consecutive keys of one push ----
-// T(k) = (number of splitters <= k) - 1, in [-1, ntiles]; seg[p][t] = number
-// of keys with T < t, written where T steps up between consecutive keys.
-__device__ __forceinline__ void stream_item(const JobDev& J, uint32_t p, uint32_t c, int lane) {
+// seg[p][t] = lower_bound(S_p, split[t]).  A chunk [i0, i0 + cl) owns the
+// splitters whose lower bound falls inside it (the push's last chunk also
+// those past its last key): split[t] > S[i0-1] and split[t] <= S[i0+cl-1].
+// One lane per splitter, 64 consecutive splitters per window; each lane
+// binary-searches its splitter in the chunk's keys, staged in LDS.
+__device__ __forceinline__ void stream_item(const JobDev& J, uint32_t p, uint32_t c, int lane,
+                                            uint64_t* ck /* LDS: this wave's chunk keys */) {
   const uint64_t* S = J.pkeys[p];
   const uint64_t n = J.pn[p];
   const uint32_t nt = J.ntiles;
   const uint64_t* sp = J.split;
   uint32_t* seg = J.seg + (size_t)p * (nt + 1u);
   const uint64_t i0 = (uint64_t)c * kStreamChunk;
-  // this lane's keys i0 + 4*lane + j
-  const uint64_t ib = i0 + 4u * (uint32_t)lane;
+  const uint32_t cl = (uint32_t)(n - i0 < kStreamChunk ? n - i0 : kStreamChunk);
+  const bool last = i0 + cl == n;
+  // the chunk's keys into LDS (4 per lane); +inf past the push's end
   uint64_t k[4];
 #pragma unroll
-  for (int j = 0; j < 4; ++j) k[j] = ib + j < n ? S[ib + j] : ~0ull;
-  // T0: tile of the key before the chunk (-1 for the push's first chunk);
-  // every key of a sorted chunk lies in a tile >= T0
+  for (int j = 0; j < 4; ++j) {
+    const uint32_t x = 4u * (uint32_t)lane + j;
+    k[j] = x < cl ? S[i0 + x] : ~0ull;
+  }
+  // T0 = (splitters <= S[i0-1]) - 1: an interpolated guess checked against a
+  // window of 64 splitters around it (murmur-hashed keys and D are near-
+  // uniform, so the guess is a few tiles off), else a 64-ary search
   int64_t T0 = -1;
-  const uint64_t kp = i0 > 0 ? uni64(S[i0 - 1]) : 0ull;
   if (i0 > 0) {
-    // upper_bound over split[0 .. nt] by 64-ary wave search
-    T0 = (int64_t)dev::wave_search(sp, (uint64_t)nt + 1u, kp, true, lane) - 1;
-  }
-  // window: the 64 splitters after T0, one per lane (past split[nt]: +inf)
-  const uint64_t w = T0 + 1 + lane <= (int64_t)nt ? sp[T0 + 1 + lane] : ~0ull;
-  const uint64_t wlast = uni64((uint64_t)__shfl((long long)w, 63, 64));
-  const bool wfull = T0 + 64 <= (int64_t)nt;  // the window's last entry is a real splitter
-  int64_t T[4];
-#pragma unroll
-  for (int j = 0; j < 4; ++j) {
-    const uint64_t key = k[j];
-    // splitters of the window <= key: a binary search over the lanes' window
-    // entries, by every lane (a shuffle reads nothing from an inactive lane)
-    int cnt = 0;
-#pragma unroll
-    for (int step = 32; step > 0; step >>= 1) {
-      const uint64_t wv = (uint64_t)__shfl((long long)w, cnt + step - 1, 64);
-      if (wv <= key) cnt += step;
+    const uint64_t kp = uni64(S[i0 - 1]);
+    const uint64_t s0 = uni64(sp[0]), sn = uni64(sp[nt]);
+    if (kp >= sn) {
+      T0 = nt;
+    } else if (kp >= s0) {
+      const double f = (double)(kp - s0) / (double)(sn - s0);
+      int64_t g = (int64_t)(f * (double)nt) - 32;
+      g = g < 0 ? 0 : (g + 64 > (int64_t)nt + 1 ? (int64_t)nt + 1 - 64 : g);
+      g = g < 0 ? 0 : g;
+      const int64_t t = g + lane;
+      const bool le = t <= (int64_t)nt && sp[t] <= kp;
+      const uint32_t cnt = (uint32_t)__popcll(__ballot(le));
+      const bool inside = (cnt > 0 || g == 0) && (cnt < 64 || g + 64 > (int64_t)nt);
+      if (inside)
+        T0 = g + (int64_t)cnt - 1;
+      else
+        T0 = (int64_t)dev::wave_search(sp, (uint64_t)nt + 1u, kp, true, lane) - 1;
     }
-    int64_t t = T0 + (int64_t)cnt;
-    if (wfull && key >= wlast) {
-      // beyond the window (a very sparse push): search the rest
-      uint64_t lo = (uint64_t)(T0 + 65), len = (uint64_t)nt + 1u - lo;
-      while (len > 0) {
-        const uint64_t half = len >> 1;
-        if (sp[lo + half] <= key) {
-          lo += half + 1;
-          len -= half + 1;
-        } else {
-          len = half;
-        }
-      }
-      t = (int64_t)lo - 1;
-    }
-    T[j] = t > (int64_t)nt ? (int64_t)nt : t;
   }
-  // predecessor of this lane's first key: lane-1's last key / tile; lane 0
-  // takes the key before the chunk (T0)
-  const int64_t Tp_l = (int64_t)__shfl_up((long long)T[3], 1, 64);
-  const uint64_t kp_l = (uint64_t)__shfl_up((long long)k[3], 1, 64);
-  int64_t Tp = lane == 0 ? T0 : Tp_l;
-  uint64_t kprev = lane == 0 ? kp : kp_l;
-  bool hasprev = lane > 0 || i0 > 0;
+  // stores before the wave's reads of them: LDS accesses of one wave are
+  // ordered; the fences keep the compiler from moving the reads up
+#pragma unroll
+  for (int j = 0; j < 4; ++j) ck[4 * lane + j] = k[j];
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+  __builtin_amdgcn_wave_barrier();
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+  const uint64_t klast = uni64(ck[cl - 1]);
+  for (int64_t t0 = T0 + 1; t0 <= (int64_t)nt; t0 += 64) {
+    const int64_t t = t0 + lane;
+    const uint64_t sv = t <= (int64_t)nt ? sp[t] : ~0ull;
+    // keys of the chunk below sv: lower_bound over ck[0, cl)
+    uint32_t pos = 0;
+#pragma unroll
+    for (uint32_t st = kStreamChunk / 2; st > 0; st >>= 1)
+      if (pos + st <= cl && ck[pos + st - 1] < sv) pos += st;
+    pos += (pos < cl && ck[pos] < sv) ? 1u : 0u;
+    if (t <= (int64_t)nt && (pos < cl || last)) seg[t] = (uint32_t)(i0 + pos);
+    // later windows own nothing once a splitter passes the chunk's last key
+    // (the push's last chunk fills every remaining boundary with n)
+    if (!last && uni64((uint64_t)__shfl((long long)sv, 63, 64)) > klast) break;
+  }
+  // order check: a key not above its predecessor cannot match
   uint32_t bad = 0;
+  {
+    const uint64_t kprev_l = (uint64_t)__shfl_up((long long)k[3], 1, 64);
+    uint64_t prev = lane == 0 ? (i0 > 0 ? S[i0 - 1] : 0ull) : kprev_l;
+    bool has = lane > 0 || i0 > 0;
 #pragma unroll
-  for (int j = 0; j < 4; ++j) {
-    const uint64_t i = ib + j;
-    if (i < n) {
-      if (hasprev && !(kprev < k[j])) ++bad;  // not strictly increasing
-      for (int64_t t = Tp + 1; t <= T[j]; ++t) seg[t] = (uint32_t)i;
-      if (T[j] > Tp) Tp = T[j];
-      kprev = k[j];
-      hasprev = true;
-      if (i == n - 1)  // past the push's last key: every later boundary is n
-        for (int64_t t = Tp + 1; t <= (int64_t)nt; ++t) seg[t] = (uint32_t)n;
+    for (int j = 0; j < 4; ++j) {
+      if (4u * (uint32_t)lane + j < cl) {
+        if (has && !(prev < k[j])) ++bad;
+        prev = k[j];
+        has = true;
+      }
     }
   }
-  const unsigned long long bm = __ballot(bad != 0);
-  if (bm) {
-    // a later key not above its predecessor: the push cannot match fully
-    if (bad)
-      __hip_atomic_fetch_add(J.fail + p, (unsigned long long)bad, __ATOMIC_RELAXED,
-                             __HIP_MEMORY_SCOPE_AGENT);
-  }
+  if (__ballot(bad != 0) && bad)
+    __hip_atomic_fetch_add(J.fail + p, (unsigned long long)bad, __ATOMIC_RELAXED,
+                           __HIP_MEMORY_SCOPE_AGENT);
 }
 
 __global__ __launch_bounds__(256) void partition_kernel(const JobDev* __restrict__ jobs,
                                                         const uint64_t* __restrict__ items,
                                                         uint32_t nitems) {
+  __shared__ uint64_t ck[4][kStreamChunk];
   const uint32_t item = uni((blockIdx.x * 256u + threadIdx.x) >> 6);
   const int lane = threadIdx.x & 63;
   if (item >= nitems) return;
@@ -202,7 +206,7 @@ __global__ __launch_bounds__(256) void partition_kernel(const JobDev* __restrict
   const uint32_t x = (uint32_t)it & 0xffffffu;
   const JobDev& J = jobs[j];
   if (J.mode == kStream)
-    stream_item(J, p, x, lane);
+    stream_item(J, p, x, lane, ck[threadIdx.x >> 6]);
   else
     search_item(J, p, x, lane);
 }

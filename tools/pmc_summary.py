@@ -1,4 +1,4 @@
-"""Summarise rocprofv3 CSV output of tools/pmc.sh: per-kernel mean duration
+"""Summarise rocprofv3 CSV output of tools/pmc2.sh: per-kernel mean duration
 and mean counter values per dispatch (HBM bytes with the gfx950 FETCH_SIZE
 x2 correction of MI355X_MICROARCH.md "HBM")."""
 import csv
@@ -16,8 +16,8 @@ def rows(pattern):
 
 
 def short(name):
-    for k in ("tile_kernel", "rows_kernel", "stream4_kernel", "stream3_kernel", "stream2_kernel", "stream_kernel", "aggregate_v5_kernel", "aggregate_v4_kernel",
-              "aggregate_kernel", "partition_kernel", "gather_kernel", "union", "slice_kernel"):
+    for k in ("tile_kernel", "splitter_kernel", "partition_kernel", "gather_kernel", "union",
+              "slice_kernel"):
         if k in name:
             return k
     return None
@@ -26,7 +26,7 @@ def short(name):
 def main(out):
     res = {"kernels": {}, "counters": {}}
     dur = defaultdict(list)
-    for r in rows(os.path.join(out, "trace", "**", "*kernel_trace.csv")):
+    for r in rows(os.path.join(out, "p1", "**", "*kernel_trace.csv")):
         k = short(r.get("Kernel_Name", ""))
         if k:
             dur[k].append(int(r["End_Timestamp"]) - int(r["Start_Timestamp"]))
