@@ -24,15 +24,18 @@ enum PartMode : uint32_t { kSearch = 0, kStream = 1 };
 constexpr uint32_t kStreamChunk = 256;  // push keys per streaming-partition wave
 
 // One (channel, time) aggregate as the partition kernels see it.  All
-// pointers are device pointers.  seg is push-major: seg[p*(ntiles+1) + b] =
-// first index of push p whose key is >= D[b*tile] (b < ntiles) or
-// > D[nslots-1] (b == ntiles): SArray::findRange restated per tile.
+// pointers are device pointers.  seg[p*segq + b*segb] = first index of push
+// p whose key is >= D[b*tile] (b < ntiles) or > D[nslots-1] (b == ntiles):
+// SArray::findRange restated per tile.  kStream jobs store it push-major
+// (segq = ntiles + 1, segb = 1: a chunk's boundaries are contiguous), kSearch
+// jobs tile-major (segq = 1, segb = npush: a tile's bounds of every push share
+// one cache line).
 struct JobDev {
   const uint64_t* dkeys;          // D + lo
   uint64_t nslots;                // hi - lo
   const uint64_t* const* pkeys;   // [npush]
   const uint64_t* pn;             // [npush]
-  uint32_t* seg;                  // [npush * (ntiles + 1)]
+  uint32_t* seg;                  // [npush * (ntiles + 1)], strides segq / segb
   unsigned long long* fail;       // [npush] match failures
   uint64_t* split;                // kStream: [ntiles + 1] tile splitters
   uint32_t npush;
@@ -40,13 +43,13 @@ struct JobDev {
   uint32_t split_begin;           // kStream: first splitter item of this job
   uint32_t mode;                  // PartMode
   uint32_t tile;                  // slots per tile
-  uint32_t pad;
+  uint32_t segq, segb;
 };
 
 // One workgroup tile of the aggregate kernel.
 struct TileDesc {
   const uint64_t* dk;             // D + lo + slot0
-  const uint32_t* seg;            // &job.seg[t]; push q's bounds: seg[q*stride], seg[q*stride+1]
+  const uint32_t* seg;            // &job.seg[t*segb]; push q's bounds: seg[q*stride], seg[q*stride+segb]
   const uint64_t* const* pkeys;   // job push key pointers [npush]
   const void* const* pvals;       // job push value pointers [npush * m]
   const uint64_t* pn;             // job push lengths [npush]
@@ -55,8 +58,9 @@ struct TileDesc {
   uint64_t slot0;                 // first slot of the tile in the job
   uint32_t nt;                    // slots in this tile (<= kTileSlots)
   uint32_t np;                    // pushes of the job
-  uint32_t stride;                // ntiles + 1
+  uint32_t stride;                // the job's segq
   uint32_t flags;
+  uint32_t segb;                  // the job's segb
 };
 
 // ---- kernel launchers; all enqueue on `stream` only ----
@@ -66,9 +70,13 @@ struct TileDesc {
 hipError_t launch_partition(const JobDev* d_jobs, const uint32_t* d_split_item_job,
                             uint32_t nsplit_items, const uint64_t* d_items,
                             uint32_t nitems, hipStream_t stream);
-// aggregate (psg_tile.hip): one workgroup per tile of kTileSlots slots
+// aggregate: one workgroup per tile of kTileSlots slots.  psg_tile.hip:
+// every round holds one push (long pieces); psg_tile_packed.hip: rounds may
+// hold several pushes (many short pieces)
 hipError_t launch_aggregate_tile(int dtype, int m, const TileDesc* d_tiles, uint32_t ntiles,
                                  hipStream_t stream);
+hipError_t launch_aggregate_tile_packed(int dtype, int m, const TileDesc* d_tiles,
+                                        uint32_t ntiles, hipStream_t stream);
 hipError_t launch_gather(int dtype, const uint64_t* dkeys, uint64_t nd,
                          const void* dvals, const uint64_t* req, uint64_t nreq,
                          void* out, unsigned long long* matched,

@@ -3,10 +3,11 @@
 // (reference src/base/shared_array_inl.h:164-171, and the per-separator
 // lower_bound of sliceKeyOrderedMsg, src/system/message.h:96-99).
 //
-// Output, per job, push-major: seg[p*(ntiles+1) + b] = first index of push p
-// whose key is >= D[b*tile] (b < ntiles), or > D[nslots-1] (b == ntiles).
-// The aggregate kernel (psg_tile.hip) reads push p's piece of tile t as
-// [seg[p][t], seg[p][t+1]).
+// Output, per job: seg[p*segq + b*segb] = first index of push p whose key is
+// >= D[b*tile] (b < ntiles), or > D[nslots-1] (b == ntiles); push-major for
+// kStream jobs, tile-major for kSearch jobs (psg_internal.h JobDev).  The
+// aggregate kernel (psg_tile.hip) reads push p's piece of tile t as
+// [seg(p, t), seg(p, t + 1)).
 //
 // Two ways to fill it (JobDev::mode, chosen per job by the host from the
 // mean piece length):
@@ -99,7 +100,7 @@ __device__ __forceinline__ void search_item(const JobDev& J, uint32_t p, uint32_
     res = a + 1u + below;
   }
   if (valid) {
-    J.seg[(size_t)p * (J.ntiles + 1u) + b] = (uint32_t)res;
+    J.seg[(size_t)p * J.segq + (size_t)b * J.segb] = (uint32_t)res;
     if (b == 0) J.fail[p] = 0ull;  // the aggregate launch follows in-stream
   }
 }
@@ -116,7 +117,7 @@ __device__ __forceinline__ void stream_item(const JobDev& J, uint32_t p, uint32_
   const uint64_t n = J.pn[p];
   const uint32_t nt = J.ntiles;
   const uint64_t* sp = J.split;
-  uint32_t* seg = J.seg + (size_t)p * (nt + 1u);
+  uint32_t* seg = J.seg + (size_t)p * J.segq;  // kStream: push-major, segb = 1
   const uint64_t i0 = (uint64_t)c * kStreamChunk;
   const uint32_t cl = (uint32_t)(n - i0 < kStreamChunk ? n - i0 : kStreamChunk);
   const bool last = i0 + cl == n;

@@ -71,6 +71,10 @@ struct JobSpec {
 // (DESIGN.md 4.1): a boundary search reads ~5 random lines (~600 B), the
 // stream 8 B per key.
 constexpr double kStreamBelow = 64.0;
+// Mean piece length below which the aggregate kernel packs several pushes'
+// pieces into one 64-lane round; above it rounds are
+// push-uniform, which is faster while most rounds are full anyway.
+constexpr double kPackBelow = 16.0;
 
 // PSG_PART_MODE=search|stream forces the partition mode (A/B measurements);
 // read once per job-table build, never inside a launch.
@@ -82,8 +86,16 @@ int forced_part_mode() {
   return -1;
 }
 
+// PSG_PACK=0|1 forces the round form (A/B measurements); read once per
+// job-table build, never inside a launch.
+int forced_pack() {
+  const char* e = getenv("PSG_PACK");
+  return e && (e[0] == '0' || e[0] == '1') ? e[0] - '0' : -1;
+}
+
 struct JobTable {
   int device = -1;
+  bool pack = false;  // rounds may hold several pushes
   int dtype = 0, m = 1;
   std::vector<JobDev> h;
   // per job (host): pushes kept (non-empty) and where their matched counts go
@@ -93,6 +105,7 @@ struct JobTable {
     std::vector<uint32_t> slot;        // kept push -> index in the caller's push list
     uint32_t ncaller = 0;              // caller's push count (empties included)
     uint32_t* seg = nullptr;
+    uint32_t segq = 1;                 // seg stride between pushes
     unsigned long long* fail = nullptr;
   };
   std::vector<JobInfo> info;
@@ -125,6 +138,7 @@ struct JobTable {
     struct Offs { size_t pk, pv, pn, out, fail, seg, split; };
     std::vector<Offs> offs(jobs.size());
     uint64_t tiles = 0, items = 0, sitems = 0;
+    double kv_all = 0, pieces_all = 0;
     for (size_t j = 0; j < jobs.size(); ++j) {
       const JobSpec& s = jobs[j];
       JobInfo& I = info[j];
@@ -151,7 +165,12 @@ struct JobTable {
       d.ntiles = I.ntiles;
       d.tile = tile;
       const double piece = I.np && I.ntiles ? (double)kv / ((double)I.np * I.ntiles) : 1e9;
+      kv_all += (double)kv;
+      pieces_all += (double)I.np * I.ntiles;
       d.mode = forced >= 0 ? (uint32_t)forced : (piece < kStreamBelow ? psg::kStream : psg::kSearch);
+      d.segq = d.mode == psg::kStream ? I.ntiles + 1 : 1u;
+      d.segb = d.mode == psg::kStream ? 1u : I.np;
+      I.segq = d.segq;
       tiles += I.ntiles;
       if (I.ntiles && I.np) {
         if (d.mode == psg::kSearch) {
@@ -165,6 +184,10 @@ struct JobTable {
       if (tiles >= (1ull << 31) || items >= (1ull << 31) || sitems >= (1ull << 31))
         return fail(PSG_ERR_ARG, "batch too large (%llu tiles)", (unsigned long long)tiles);
       if (j >= (1ull << 27)) return fail(PSG_ERR_ARG, "too many jobs");
+    }
+    {
+      const int fp = forced_pack();
+      pack = fp >= 0 ? fp == 1 : (pieces_all > 0 && kv_all / pieces_all < kPackBelow);
     }
     size_t off = align_up(sizeof(JobDev) * jobs.size(), 256);
     const size_t tiles_off = off;
@@ -239,7 +262,7 @@ struct JobTable {
         psg::TileDesc& T = htiles[tcur++];
         const uint64_t slot0 = (uint64_t)t * tile;
         T.dk = s.keys + slot0;
-        T.seg = d.seg + t;
+        T.seg = d.seg + (size_t)t * d.segb;
         T.pkeys = d.pkeys;
         T.pvals = (const void* const*)(base + o.pv);
         T.pn = d.pn;
@@ -248,7 +271,8 @@ struct JobTable {
         T.slot0 = slot0;
         T.nt = (uint32_t)std::min<uint64_t>(tile, s.nslots - slot0);
         T.np = np;
-        T.stride = nt + 1;
+        T.stride = d.segq;
+        T.segb = d.segb;
         T.flags = s.flags;
       }
     }
@@ -268,6 +292,8 @@ struct JobTable {
     if (h.empty()) return PSG_OK;
     if (stage == 0)
       HIP_TRY(psg::launch_partition(d_jobs, d_split_items, nsplit, d_items, nitems, s));
+    else if (pack)
+      HIP_TRY(psg::launch_aggregate_tile_packed(dtype, m, d_tiles, ntiles, s));
     else
       HIP_TRY(psg::launch_aggregate_tile(dtype, m, d_tiles, ntiles, s));
     return PSG_OK;
@@ -289,10 +315,12 @@ struct JobTable {
       if (np && nt) {
         std::vector<unsigned long long> f(np);
         std::vector<uint32_t> first(np), last(np);
-        const size_t pitch = 4 * (size_t)(nt + 1);
+        const size_t pitch = 4 * (size_t)I.segq;
+        const size_t segb = I.segq == 1 ? np : 1;  // tile-major / push-major
         HIP_TRY(hipMemcpy(f.data(), I.fail, 8 * np, hipMemcpyDeviceToHost));
         HIP_TRY(hipMemcpy2D(first.data(), 4, I.seg, pitch, 4, np, hipMemcpyDeviceToHost));
-        HIP_TRY(hipMemcpy2D(last.data(), 4, I.seg + nt, pitch, 4, np, hipMemcpyDeviceToHost));
+        HIP_TRY(hipMemcpy2D(last.data(), 4, I.seg + (size_t)nt * segb, pitch, 4, np,
+                            hipMemcpyDeviceToHost));
         for (uint32_t p = 0; p < np; ++p) {
           const uint64_t covered = last[p] >= first[p] ? (uint64_t)(last[p] - first[p]) : 0;
           mt[I.slot[p]] = covered >= f[p] ? covered - f[p] : 0;

@@ -1,32 +1,33 @@
-// psg_tile.hip -- the aggregate kernel for long pieces (push-uniform rounds):
-// one 256-thread workgroup per tile of kTS server slots, built for
-// instruction efficiency.  psg_tile_packed.hip is its form for many short
-// pieces (rounds that pack several pushes).
+// psg_tile_packed.hip -- the aggregate kernel for sparse jobs (many short
+// pieces per tile): one 256-thread workgroup per tile of kTS = 1024 server
+// slots.  Jobs whose pieces are long go to psg_tile.hip's push-uniform
+// rounds instead (the runtime picks by mean piece length, kPackBelow).
 //
 // Reference semantics: KVVector::serialSetValue / parallelSetValue
 // (src/parameter/kv_vector.h:84-204) over oldMatch / match
 // (src/system/message.h:134-267): out[j] = fold over pushes p in arrival
 // order of V_p[k] where S_p[k] == D[lo+j]; the first push assigns, later
-// pushes add, and the serial path adds +0.0 for absent pushes (one "+0.0"
-// per run of absent pushes is exact, see dev::fold_step).
+// pushes add, and the serial path adds +0.0 for every absent push (one
+// "+0.0" per run of absent pushes is exact: x + 0.0 + 0.0 == x + 0.0).
 //
-// Shape (DESIGN.md section 4.2):
-//   * the partition (psg_partition.hip) has cut every push at every tile's
-//     first server key, so push q's keys of this tile are
-//     S_q[seg(q, t), seg(q, t+1)) (strides in the TileDesc);
-//   * the pieces are split into "rounds" of 64 consecutive keys of ONE push,
-//     numbered push-major; each wave takes a contiguous run of rounds, so a
-//     round's push (pointers, bounds) is wave-uniform and every element load
-//     is a coalesced 512 B (keys) / 256 B (f32 values) wave access;
-//   * all of a wave's element loads are issued before the tile's bucket
-//     table is built, so they overlap it;
-//   * D goes to LDS; a bucket table (histogram + scan, 2 buckets per slot,
-//     the tile's key range scaled by one high multiply) turns a search into
-//     one table read and one paired key read;
+// Shape (DESIGN.md 4.2):
+//   * the partition (psg_partition.hip) has cut every push at every tile:
+//     push q's keys of this tile are S_q[seg(q, t), seg(q, t+1));
+//   * pushes are taken in groups of <= kG (one lane of wave 0 each); the
+//     group's pieces are concatenated push-major and cut into ROUNDS of 64
+//     consecutive elements, so a round may hold the tail of one piece and
+//     the heads of the next (short pieces of many sparse pushes fill a
+//     round instead of leaving it mostly idle);
+//   * each wave takes a contiguous run of rounds per pass and issues all
+//     its element loads before the tile's bucket table is built;
+//   * D goes to LDS; a bucket table (2 buckets per slot over the tile's key
+//     range, one high multiply) turns a search into one table read and one
+//     paired key read;
 //   * the fold runs wave by wave (4 barrier steps): rounds are push-major
 //     and waves hold contiguous runs of them, so every slot sees its
-//     contributions in arrival order with no atomics; sums and "last push
-//     holding the slot" live in LDS;
+//     contributions in arrival order with no atomics.  Inside one round two
+//     pushes can hit one slot: a per-wave slot bitmap detects that, and such
+//     a round folds push by push in lane (= push) order;
 //   * thread t owns slots 4t..4t+3: 16-B loads of D and 16-B stores;
 //   * consecutive tiles run on one XCD (blocks b and b+8 share one), so the
 //     cache lines two neighbouring tiles' pieces share are read once.
@@ -37,7 +38,6 @@
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
-#include "psg_device.h"
 #include "psg_internal.h"
 
 #define AS1 __attribute__((address_space(1)))
@@ -62,9 +62,11 @@ constexpr int kSPT = kTS / kNT;  // slots per thread (contiguous)
 constexpr int kNB = 2 * kTS;     // buckets
 constexpr int kBPT = kNB / kNT;  // bucket-table entries per thread in the scan
 constexpr int kCap = 6;          // rounds a wave holds per pass
-constexpr int kGroup = 32;       // pushes per group (one lane of wave 0 each)
+constexpr int kG = 64;           // pushes per group (one lane of wave 0 each)
+constexpr int kRMax = 160;       // rounds per group
 static_assert(kSPT == 4 && kBPT == 8, "layout");
 static_assert(kTS <= 0x7ffe, "u16 positions");
+static_assert(kG + 2 <= 255, "u8 lastl");
 
 typedef unsigned long long u64x2 __attribute__((ext_vector_type(2)));
 typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
@@ -79,9 +81,7 @@ __device__ __forceinline__ uint32_t xcd_tile(uint32_t b, uint32_t n) {
 }
 
 // inclusive 64-lane prefix sum by DPP (row shifts, then row broadcasts):
-// immediate lane controls, so no per-lane shuffle addresses stay live (the
-// __shfl_up form kept six address VGPRs alive across the kernel and spilled
-// them at 8 waves/SIMD)
+// immediate lane controls, so no per-lane shuffle addresses stay live
 __device__ __forceinline__ uint32_t wave_scan_incl(uint32_t x) {
   x += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x111, 0xf, 0xf, false);  // row_shr:1
   x += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x112, 0xf, 0xf, false);  // row_shr:2
@@ -92,17 +92,18 @@ __device__ __forceinline__ uint32_t wave_scan_incl(uint32_t x) {
   return x;
 }
 
-
 // workgroups per CU the LDS allows (8 for the f32, m = 1 headline case):
 // the register budget follows it through __launch_bounds__
 template <typename V, int M>
 constexpr int occupancy() {
-  constexpr int lds = 19328 + (int)(M * sizeof(V) - 4) * kTS + (M - 1) * 8 * kGroup;
+  constexpr int lds = 19504 + (int)(M * sizeof(V) - 4) * kTS + (M - 1) * 8 * kG;
   return 163840 / lds >= 8 ? 8 : 163840 / lds;
 }
 
+// rounds of 64 consecutive elements of the concatenated pieces: a round
+// can hold several pushes
 template <typename V, int M>
-__global__ __launch_bounds__(kNT, (occupancy<V, M>())) void tile_kernel(
+__global__ __launch_bounds__(kNT, (occupancy<V, M>())) void tile_packed_kernel(
     const TileDesc* __restrict__ tiles, uint32_t ntiles) {
   __shared__ __attribute__((aligned(16))) uint64_t dk[kTS + 8];
   // bucket starts (u16); the histogram counts in it as packed pairs by 32-bit atomics
@@ -112,13 +113,16 @@ __global__ __launch_bounds__(kNT, (occupancy<V, M>())) void tile_kernel(
   // last push holding the slot, relative to the group base g0: last + 2 - g0,
   // 0 when it precedes g0 - 1 (so the value fits a byte for any push count)
   __shared__ __attribute__((aligned(16))) uint8_t lastl[kTS];
-  __shared__ uint32_t rpre[kGroup + 1];             // rounds before push q of the group
-  __shared__ uint16_t rtab[kGroup * (kTS / 64)];    // round -> q << 4 | chunk
-  __shared__ uint32_t pln[kGroup];                  // piece length
-  __shared__ uint64_t pkp[kGroup], pvp[kGroup * M];  // piece starts (keys, values)
+  // pre[q] = elements of the group before push q, rq[R] = push of round R's
+  // first element (+ a sentinel)
+  __shared__ uint32_t pre[kG + 1];
+  __shared__ uint16_t rq[kRMax + 4];
+  __shared__ uint64_t pkp[kG], pvp[kG * M];  // piece starts (keys, values)
+  __shared__ uint32_t cbits[kNW][kTS / 32];  // per-wave slot bitmap: collision test
   __shared__ int lastpos[kNW];
   __shared__ int pcarry;
   __shared__ uint32_t wsum[kNW];
+  __shared__ uint32_t gsh[2];            // pushes in the group, rounds in the group
 
   const uint32_t w = uni((uint32_t)threadIdx.x >> 6);
   const int tid = threadIdx.x;
@@ -132,7 +136,7 @@ __global__ __launch_bounds__(kNT, (occupancy<V, M>())) void tile_kernel(
   const bool cont = (T.flags & kFlagCont) != 0;
   const uint64_t* Dg = T.dk;
 
-  // ---- push tables of a group (wave 0, one lane per push), round prefix
+  // ---- push tables of a group (wave 0, one lane per push), rounds
   auto load_tables = [&](uint32_t g0) {
     if (w == 0) {
       // a fresh copy of the lane id per call: otherwise the compiler hoists
@@ -140,9 +144,12 @@ __global__ __launch_bounds__(kNT, (occupancy<V, M>())) void tile_kernel(
       // 64 VGPRs, spills them to scratch in every workgroup (HBM writes)
       int lane = tid & 63;
       asm volatile("" : "+v"(lane));
-      const uint32_t gp = np - g0 < (uint32_t)kGroup ? np - g0 : (uint32_t)kGroup;
-      uint32_t nr = 0;
-      if ((uint32_t)lane < gp) {
+      const uint32_t gq = np - g0 < (uint32_t)kG ? np - g0 : (uint32_t)kG;
+      uint32_t len = 0, over = 0;
+      uint64_t kp = 0, vp[M];
+#pragma unroll
+      for (int mi = 0; mi < M; ++mi) vp[mi] = 0;
+      if ((uint32_t)lane < gq) {
         const uint32_t q = g0 + (uint32_t)lane;
         const uint32_t* sg = T.seg + (size_t)q * T.stride;
         const uint32_t n = (uint32_t)G(T.pn)[q];
@@ -150,50 +157,61 @@ __global__ __launch_bounds__(kNT, (occupancy<V, M>())) void tile_kernel(
         // bounds from a failed partition (an unsorted push) stay inside the push
         a = a < n ? a : n;
         b = b < n ? b : n;
-        // pieces out of order (the push is unsorted) or longer than the tile
-        // (duplicates): those keys cannot all match
-        const uint32_t over = b < a ? 1u : (b - a > (uint32_t)kTS ? b - a - (uint32_t)kTS : 0u);
-        if (over)
-          __hip_atomic_fetch_add(GW(T.fail) + q, (unsigned long long)over, __ATOMIC_RELAXED,
-                                 __HIP_MEMORY_SCOPE_AGENT);
-        // a piece lies inside one tile, so it holds at most kTS keys
-        const uint32_t len = b > a ? (b - a < (uint32_t)kTS ? b - a : (uint32_t)kTS) : 0u;
-        pln[lane] = len;
-        const uint64_t* kp = G(T.pkeys)[q];
-        pkp[lane] = (uint64_t)(kp + a);
+        // pieces out of order or longer than the tile (duplicates): those
+        // keys cannot all match
+        over = b < a ? 1u : (b - a > (uint32_t)kTS ? b - a - (uint32_t)kTS : 0u);
+        len = b > a ? (b - a < (uint32_t)kTS ? b - a : (uint32_t)kTS) : 0u;
+        kp = (uint64_t)(G(T.pkeys)[q] + a);
 #pragma unroll
-        for (int mi = 0; mi < M; ++mi) {
-          const V* vp = (const V*)G(T.pvals)[(size_t)q * M + mi];
-          pvp[lane * M + mi] = (uint64_t)(vp + a);
-        }
-        nr = (len + 63u) >> 6;
+        for (int mi = 0; mi < M; ++mi)
+          vp[mi] = (uint64_t)((const V*)G(T.pvals)[(size_t)q * M + mi] + a);
       }
-      const uint32_t x = wave_scan_incl(nr);
-      if (lane < kGroup) rpre[lane + 1] = x;
-      if (lane == 0) rpre[0] = 0;
+      // elements through this push
+      const uint32_t x = wave_scan_incl(len);
+      // the group: the pushes whose rounds fit kRMax (>= 1: a piece is <= 16 rounds)
+      const uint32_t gp =
+          (uint32_t)__popcll(__ballot((uint32_t)lane < gq && x <= (uint32_t)(kRMax * 64)));
+      if ((uint32_t)lane < gp) {
+        pkp[lane] = kp;
+#pragma unroll
+        for (int mi = 0; mi < M; ++mi) pvp[lane * M + mi] = vp[mi];
+        if (over)
+          __hip_atomic_fetch_add(GW(T.fail) + g0 + lane, (unsigned long long)over,
+                                 __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        pre[lane + 1] = x;
+        // the rounds whose first element lies in this piece
 #pragma nounroll
-      for (uint32_t c = 0; c < nr; ++c) rtab[x - nr + c] = (uint16_t)((uint32_t)lane << 4 | c);
+        for (uint32_t r = (x - len + 63u) >> 6; r * 64u < x; ++r) rq[r] = (uint16_t)lane;
+      }
+      if (lane == 0) {
+        pre[0] = 0;
+        gsh[0] = gp;
+      }
+      if ((uint32_t)lane + 1u == gp) {
+        gsh[1] = (x + 63u) >> 6;
+        rq[(x + 63u) >> 6] = (uint16_t)lane;  // sentinel: the last round's search bound
+      }
     }
   };
   if (np) load_tables(0);
 
   // ---- D keys, continued sums: thread t owns slots 4t..4t+3
-  const uint32_t s0 = 4u * (uint32_t)tid;
+  const uint32_t s0i = 4u * (uint32_t)tid;
   uint64_t d[4];
-  if (s0 + 3u < nt && ((uintptr_t)Dg & 15u) == 0u) {
-    const u64x2 x0 = *(const AS1 u64x2*)(Dg + s0);
-    const u64x2 x1 = *(const AS1 u64x2*)(Dg + s0 + 2);
+  if (s0i + 3u < nt && ((uintptr_t)Dg & 15u) == 0u) {
+    const u64x2 x0 = *(const AS1 u64x2*)(Dg + s0i);
+    const u64x2 x1 = *(const AS1 u64x2*)(Dg + s0i + 2);
     d[0] = x0.x; d[1] = x0.y; d[2] = x1.x; d[3] = x1.y;
   } else {
 #pragma unroll
-    for (int j = 0; j < 4; ++j) d[j] = s0 + j < nt ? G(Dg)[s0 + j] : ~0ull;
+    for (int j = 0; j < 4; ++j) d[j] = s0i + j < nt ? G(Dg)[s0i + j] : ~0ull;
   }
   V a0[M][4];
 #pragma unroll
   for (int mi = 0; mi < M; ++mi)
 #pragma unroll
     for (int j = 0; j < 4; ++j)
-      a0[mi][j] = (cont && s0 + j < nt) ? G((const V*)T.out[mi] + T.slot0)[s0 + j] : V(0);
+      a0[mi][j] = (cont && s0i + j < nt) ? G((const V*)T.out[mi] + T.slot0)[s0i + j] : V(0);
 
   // bucket of a key: the tile's key range [klo, khi] scaled onto [0, kNB) by
   // one 32x32 high multiply; keys outside the range land in an end bucket
@@ -211,31 +229,36 @@ __global__ __launch_bounds__(kNT, (occupancy<V, M>())) void tile_kernel(
     return x > r32 ? (uint32_t)(kNB - 1) : __umulhi((uint32_t)x, mul);
   };
 
-  // ---- install D, sums, lastl; clear the histogram
+  // ---- install D, sums, lastl; clear the histogram and the bitmaps
 #pragma unroll
   for (int j = 0; j < 4; ++j) {
-    dk[s0 + j] = d[j];
+    dk[s0i + j] = d[j];
 #pragma unroll
-    for (int mi = 0; mi < M; ++mi) acc[mi][s0 + j] = a0[mi][j];
-    lastl[s0 + j] = 1;  // last = -1 = g0 - 1
+    for (int mi = 0; mi < M; ++mi) acc[mi][s0i + j] = a0[mi][j];
+    lastl[s0i + j] = 1;  // last = -1 = g0 - 1
   }
   if (tid < 8) dk[kTS + tid] = ~0ull;
   {
-    uint32_t z = 0;  // zero
+    uint32_t z = 0;  // opaque zero: not a hoisted (and spilled) constant vector
+    asm volatile("" : "+v"(z));
     *(u32x4*)&bt[tid * kBPT] = u32x4{z, z, z, z};
+    if (lane < kTS / 32) cbits[w][lane] = z;
   }
   if (tid == 0) pcarry = -1;
   __syncthreads();  // (1) tables, D, cleared histogram
 
   // ---- a pass: this wave's run of rounds, loaded into registers
-  uint32_t done = 0, U = np ? uni(rpre[np < (uint32_t)kGroup ? np : kGroup]) : 0u;
-  uint32_t g0 = 0;
+  uint32_t gp = np ? uni(gsh[0]) : 0u;
+  uint32_t U = np ? uni(gsh[1]) : 0u;
+  uint32_t Et = np ? uni(pre[gp]) : 0u;  // elements of the group
+  uint32_t done = 0, g0 = 0;
   uint32_t nrw = 0, ua = 0, Rw = 0;
-  uint32_t re[kCap];  // round: q << 4 | chunk (the same in every lane)
+  // per lane and held round r, 8 bits: q | first-of-piece << 6 | exists << 7
+  // (packed 4 rounds per register: a 64-VGPR budget holds 6 rounds unspilled)
+  uint32_t rp[(kCap + 3) / 4];
   uint64_t ek[kCap];
   V ev[kCap][M];
-  uint32_t fl = 0;  // per lane: bit r = element of round r exists, bit 8+r = found,
-                    // bit 16+r = found and in order (VGPR bits, not SGPR lane masks)
+  uint32_t mmask = 0;  // wave-uniform: bit r = round r holds more than one push
   auto load_pass = [&]() {
     const uint32_t rem = U - done;
     Rw = (rem + kNW - 1) / kNW;
@@ -243,36 +266,43 @@ __global__ __launch_bounds__(kNT, (occupancy<V, M>())) void tile_kernel(
     ua = done + w * Rw;
     const uint32_t ub = ua + Rw < U ? ua + Rw : U;
     nrw = ub > ua ? ub - ua : 0u;
-    fl = 0;
+    mmask = 0;
+#pragma unroll
+    for (int r = 0; r < (kCap + 3) / 4; ++r) rp[r] = 0;
 #pragma unroll
     for (int r = 0; r < kCap; ++r) {
-      re[r] = 0;
       if ((uint32_t)r < nrw) {
-        const uint32_t e = rtab[ua + (uint32_t)r];
-        const uint32_t q = e >> 4;
-        const uint32_t i = (e & 15u) * 64u + (uint32_t)lane;
-        re[r] = e;
-        const bool have = i < pln[q];
-        fl |= (uint32_t)have << r;  // shift of a 0/1: no literal masks held in VGPRs
-        const uint32_t x = have ? i : 0u;
-        ek[r] = G((const uint64_t*)pkp[q])[x];
+        const uint32_t R = ua + (uint32_t)r;
+        const uint32_t e = R * 64u + (uint32_t)lane;
+        // push of element e: the largest q in [rq[R], rq[R+1]] with pre[q] <= e
+        const uint32_t qlo = uni(rq[R]);
+        const uint32_t qhi = uni(rq[R + 1]);
+        uint32_t q = qlo;
+        const uint32_t span = qhi - qlo;  // wave-uniform trip count
+        for (uint32_t st = span ? 1u << (31 - __builtin_clz(span)) : 0u; st; st >>= 1)
+          if (q + st <= qhi && pre[q + st] <= e) q += st;
+        const bool have = e < Et;
+        if (!have) q = qlo;  // a piece that exists: its first element is a safe address
+        const uint32_t i = have ? e - pre[q] : 0u;
+        mmask |= (__ballot(have && q != qlo) != 0 ? 1u : 0u) << r;
+        rp[r >> 2] |= (q | (uint32_t)(have && i == 0u) << 6 | (uint32_t)have << 7) << (8 * (r & 3));
+        ek[r] = G((const uint64_t*)pkp[q])[i];
 #pragma unroll
-        for (int mi = 0; mi < M; ++mi) ev[r][mi] = G((const V*)pvp[q * M + mi])[x];
+        for (int mi = 0; mi < M; ++mi) ev[r][mi] = G((const V*)pvp[q * M + mi])[i];
       }
     }
   };
   if (U) load_pass();
 
-
   // ---- bucket table: histogram, exclusive scan -> bt[b] = first slot of bucket b
   // D keys back from LDS: the registers that held them are free during the
-  // pass's element loads (8 waves/SIMD leave 64 VGPRs)
-  const u64x2 y0 = *(const u64x2*)&dk[s0];
-  const u64x2 y1 = *(const u64x2*)&dk[s0 + 2];
+  // pass's element loads
+  const u64x2 y0 = *(const u64x2*)&dk[s0i];
+  const u64x2 y1 = *(const u64x2*)&dk[s0i + 2];
   const uint64_t dd[4] = {y0.x, y0.y, y1.x, y1.y};
 #pragma unroll
   for (int j = 0; j < 4; ++j)
-    if (s0 + j < nt)
+    if (s0i + j < nt)
     {  // counts <= kTS < 2^16: no carry between the packed halves
       const uint32_t b = bucket(dd[j]);
       __hip_atomic_fetch_add(&bt32[b >> 1], 1u << (16 * (b & 1u)), __ATOMIC_RELAXED,
@@ -305,21 +335,24 @@ __global__ __launch_bounds__(kNT, (occupancy<V, M>())) void tile_kernel(
 
   for (;;) {
     if (!U) {  // this group of pushes has no keys in the tile, or is done
-      g0 += kGroup;
+      g0 += gp;
       if (g0 >= np) break;
       // rebase lastl on the new group: last == g0 - 1 -> 1, older -> 0
 #pragma unroll
-      for (int j = 0; j < 4; ++j) lastl[s0 + j] = lastl[s0 + j] == kGroup + 1 ? 1 : 0;
+      for (int j = 0; j < 4; ++j) lastl[s0i + j] = lastl[s0i + j] == gp + 1u ? 1 : 0;
       load_tables(g0);
       __syncthreads();
-      U = uni(rpre[np - g0 < (uint32_t)kGroup ? np - g0 : kGroup]);
+      gp = uni(gsh[0]);
+      U = uni(gsh[1]);
+      Et = uni(pre[gp]);
       done = 0;
       if (U) load_pass();
       continue;
     }
+    auto re = [&](int r) -> uint32_t { return (rp[r >> 2] >> (8 * (r & 3))) & 0xffu; };
     // ---- search every held round
     uint32_t pos[kCap];
-    fl &= 0xffu;
+    uint32_t okm = 0;  // per lane: bit r = found; bit 8 + r = found and in order
 #pragma unroll
     for (int r = 0; r < kCap; ++r) {
       pos[r] = 0;
@@ -339,7 +372,7 @@ __global__ __launch_bounds__(kNT, (occupancy<V, M>())) void tile_kernel(
         }
         const uint64_t k0 = dk[l], k1 = dk[l + 1];
         pos[r] = l + ((n > 0u && k0 < k) ? 1u : 0u) + ((n > 1u && k1 < k) ? 1u : 0u);
-        fl |= (uint32_t)((n > 0u && k0 == k) || (n > 1u && k1 == k)) << (8 + r);
+        okm |= (uint32_t)((n > 0u && k0 == k) || (n > 1u && k1 == k)) << r;
       }
     }
     int mylast = 0;  // position held by lane 63 in this wave's last round
@@ -349,29 +382,48 @@ __global__ __launch_bounds__(kNT, (occupancy<V, M>())) void tile_kernel(
     if (nrw && lane == 63) lastpos[w] = mylast;
     __syncthreads();  // (5) lastpos of every wave
 
-    // ---- order check
+    // ---- order check: strictly increasing positions inside a piece
 #pragma unroll
     for (int r = 0; r < kCap; ++r) {
       if ((uint32_t)r < nrw) {
-        int prev0;
-        if ((re[r] & 15u) == 0u) prev0 = -1;  // first round of the piece
-        else if (r > 0) prev0 = __builtin_amdgcn_readlane((int)pos[r - 1], 63);
+        int prev0;  // position of the element before lane 0's
+        if (r > 0) prev0 = __builtin_amdgcn_readlane((int)pos[r - 1], 63);
         else prev0 = w > 0 ? lastpos[w - 1] : pcarry;
-        const int prev = __builtin_amdgcn_update_dpp(prev0, (int)pos[r], 0x138, 0xf, 0xf, false);
-        const bool ok = ((fl >> r) & 1u) && ((fl >> (8 + r)) & 1u) && (int)pos[r] > prev;
-        fl |= (uint32_t)ok << (16 + r);
+        int prev = __builtin_amdgcn_update_dpp(prev0, (int)pos[r], 0x138, 0xf, 0xf, false);
+        if ((re(r) >> 6) & 1u) prev = -1;  // first element of its piece
+        const bool ok = ((re(r) >> 7) & 1u) && ((okm >> r) & 1u) && (int)pos[r] > prev;
+        okm |= (uint32_t)ok << (8 + r);
       }
     }
-    // elements that exist but did not match: one ballot per pass, counts per
-    // round only when there are any
-    if (__ballot((fl & ~(fl >> 16) & 0xffu) != 0u)) {
+    // elements that exist but did not match: one ballot per pass; counted per
+    // push only when there are any
+    {
+      uint32_t exist = 0;
+#pragma unroll
+      for (int r = 0; r < kCap; ++r) exist |= ((re(r) >> 7) & 1u) << r;
+      const uint32_t badm = exist & ~(okm >> 8);
+      if (__ballot(badm != 0u)) {
+#pragma unroll
+        for (int r = 0; r < kCap; ++r)
+          if ((badm >> r) & 1u)
+            __hip_atomic_fetch_add(GW(T.fail) + g0 + (re(r) & 63u), 1ull, __ATOMIC_RELAXED,
+                                   __HIP_MEMORY_SCOPE_AGENT);
+      }
+    }
+    // ---- rounds holding several pushes: do two of them hit one slot?
+    uint32_t cmask = 0;  // wave-uniform: bit r = round r needs the push-ordered fold
+    if (mmask) {
 #pragma unroll
       for (int r = 0; r < kCap; ++r) {
-        const uint64_t bad = __ballot(((fl >> r) & ~(fl >> (16 + r)) & 1u) != 0u);
-        if ((uint32_t)r < nrw && bad && lane == 0)
-          __hip_atomic_fetch_add(GW(T.fail) + g0 + (re[r] >> 4),
-                                 (unsigned long long)__popcll(bad), __ATOMIC_RELAXED,
-                                 __HIP_MEMORY_SCOPE_AGENT);
+        if ((mmask >> r) & 1u) {
+          const bool ok = (okm >> (8 + r)) & 1u;
+          const uint32_t s = pos[r], bit = 1u << (s & 31u);
+          uint32_t old = 0;
+          if (ok) old = __hip_atomic_fetch_or(&cbits[w][s >> 5], bit, __ATOMIC_RELAXED,
+                                              __HIP_MEMORY_SCOPE_WAVEFRONT);
+          cmask |= (__ballot(ok && (old & bit)) != 0 ? 1u : 0u) << r;
+          if (ok) cbits[w][s >> 5] = 0u;
+        }
       }
     }
 
@@ -382,19 +434,37 @@ __global__ __launch_bounds__(kNT, (occupancy<V, M>())) void tile_kernel(
       if (st == w) {
 #pragma unroll
         for (int r = 0; r < kCap; ++r) {
-          if ((uint32_t)r < nrw && ((fl >> (16 + r)) & 1u)) {
-            const uint32_t q = re[r] >> 4;
+          if ((uint32_t)r < nrw) {
+            bool pend = (okm >> (8 + r)) & 1u;
+            const uint32_t q = re(r) & 63u;
             const uint32_t s = pos[r];
-            const uint32_t l1 = lastl[s];
             const bool first = g0 + q == 0u && !cont;
-            const bool gap = !parallel && l1 <= q;  // last < g0 + q - 1
+            auto apply = [&]() {
+              const uint32_t l1 = lastl[s];
+              const bool gap = !parallel && l1 <= q;  // last < g0 + q - 1
 #pragma unroll
-            for (int mi = 0; mi < M; ++mi) {
-              const V a = acc[mi][s];
-              const V ag = gap ? a + V(0) : a;
-              acc[mi][s] = first ? ev[r][mi] : ag + ev[r][mi];
+              for (int mi = 0; mi < M; ++mi) {
+                const V a = acc[mi][s];
+                const V ag = gap ? a + V(0) : a;
+                acc[mi][s] = first ? ev[r][mi] : ag + ev[r][mi];
+              }
+              lastl[s] = (uint8_t)(q + 2u);
+            };
+            if (!((cmask >> r) & 1u)) {
+              if (pend) apply();  // no two lanes of the round on one slot
+            } else {
+              // push-ordered: the lowest pending push applies first
+              for (;;) {
+                const unsigned long long pm = __ballot(pend);
+                if (!pm) break;
+                const uint32_t qmin =
+                    (uint32_t)__builtin_amdgcn_readlane((int)q, (int)__builtin_ctzll(pm));
+                if (pend && q == qmin) {
+                  apply();
+                  pend = false;
+                }
+              }
             }
-            lastl[s] = (uint8_t)(q + 2u);
           }
         }
         if (w == wl && lane == 63) pcarry = mylast;
@@ -413,11 +483,17 @@ __global__ __launch_bounds__(kNT, (occupancy<V, M>())) void tile_kernel(
   }
 
   // ---- trailing "+0.0" of absent last pushes (serial), stores
+  const uint32_t gl = g0 - gp;  // base of the last group (0 without pushes)
+  // the slot offset afresh (an opaque thread id): kept live across the main
+  // loop it is the one value the 64-VGPR budget spills to scratch
+  uint32_t s0 = (uint32_t)threadIdx.x;
+  asm volatile("" : "+v"(s0));
+  s0 *= 4u;
   V res[M][4];
 #pragma unroll
   for (int j = 0; j < 4; ++j) {
-    // the last group's base is g0 - kGroup: gap iff last < np - 1
-    const bool gap = !parallel && (uint32_t)lastl[s0 + j] < np - (g0 - kGroup) + 1u;
+    // gap iff last < np - 1
+    const bool gap = !parallel && (uint32_t)lastl[s0 + j] < np - gl + 1u;
 #pragma unroll
     for (int mi = 0; mi < M; ++mi) {
       const V a = acc[mi][s0 + j];
@@ -449,7 +525,7 @@ __global__ __launch_bounds__(kNT, (occupancy<V, M>())) void tile_kernel(
 
 template <typename V, int M>
 hipError_t go(const TileDesc* t, uint32_t n, hipStream_t s) {
-  hipLaunchKernelGGL((tile_kernel<V, M>), dim3(n), dim3(kNT), 0, s, t, n);
+  hipLaunchKernelGGL((tile_packed_kernel<V, M>), dim3(n), dim3(kNT), 0, s, t, n);
   return hipGetLastError();
 }
 
@@ -466,8 +542,8 @@ hipError_t launch_m(int m, const TileDesc* t, uint32_t n, hipStream_t s) {
 
 }  // namespace
 
-hipError_t launch_aggregate_tile(int dtype, int m, const TileDesc* d_tiles, uint32_t ntiles,
-                                 hipStream_t stream) {
+hipError_t launch_aggregate_tile_packed(int dtype, int m, const TileDesc* d_tiles,
+                                        uint32_t ntiles, hipStream_t stream) {
   if (ntiles == 0) return hipSuccess;
   return dtype == 0 ? launch_m<float>(m, d_tiles, ntiles, stream)
                     : launch_m<double>(m, d_tiles, ntiles, stream);
