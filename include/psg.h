@@ -165,6 +165,20 @@ int psg_shard_bounds(size_t n, uint64_t* bounds);
 int psg_slice_dev(const uint64_t* keys, uint64_t n, uint64_t kb, uint64_t ke,
                   const uint64_t* sep, int nsep, uint64_t* pos, void* stream);
 
+/* ------------------------------------------------------------------ */
+/* Wire ingress: key signatures of the key cache                       */
+/* ------------------------------------------------------------------ */
+/* CRC-32C of device-resident byte segments: out[i] = crc32c::Extend(
+ * init ? init[i] : 0, data + off[i], min(off[i+1] - off[i], max_len))
+ * (src/util/crc32c.cc:283-330; crc32c::Value = init 0).  The key signature
+ * of RNode::cacheKeySender/cacheKeyRecver (src/system/remote_node.cc:108,
+ * 163) is max_len = PSG_MAX_SIG_LEN over the key bytes.  off[nseg+1], init
+ * (nullable) and out[nseg] are device arrays; enqueued on `stream`. */
+#define PSG_MAX_SIG_LEN 2048 /* RNode::max_sig_len_, remote_node.h:96 */
+int psg_crc32c_dev(const void* data, const uint64_t* off, uint64_t nseg,
+                   uint64_t max_len, const uint32_t* init, uint32_t* out,
+                   void* stream);
+
 #ifdef __cplusplus
 }
 #endif

@@ -379,3 +379,27 @@ void orc_shuffle_keys(const uint64_t* ids, size_t n, uint32_t seed,
     out[i] = o[0] ^ o[1];
   }
 }
+
+/* ---------------------------------------------------------------------- */
+/* crc32c::Extend (util/crc32c.cc:283-330), restated bit by bit: reflected */
+/* Castagnoli polynomial 0x82f63b78, register inverted on entry and exit.  */
+/* The reference's slicing-by-4 table walk computes the same function.     */
+/* ---------------------------------------------------------------------- */
+uint32_t orc_crc32c_extend(uint32_t init, const void* data, size_t n) {
+  const uint8_t* p = (const uint8_t*)data;
+  uint32_t l = init ^ 0xffffffffu;
+  for (size_t i = 0; i < n; ++i) {
+    l ^= p[i];
+    for (int b = 0; b < 8; ++b) l = (l & 1u) ? (l >> 1) ^ 0x82f63b78u : l >> 1;
+  }
+  return l ^ 0xffffffffu;
+}
+
+/* crc32c::Mask / Unmask (util/crc32c.h:29-38) */
+uint32_t orc_crc32c_mask(uint32_t crc) {
+  return ((crc >> 15) | (crc << 17)) + 0xa282ead8u;
+}
+uint32_t orc_crc32c_unmask(uint32_t masked) {
+  const uint32_t rot = masked - 0xa282ead8u;
+  return (rot >> 17) | (rot << 15);
+}

@@ -109,6 +109,13 @@ void orc_murmur3_x64_128(const void* key, int len, uint32_t seed,
 void orc_shuffle_keys(const uint64_t* ids, size_t n, uint32_t seed,
                       uint64_t* out);
 
+/* crc32c::Extend / Mask / Unmask (util/crc32c.cc:283-330, crc32c.h:29-38);
+ * Value(data, n) = Extend(0, data, n).  The key-cache signature is
+ * Value(keys, min(bytes, 2048)) (system/remote_node.cc:108,163). */
+uint32_t orc_crc32c_extend(uint32_t init, const void* data, size_t n);
+uint32_t orc_crc32c_mask(uint32_t crc);
+uint32_t orc_crc32c_unmask(uint32_t masked);
+
 #ifdef __cplusplus
 }
 #endif

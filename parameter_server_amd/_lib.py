@@ -91,6 +91,7 @@ SIGNATURES = {
     "psg_key_union_dev": (C.c_int, [_p, _u64, _p, _u64, _p, _pu64, _p]),
     "psg_shard_bounds": (C.c_int, [_sz, _pu64]),
     "psg_slice_dev": (C.c_int, [_p, _u64, _u64, _u64, _p, C.c_int, _p, _p]),
+    "psg_crc32c_dev": (C.c_int, [_p, _p, _u64, _u64, _p, _p, _p]),
 }
 
 _LIB = None

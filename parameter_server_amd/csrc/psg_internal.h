@@ -93,4 +93,11 @@ hipError_t launch_slice(const uint64_t* keys, uint64_t n, uint64_t kb,
                         uint64_t ke, const uint64_t* sep, int nsep,
                         uint64_t* pos, hipStream_t stream);
 
+// CRC-32C (psg_crc32c.hip): out[i] = crc32c::Extend(init ? init[i] : 0,
+// data + off[i], min(off[i+1] - off[i], max_len)); all pointers device
+uint64_t crc32c_chunks_per_segment(uint64_t max_len);
+hipError_t launch_crc32c(const uint8_t* data, const uint64_t* off, uint64_t nseg,
+                         uint64_t max_len, const uint32_t* init, uint32_t* out,
+                         hipStream_t stream);
+
 }  // namespace psg

@@ -638,6 +638,15 @@ int psg_slice_dev(const uint64_t* keys, uint64_t n, uint64_t kb, uint64_t ke,
   return PSG_OK;
 }
 
+int psg_crc32c_dev(const void* data, const uint64_t* off, uint64_t nseg, uint64_t max_len,
+                   const uint32_t* init, uint32_t* out, void* stream) {
+  if (nseg == 0) return PSG_OK;
+  if (!data || !off || !out) return fail(PSG_ERR_ARG, "null argument");
+  HIP_TRY(psg::launch_crc32c((const uint8_t*)data, off, nseg, max_len, init, out,
+                             (hipStream_t)stream));
+  return PSG_OK;
+}
+
 // --------------------------------------------------------------- context --
 int psg_create(int device, int dtype, unsigned flags, psg_ctx** out) {
   if (!out) return fail(PSG_ERR_ARG, "null out");

@@ -15,6 +15,7 @@ import numpy as np
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 ORC_PATH = os.path.join(ROOT, "oracle", "liborc.so")
 REF_MURMUR_PATH = os.path.join(ROOT, "oracle", "_ref", "libref_murmur3.so")
+REF_CRC_PATH = os.path.join(ROOT, "oracle", "_ref", "libref_crc32c.so")
 
 _p = C.c_void_p
 _sz = C.c_size_t
@@ -48,6 +49,9 @@ def orc() -> C.CDLL:
                                             _psz, _psz, _psz]),
             "orc_murmur3_x64_128": (None, [_p, C.c_int, C.c_uint32, _p]),
             "orc_shuffle_keys": (None, [_p, _sz, C.c_uint32, _p]),
+            "orc_crc32c_extend": (C.c_uint32, [C.c_uint32, _p, _sz]),
+            "orc_crc32c_mask": (C.c_uint32, [C.c_uint32]),
+            "orc_crc32c_unmask": (C.c_uint32, [C.c_uint32]),
         }
         for name, (res, args) in sig.items():
             f = getattr(L, name)
@@ -159,3 +163,37 @@ def ref_shuffle_keys(ids, seed=512927377):
         f(_a(x), 8, seed, _a(o))
         out[i] = o[0] ^ o[1]
     return out
+
+
+# ---- crc32c (util/crc32c.cc:283-330): the key-cache signature ------------
+def crc32c(data, init: int = 0) -> int:
+    """crc32c::Extend(init, data, len(data)); Value = init 0."""
+    b = bytes(memoryview(np.ascontiguousarray(data)).cast("B")) if not isinstance(data, bytes) else data
+    return int(orc().orc_crc32c_extend(init, b, len(b)))
+
+
+def crc32c_mask(c: int) -> int:
+    return int(orc().orc_crc32c_mask(c))
+
+
+def crc32c_unmask(c: int) -> int:
+    return int(orc().orc_crc32c_unmask(c))
+
+
+def key_signature(keys, max_sig_len: int = 2048) -> int:
+    """RNode::cacheKeySender/Recver signature (remote_node.cc:108,163):
+    Value(key bytes, min(key bytes, max_sig_len_))."""
+    b = u64(keys).tobytes()
+    return crc32c(b[:max_sig_len])
+
+
+def ref_crc_available() -> bool:
+    return os.path.exists(REF_CRC_PATH)
+
+
+def ref_crc32c(data: bytes, init: int = 0) -> int:
+    """The reference's own crc32c::Extend (src/util/crc32c.cc compiled in place)."""
+    L = C.CDLL(REF_CRC_PATH)
+    L.ref_crc32c_extend.restype = C.c_uint
+    L.ref_crc32c_extend.argtypes = [C.c_uint, C.c_char_p, _sz]
+    return int(L.ref_crc32c_extend(init, data, len(data)))
