@@ -48,7 +48,9 @@ typedef enum psg_status {
   PSG_ERR_UNSORTED = -7,   /* key-only push not strictly increasing */
   PSG_ERR_SIZE = -8,       /* CHECK_EQ(recv_data.size(), recv_key.size()) :108,187 */
   PSG_ERR_CHANNEL = -9,    /* pushes of one time t name different channels */
-  PSG_ERR_EMPTY_KEYS = -10 /* value push to a channel with no server keys */
+  PSG_ERR_EMPTY_KEYS = -10, /* value push to a channel with no server keys */
+  PSG_ERR_SIGNATURE = -11   /* key signature / key cache mismatch
+                               CHECK_EQ remote_node.cc:163,174 */
 } psg_status;
 
 typedef enum psg_dtype { PSG_F32 = 0, PSG_F64 = 1 } psg_dtype;
@@ -60,6 +62,13 @@ typedef enum psg_dtype { PSG_F32 = 0, PSG_F64 = 1 } psg_dtype;
  * reproduced bit-exactly. */
 #define PSG_SERIAL_MATCH 0u
 #define PSG_PARALLEL_MATCH 1u
+/* Context option (psg_create / psg_set_match_flags flags): the caller keeps
+ * the key and value buffers of psg_push / psg_push_cached valid and
+ * unmodified until psg_received of that time returns -- as the reference's
+ * MessagePtr keeps a message's SArrays alive -- so pinned buffers are DMA'd
+ * without a wait per push.  Without it every push returns with the caller's
+ * buffers free. */
+#define PSG_HOLD_BUFFERS 0x100u
 
 int psg_abi_version(void);
 const char* psg_status_string(int status);
@@ -93,11 +102,43 @@ int psg_value_copy(psg_ctx* ctx, int chl, size_t off, size_t n, void* out);
 
 /* Value push: setValue(msg) for msg->value of m arrays, each n entries,
  * msg->task.key_range() = [kb, ke), msg->task.time() = time,
- * msg->task.key_channel() = chl.  vals[i] points to array i.  Host data is
- * staged before return; the merge runs asynchronously on the context's
- * stream and its match check is reported by psg_received for `time`. */
+ * msg->task.key_channel() = chl.  vals[i] points to array i.  The caller's
+ * buffers are free on return: pinned host memory (hipHostMalloc /
+ * hipHostRegister) is DMA'd directly, pageable memory is copied into a
+ * pinned staging ring whose DMA continues after return.  The merge runs
+ * asynchronously on the context's stream and its match check is reported
+ * by psg_received for `time`. */
 int psg_push(psg_ctx* ctx, int chl, int time, uint64_t kb, uint64_t ke,
              const uint64_t* keys, size_t n, int m, const void* const* vals);
+
+/* Value or key push through the receiver's key cache: RNode::cacheKeyRecver
+ * (src/system/remote_node.cc:139-184) followed by setValue.  The server
+ * keeps one cache per remote node (RNode::key_cache_, remote_node.h:92-93):
+ * `sender` names it (any caller-chosen id, e.g. the worker's rank).  `kc` carries
+ * the task's key-cache fields:
+ *   PSG_KC_SIG   task.has_key_signature(), signature `sig`;
+ *   PSG_KC_KEYS  task.has_key(): the message carries keys[nkeys];
+ *   PSG_KC_ERASE task.erase_key_cache().
+ * Each cache is indexed by (chl, [kb, ke)).  No signature: the entry is
+ * dropped and the message's keys are used.  Signature + keys: the keys'
+ * crc32c over their first PSG_MAX_SIG_LEN bytes (computed on the GPU) must
+ * equal `sig` (else PSG_ERR_SIGNATURE), and the resident copy is cached.
+ * Signature without keys: the cached keys are used in place (no key bytes
+ * cross PCIe); a missing entry or another signature is PSG_ERR_SIGNATURE
+ * (sig 0 against a missing entry restores no keys: the message is
+ * ignored, as the reference's empty key list is).  m == 0 (or nvals == 0)
+ * is a key-only message (setUnion); otherwise nvals must equal the key
+ * count (PSG_ERR_SIZE). */
+#define PSG_KC_SIG 1u
+#define PSG_KC_KEYS 2u
+#define PSG_KC_ERASE 4u
+int psg_push_cached(psg_ctx* ctx, int sender, int chl, int time, uint64_t kb,
+                    uint64_t ke, unsigned kc, uint32_t sig, const uint64_t* keys, size_t nkeys,
+                    int m, const void* const* vals, size_t nvals);
+/* RNode::clearCache (remote_node.h:54) / memSize (remote_node.cc:186-195)
+ * of one sender's cache (sender < 0: every sender). */
+int psg_key_cache_clear(psg_ctx* ctx, int sender);
+int psg_key_cache_bytes(psg_ctx* ctx, int sender, size_t* bytes);
 /* Shape of the aggregate of `time`: m arrays over server positions
  * [lo, hi) of key(chl).  PSG_ERR_NO_TIME if nothing was pushed. */
 int psg_received_shape(psg_ctx* ctx, int time, int* m, size_t* lo,
@@ -108,7 +149,8 @@ int psg_received_shape(psg_ctx* ctx, int time, int* m, size_t* lo,
 int psg_received(psg_ctx* ctx, int time, int m, void* const* out);
 
 /* Pull reply: getValue(msg) (kv_vector.h:206-227): out[i] = value(chl) at
- * keys[i], 0 where keys[i] is not a server key.  keys sorted. */
+ * keys[i], 0 where keys[i] is not a server key.  keys sorted (repeats
+ * allowed); PSG_ERR_UNSORTED otherwise. */
 int psg_gather(psg_ctx* ctx, int chl, const uint64_t* keys, size_t n,
                void* out, size_t* matched);
 

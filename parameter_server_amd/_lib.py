@@ -30,11 +30,17 @@ PSG_ERR_UNSORTED = -7
 PSG_ERR_SIZE = -8
 PSG_ERR_CHANNEL = -9
 PSG_ERR_EMPTY_KEYS = -10
+PSG_ERR_SIGNATURE = -11
+PSG_KC_SIG = 1
+PSG_KC_KEYS = 2
+PSG_KC_ERASE = 4
+PSG_MAX_SIG_LEN = 2048
 
 PSG_F32 = 0
 PSG_F64 = 1
 PSG_SERIAL_MATCH = 0
 PSG_PARALLEL_MATCH = 1
+PSG_HOLD_BUFFERS = 0x100
 MAX_VALUE_ARRAYS = 4
 
 # Every symbol include/psg.h declares, with its ctypes signature.
@@ -76,6 +82,10 @@ SIGNATURES = {
     "psg_value_copy": (C.c_int, [_p, C.c_int, _sz, _sz, _p]),
     "psg_push": (C.c_int, [_p, C.c_int, C.c_int, _u64, _u64, _p, _sz, C.c_int,
                            C.POINTER(_p)]),
+    "psg_push_cached": (C.c_int, [_p, C.c_int, C.c_int, C.c_int, _u64, _u64, C.c_uint,
+                                  C.c_uint32, _p, _sz, C.c_int, _p, _sz]),
+    "psg_key_cache_clear": (C.c_int, [_p, C.c_int]),
+    "psg_key_cache_bytes": (C.c_int, [_p, C.c_int, _psz]),
     "psg_received_shape": (C.c_int, [_p, C.c_int, C.POINTER(C.c_int), _psz, _psz]),
     "psg_received": (C.c_int, [_p, C.c_int, C.c_int, C.POINTER(_p)]),
     "psg_gather": (C.c_int, [_p, C.c_int, _p, _sz, _p, _psz]),

@@ -83,7 +83,8 @@ hipError_t launch_gather(int dtype, const uint64_t* dkeys, uint64_t nd,
                          hipStream_t stream);
 // keys strictly increasing?  *bad (device) += number of violations.
 hipError_t launch_check_sorted(const uint64_t* keys, uint64_t n,
-                               unsigned long long* bad, hipStream_t stream);
+                               unsigned long long* bad, hipStream_t stream,
+                               bool strict = true);
 // out = a U b (strictly increasing inputs).  scratch: >= union_scratch_bytes(nb).
 size_t union_scratch_bytes(uint64_t nb);
 hipError_t launch_union(const uint64_t* a, uint64_t na, const uint64_t* b,
@@ -92,6 +93,11 @@ hipError_t launch_union(const uint64_t* a, uint64_t na, const uint64_t* b,
 hipError_t launch_slice(const uint64_t* keys, uint64_t n, uint64_t kb,
                         uint64_t ke, const uint64_t* sep, int nsep,
                         uint64_t* pos, hipStream_t stream);
+
+// sum over job `job`'s pushes of (keys - matched keys) into *bad (after the
+// aggregate of that job's table ran on the same stream)
+hipError_t launch_unmatched(const JobDev* jobs, uint32_t job, uint32_t npush,
+                            unsigned long long* bad, hipStream_t stream);
 
 // CRC-32C (psg_crc32c.hip): out[i] = crc32c::Extend(init ? init[i] : 0,
 // data + off[i], min(off[i+1] - off[i], max_len)); all pointers device

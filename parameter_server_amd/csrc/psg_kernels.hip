@@ -49,9 +49,9 @@ __global__ __launch_bounds__(256) void gather_kernel(
 }
 
 __global__ __launch_bounds__(256) void check_sorted_kernel(
-    const uint64_t* __restrict__ k, uint64_t n, unsigned long long* bad) {
+    const uint64_t* __restrict__ k, uint64_t n, unsigned long long* bad, bool strict) {
   const uint64_t i = (uint64_t)blockIdx.x * 256u + threadIdx.x;
-  const bool b = (i > 0 && i < n) && !(k[i - 1] < k[i]);
+  const bool b = (i > 0 && i < n) && (strict ? !(k[i - 1] < k[i]) : k[i] < k[i - 1]);
   const unsigned long long m = __ballot(b);
   if ((threadIdx.x & 63) == 0 && m) atomicAdd(bad, (unsigned long long)__popcll(m));
 }
@@ -187,6 +187,34 @@ __global__ __launch_bounds__(256) void slice_kernel(
   if (lane == 0) pos[s] = r;
 }
 
+// keys of a job's pushes that were not matched, summed into *bad: push p
+// covered seg(p, last) - seg(p, 0) positions of which fail[p] failed
+// (the count the reference CHECKs per push, kv_vector.h:134,192)
+__global__ __launch_bounds__(256) void unmatched_kernel(const JobDev* __restrict__ jobs,
+                                                        uint32_t j,
+                                                        unsigned long long* __restrict__ bad) {
+  const JobDev& J = jobs[j];
+  const uint32_t p = blockIdx.x * 256u + threadIdx.x;
+  uint64_t miss = 0;
+  if (p < J.npush) {
+    const uint64_t n = J.pn[p];
+    uint64_t matched = 0;
+    if (J.ntiles) {
+      const uint32_t a = J.seg[(size_t)p * J.segq];
+      const uint32_t b = J.seg[(size_t)p * J.segq + (size_t)J.ntiles * J.segb];
+      const uint64_t covered = b >= a ? b - a : 0;
+      const uint64_t f = J.fail[p];
+      matched = covered >= f ? covered - f : 0;
+    }
+    miss = n - (matched < n ? matched : n);
+  }
+  // one atomic per wave
+  for (int d = 32; d >= 1; d >>= 1) miss += (uint64_t)__shfl_xor((long long)miss, d, 64);
+  if ((threadIdx.x & 63) == 0 && miss)
+    __hip_atomic_fetch_add(bad, (unsigned long long)miss, __ATOMIC_RELAXED,
+                           __HIP_MEMORY_SCOPE_AGENT);
+}
+
 }  // namespace
 // ----------------------------------------------------------------------
 // launchers
@@ -209,10 +237,10 @@ hipError_t launch_gather(int dtype, const uint64_t* dkeys, uint64_t nd,
 }
 
 hipError_t launch_check_sorted(const uint64_t* keys, uint64_t n,
-                               unsigned long long* bad, hipStream_t stream) {
+                               unsigned long long* bad, hipStream_t stream, bool strict) {
   if (n < 2) return hipSuccess;
   hipLaunchKernelGGL(check_sorted_kernel, dim3((uint32_t)((n + 255) / 256)),
-                     dim3(256), 0, stream, keys, n, bad);
+                     dim3(256), 0, stream, keys, n, bad, strict);
   return hipGetLastError();
 }
 
@@ -251,6 +279,14 @@ hipError_t launch_slice(const uint64_t* keys, uint64_t n, uint64_t kb,
   if (nsep <= 0) return hipSuccess;
   hipLaunchKernelGGL(slice_kernel, dim3((uint32_t)((nsep + 3) / 4)), dim3(256), 0,
                      stream, keys, n, kb, ke, sep, nsep, pos);
+  return hipGetLastError();
+}
+
+hipError_t launch_unmatched(const JobDev* jobs, uint32_t job, uint32_t npush,
+                            unsigned long long* bad, hipStream_t stream) {
+  if (npush == 0) return hipSuccess;
+  hipLaunchKernelGGL(unmatched_kernel, dim3((npush + 255) / 256), dim3(256), 0, stream, jobs, job,
+                     bad);
   return hipGetLastError();
 }
 

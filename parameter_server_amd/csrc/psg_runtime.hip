@@ -10,11 +10,14 @@
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <iterator>
 #include <cstdarg>
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
+#include <deque>
 #include <map>
+#include <memory>
 #include <mutex>
 #include <string>
 #include <unordered_map>
@@ -116,18 +119,37 @@ struct JobTable {
   psg::TileDesc* d_tiles = nullptr;
   uint32_t* d_split_items = nullptr;
   uint64_t* d_items = nullptr;
-  std::vector<char> host_img;
+  // pinned host images of the blob, used alternately: a build fills one
+  // while the previous build's copy may still be in flight
+  char* himg[2] = {nullptr, nullptr};
+  size_t himg_cap[2] = {0, 0};
+  hipEvent_t himg_ev[2] = {nullptr, nullptr};
+  int himg_cur = 0;
 
-  void release() {
+  void release_blob() {
     if (blob) (void)hipFree(blob);
     blob = nullptr;
     blob_bytes = 0;
   }
+  void release() {
+    release_blob();
+    for (int i = 0; i < 2; ++i) {
+      if (himg_ev[i]) (void)hipEventSynchronize(himg_ev[i]);
+      if (himg_ev[i]) (void)hipEventDestroy(himg_ev[i]);
+      if (himg[i]) (void)hipHostFree(himg[i]);
+      himg[i] = nullptr;
+      himg_ev[i] = nullptr;
+      himg_cap[i] = 0;
+    }
+  }
 
   // Builds (or rebuilds, reusing the allocation when it fits) the device image:
   // [JobDev x njobs][TileDesc x ntiles][split items u32][items u64] then per
-  // job: pkeys, pvals, pn, out, fail, seg, split.
-  int build(int dev, int dt, int mm, const std::vector<JobSpec>& jobs) {
+  // job: pkeys, pvals, pn, out, fail, seg, split.  The image is copied on
+  // stream `strm`, without a host wait when `async`; work enqueued on
+  // `strm` afterwards sees it.
+  int build(int dev, int dt, int mm, const std::vector<JobSpec>& jobs, hipStream_t strm = nullptr,
+            bool async = false) {
     device = dev;
     dtype = dt;
     m = mm;
@@ -209,30 +231,43 @@ struct JobTable {
       if (h[j].mode == psg::kStream) off = align_up(off + 8 * (nt + 1), 256);
     }
     if (off > blob_bytes) {
-      release();
+      if (async) HIP_TRY(hipStreamSynchronize(strm));  // the old blob may be in use
+      release_blob();
       HIP_TRY(hipMalloc(&blob, off));
       blob_bytes = off;
     }
     char* base = (char*)blob;
-    host_img.assign(off, 0);
-    psg::TileDesc* htiles = (psg::TileDesc*)&host_img[tiles_off];
-    uint32_t* hsitems = (uint32_t*)&host_img[sitems_off];
-    uint64_t* hitems = (uint64_t*)&host_img[items_off];
+    const int ib = himg_cur;
+    himg_cur ^= 1;
+    if (himg_ev[ib]) HIP_TRY(hipEventSynchronize(himg_ev[ib]));
+    else HIP_TRY(hipEventCreateWithFlags(&himg_ev[ib], hipEventDisableTiming));
+    if (off > himg_cap[ib]) {
+      if (himg[ib]) HIP_TRY(hipHostFree(himg[ib]));
+      himg[ib] = nullptr;
+      himg_cap[ib] = 0;
+      HIP_TRY(hipHostMalloc((void**)&himg[ib], off));
+      himg_cap[ib] = off;
+    }
+    char* img = himg[ib];
+    memset(img, 0, off);
+    psg::TileDesc* htiles = (psg::TileDesc*)(img + tiles_off);
+    uint32_t* hsitems = (uint32_t*)(img + sitems_off);
+    uint64_t* hitems = (uint64_t*)(img + items_off);
     uint64_t tcur = 0, icur = 0, scur = 0;
     for (size_t j = 0; j < jobs.size(); ++j) {
       const JobSpec& s = jobs[j];
       JobInfo& I = info[j];
       const Offs& o = offs[j];
       const uint32_t np = I.np, nt = I.ntiles;
-      uint64_t* hk = (uint64_t*)&host_img[o.pk];
-      uint64_t* hv = (uint64_t*)&host_img[o.pv];
+      uint64_t* hk = (uint64_t*)(img + o.pk);
+      uint64_t* hv = (uint64_t*)(img + o.pv);
       for (uint32_t p = 0; p < np; ++p) {
         const uint32_t c = I.slot[p];
         hk[p] = (uint64_t)s.pkeys[c];
         for (int i = 0; i < m; ++i) hv[(size_t)p * m + i] = (uint64_t)s.pvals[(size_t)c * m + i];
       }
-      memcpy(&host_img[o.pn], I.pn.data(), 8 * np);
-      memcpy(&host_img[o.out], s.out.data(), 8 * m);
+      memcpy(img + o.pn, I.pn.data(), 8 * np);
+      memcpy(img + o.out, s.out.data(), 8 * m);
       JobDev& d = h[j];
       d.dkeys = s.keys;
       d.pkeys = (const uint64_t* const*)(base + o.pk);
@@ -276,7 +311,7 @@ struct JobTable {
         T.flags = s.flags;
       }
     }
-    memcpy(host_img.data(), h.data(), sizeof(JobDev) * h.size());
+    memcpy(img, h.data(), sizeof(JobDev) * h.size());
     ntiles = (uint32_t)tiles;
     nitems = (uint32_t)items;
     nsplit = (uint32_t)scur;
@@ -284,7 +319,9 @@ struct JobTable {
     d_tiles = (psg::TileDesc*)(base + tiles_off);
     d_split_items = (uint32_t*)(base + sitems_off);
     d_items = (uint64_t*)(base + items_off);
-    HIP_TRY(hipMemcpy(blob, host_img.data(), off, hipMemcpyHostToDevice));
+    HIP_TRY(hipMemcpyAsync(blob, img, off, hipMemcpyHostToDevice, strm));
+    HIP_TRY(hipEventRecord(himg_ev[ib], strm));
+    if (!async) HIP_TRY(hipStreamSynchronize(strm));
     return PSG_OK;
   }
 
@@ -348,19 +385,29 @@ struct psg_plan {
 // ==========================================================================
 namespace {
 
+// Device keys of one push.  Shared: a key-cache entry (RNode::key_cache_,
+// remote_node.h:92-93) and every pending push that was restored from it
+// hold the same resident copy; the last owner returns it to the pool.
+struct KeyBuf {
+  uint64_t* d = nullptr;
+  size_t n = 0, bytes = 0;
+};
+using KeyRef = std::shared_ptr<KeyBuf>;
+
 struct Channel {
   uint64_t* d_keys = nullptr;
-  size_t n = 0, cap = 0;
-  std::vector<uint64_t> h_keys;  // host mirror of key_[chl]
+  size_t n = 0, kbytes = 0;
+  std::vector<uint64_t> h_keys;  // host mirror of key_[chl] (findRange)
   void* d_vals = nullptr;
   size_t nvals = 0;
 };
 
 struct PendingPush {
-  uint64_t* d_keys = nullptr;      // keys then values in one allocation
+  KeyRef keys;
+  void* vblock = nullptr;  // the m value arrays
+  size_t vbytes = 0;
   void* d_vals[psg::kMaxM] = {};
   uint64_t n = 0;
-  size_t bytes = 0;
 };
 
 struct Aggregate {
@@ -369,9 +416,33 @@ struct Aggregate {
   void* d_out[psg::kMaxM] = {};
   std::vector<PendingPush> pending;
   uint64_t folded = 0;               // pushes already merged into d_out
-  uint64_t expected_total = 0, matched_total = 0;
-  bool unmatched = false;
+  uint64_t expected_total = 0;
+  unsigned long long* d_bad = nullptr;  // device: pushed keys not matched so far
 };
+
+// key_cache_ of remote node `sender`, index (key_channel, key_range)
+// (remote_node.cc:98-99,141-142)
+struct CacheKey {
+  int sender, chl;
+  uint64_t kb, ke;
+  bool operator<(const CacheKey& o) const {
+    if (sender != o.sender) return sender < o.sender;
+    return chl != o.chl ? chl < o.chl : kb != o.kb ? kb < o.kb : ke < o.ke;
+  }
+};
+struct CacheEntry {
+  uint32_t sig = 0;
+  KeyRef keys;
+};
+
+bool host_pinned(const void* p) {
+  hipPointerAttribute_t a;
+  if (hipPointerGetAttributes(&a, p) != hipSuccess) {
+    (void)hipGetLastError();  // pageable memory: not an error for us
+    return false;
+  }
+  return a.type == hipMemoryTypeHost;
+}
 
 }  // namespace
 
@@ -379,26 +450,51 @@ struct psg_ctx {
   int device = 0;
   int dtype = PSG_F32;
   unsigned flags = PSG_SERIAL_MATCH;
-  hipStream_t stream = nullptr;
+  hipStream_t stream = nullptr;  // kernels, D2H
+  hipStream_t copy = nullptr;    // H2D of pushes / keys / values
+  hipEvent_t copy_ev = nullptr;
   std::mutex mu;
   std::unordered_map<int, Channel> ch;
   std::map<int, Aggregate> agg;
+  std::map<CacheKey, CacheEntry> kcache;
   JobTable table;
-  unsigned long long* d_counter = nullptr;  // scratch counter (8 words)
+  unsigned long long* d_small = nullptr;  // 32 device words: counters, crc args
+  unsigned long long* h_small = nullptr;  // 32 pinned host words
   void* scratch = nullptr;
   size_t scratch_bytes = 0;
   size_t flush_pushes = psg::kMaxPush;  // pushes per aggregate launch
-  // Freed push-staging and aggregate blocks, by size: a server sees the same
-  // shapes every iteration, so after the first one no push allocates.
-  std::multimap<size_t, void*> pool;
+
+  // ---- device block pool.  Freed push, key and aggregate blocks, by size: a
+  // server sees the same shapes every iteration, so after the first one no
+  // push allocates.  A block is returned with an event recorded on `stream`
+  // (the kernels that read it were enqueued there before); a writer on
+  // another stream waits for that event before reusing it.
+  struct Pooled {
+    void* p;
+    hipEvent_t ev;
+  };
+  std::multimap<size_t, Pooled> pool;
   size_t pool_bytes = 0;
+  std::vector<hipEvent_t> free_ev;
   static constexpr size_t kPoolCap = size_t(8) << 30;
 
-  int dev_get(size_t b, void** p) {
+  int event(hipEvent_t* e) {
+    if (!free_ev.empty()) {
+      *e = free_ev.back();
+      free_ev.pop_back();
+      return PSG_OK;
+    }
+    HIP_TRY(hipEventCreateWithFlags(e, hipEventDisableTiming));
+    return PSG_OK;
+  }
+
+  int dev_get(size_t b, void** p, hipStream_t writer) {
     b = align_up(b ? b : 1, 4096);
     auto it = pool.lower_bound(b);
     if (it != pool.end() && it->first <= 2 * b) {
-      *p = it->second;
+      *p = it->second.p;
+      if (writer != stream) HIP_TRY(hipStreamWaitEvent(writer, it->second.ev, 0));
+      free_ev.push_back(it->second.ev);
       pool_bytes -= it->first;
       pool.erase(it);
       return PSG_OK;
@@ -409,21 +505,121 @@ struct psg_ctx {
   void dev_put(void* p, size_t b) {
     if (!p) return;
     b = align_up(b ? b : 1, 4096);
-    if (pool_bytes + b > kPoolCap) {
+    hipEvent_t e = nullptr;
+    if (pool_bytes + b > kPoolCap || event(&e) != PSG_OK ||
+        hipEventRecord(e, stream) != hipSuccess) {
+      if (e) free_ev.push_back(e);
+      (void)hipStreamSynchronize(stream);
       (void)hipFree(p);
       return;
     }
-    pool.emplace(b, p);
+    pool.emplace(b, Pooled{p, e});
     pool_bytes += b;
   }
   void pool_release() {
-    for (auto& kv : pool) (void)hipFree(kv.second);
+    for (auto& kv : pool) {
+      (void)hipFree(kv.second.p);
+      (void)hipEventDestroy(kv.second.ev);
+    }
     pool.clear();
     pool_bytes = 0;
+    for (hipEvent_t e : free_ev) (void)hipEventDestroy(e);
+    free_ev.clear();
+  }
+
+  int new_keys(size_t n, KeyRef* out) {
+    KeyBuf* k = new KeyBuf();
+    k->n = n;
+    k->bytes = 8 * n;
+    if (int rc = dev_get(k->bytes, (void**)&k->d, copy)) {
+      delete k;
+      return rc;
+    }
+    *out = KeyRef(k, [this](KeyBuf* q) {
+      dev_put(q->d, q->bytes);
+      delete q;
+    });
+    return PSG_OK;
+  }
+
+  // ---- host -> device on `copy`.  The caller's buffer is free on return:
+  // pinned memory is copied directly and waited for; pageable memory is
+  // copied by the CPU into a pinned staging ring whose DMA runs on while
+  // the caller goes on (no wait).
+  char* ring = nullptr;
+  size_t ring_cap = 0, ring_head = 0;
+  struct Flight {
+    size_t off, len;
+    hipEvent_t ev;
+  };
+  std::deque<Flight> fly;
+  static constexpr size_t kRingBytes = size_t(64) << 20;
+  static constexpr size_t kRingPiece = size_t(4) << 20;
+
+  int ring_reserve(size_t len, size_t* off) {
+    if (!ring) {
+      HIP_TRY(hipHostMalloc((void**)&ring, kRingBytes));
+      ring_cap = kRingBytes;
+    }
+    if (ring_head + len > ring_cap) ring_head = 0;
+    int last = -1;
+    for (size_t i = 0; i < fly.size(); ++i)
+      if (fly[i].off < ring_head + len && ring_head < fly[i].off + fly[i].len) last = (int)i;
+    if (last >= 0) {  // events complete in order on `copy`
+      HIP_TRY(hipEventSynchronize(fly[last].ev));
+      for (int i = 0; i <= last; ++i) {
+        free_ev.push_back(fly.front().ev);
+        fly.pop_front();
+      }
+    }
+    *off = ring_head;
+    ring_head += len;
+    return PSG_OK;
+  }
+
+  bool pinned_wait = false;  // a pinned copy of this call is still in flight
+  int h2d(void* dst, const void* src, size_t len) {
+    if (!len) return PSG_OK;
+    if (host_pinned(src)) {
+      HIP_TRY(hipMemcpyAsync(dst, src, len, hipMemcpyHostToDevice, copy));
+      pinned_wait = !(flags & PSG_HOLD_BUFFERS);
+      return PSG_OK;
+    }
+    for (size_t done = 0; done < len;) {
+      const size_t piece = std::min(len - done, kRingPiece);
+      size_t off;
+      if (int rc = ring_reserve(piece, &off)) return rc;
+      memcpy(ring + off, (const char*)src + done, piece);
+      HIP_TRY(hipMemcpyAsync((char*)dst + done, ring + off, piece, hipMemcpyHostToDevice, copy));
+      hipEvent_t e;
+      if (int rc = event(&e)) return rc;
+      HIP_TRY(hipEventRecord(e, copy));
+      fly.push_back(Flight{off, piece, e});
+      done += piece;
+    }
+    return PSG_OK;
+  }
+
+  // end of an API call that staged caller buffers: they must be free on
+  // return unless the caller holds them (PSG_HOLD_BUFFERS)
+  int h2d_finish() {
+    if (!pinned_wait) return PSG_OK;
+    pinned_wait = false;
+    HIP_TRY(hipEventRecord(copy_ev, copy));
+    HIP_TRY(hipEventSynchronize(copy_ev));
+    return PSG_OK;
+  }
+
+  // work enqueued on `stream` from now on sees every H2D issued so far
+  int join_copy() {
+    HIP_TRY(hipEventRecord(copy_ev, copy));
+    HIP_TRY(hipStreamWaitEvent(stream, copy_ev, 0));
+    return PSG_OK;
   }
 
   int ensure_scratch(size_t b) {
     if (b <= scratch_bytes) return PSG_OK;
+    HIP_TRY(hipStreamSynchronize(stream));
     if (scratch) HIP_TRY(hipFree(scratch));
     scratch = nullptr;
     scratch_bytes = 0;
@@ -432,8 +628,17 @@ struct psg_ctx {
     return PSG_OK;
   }
 
-  // Merge every pending push of aggregate `a` into its device output.
+  void release_push(PendingPush& pp) {
+    pp.keys.reset();
+    dev_put(pp.vblock, pp.vbytes);
+    pp.vblock = nullptr;
+  }
+
+  // Enqueue the merge of every pending push of `a` into its device output;
+  // unmatched keys accumulate in a.d_bad.  No host wait.
   int flush(Aggregate& a) {
+    if (a.pending.empty()) return PSG_OK;
+    if (int rc = join_copy()) return rc;
     while (!a.pending.empty()) {
       const size_t take = std::min(a.pending.size(), flush_pushes);
       JobSpec js;
@@ -443,29 +648,32 @@ struct psg_ctx {
                  (a.folded > 0 ? psg::kFlagCont : 0u);
       for (size_t p = 0; p < take; ++p) {
         const PendingPush& pp = a.pending[p];
-        js.pkeys.push_back(pp.d_keys);
+        js.pkeys.push_back(pp.keys->d);
         for (int i = 0; i < a.m; ++i) js.pvals.push_back(pp.d_vals[i]);
         js.pn.push_back(pp.n);
       }
       for (int i = 0; i < a.m; ++i) js.out.push_back(a.d_out[i]);
-      int rc = table.build(device, dtype, a.m, {js});
-      if (rc) return rc;
-      rc = table.run(stream);
-      if (rc) return rc;
-      HIP_TRY(hipStreamSynchronize(stream));
-      std::vector<uint64_t> mt;
-      rc = table.matched(mt);
-      if (rc) return rc;
-      for (size_t p = 0; p < take; ++p) {
-        a.matched_total += mt[p];
-        if (mt[p] != a.pending[p].n) a.unmatched = true;
-        dev_put(a.pending[p].d_keys, a.pending[p].bytes);
-      }
+      if (int rc = table.build(device, dtype, a.m, {js}, stream, true)) return rc;
+      if (int rc = table.run(stream)) return rc;
+      HIP_TRY(psg::launch_unmatched(table.d_jobs, 0, table.info[0].np, a.d_bad, stream));
+      for (size_t p = 0; p < take; ++p) release_push(a.pending[p]);
       a.pending.erase(a.pending.begin(), a.pending.begin() + take);
       a.folded += take;
     }
     return PSG_OK;
   }
+
+  void drop(Aggregate& a) {
+    const size_t sv = vsize(dtype);
+    for (auto& pp : a.pending) release_push(pp);
+    a.pending.clear();
+    for (int i = 0; i < a.m; ++i) dev_put(a.d_out[i], (a.hi - a.lo) * sv);
+    dev_put(a.d_bad, 8);
+  }
+
+  // the value push behind psg_push / psg_push_cached: keys already resident
+  int push_values(int chl, int time, uint64_t kb, uint64_t ke, const KeyRef& keys, int m,
+                  const void* const* vals);
 };
 
 namespace {
@@ -494,6 +702,7 @@ const char* psg_status_string(int s) {
     case PSG_ERR_SIZE: return "value/key size mismatch";
     case PSG_ERR_CHANNEL: return "channel mismatch";
     case PSG_ERR_EMPTY_KEYS: return "channel has no server keys";
+    case PSG_ERR_SIGNATURE: return "key signature mismatch";
     default: return "unknown status";
   }
 }
@@ -661,9 +870,12 @@ int psg_create(int device, int dtype, unsigned flags, psg_ctx** out) {
     if (v >= 1 && v <= psg::kMaxPush) c->flush_pushes = (size_t)v;
   }
   hipError_t e = hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking);
-  if (e == hipSuccess) e = hipMalloc((void**)&c->d_counter, 64);
+  if (e == hipSuccess) e = hipStreamCreateWithFlags(&c->copy, hipStreamNonBlocking);
+  if (e == hipSuccess) e = hipEventCreateWithFlags(&c->copy_ev, hipEventDisableTiming);
+  if (e == hipSuccess) e = hipMalloc((void**)&c->d_small, 256);
+  if (e == hipSuccess) e = hipHostMalloc((void**)&c->h_small, 256);
   if (e != hipSuccess) {
-    delete c;
+    psg_destroy(c);
     return fail(PSG_ERR_DEVICE, "psg_create: %s", hipGetErrorString(e));
   }
   *out = c;
@@ -673,20 +885,28 @@ int psg_create(int device, int dtype, unsigned flags, psg_ctx** out) {
 int psg_destroy(psg_ctx* c) {
   if (!c) return PSG_OK;
   (void)hipSetDevice(c->device);
-  (void)hipStreamSynchronize(c->stream);
-  for (auto& kv : c->agg) {
-    for (auto& pp : kv.second.pending) (void)hipFree(pp.d_keys);
-    for (int i = 0; i < kv.second.m; ++i) (void)hipFree(kv.second.d_out[i]);
-  }
+  if (c->copy) (void)hipStreamSynchronize(c->copy);
+  if (c->stream) (void)hipStreamSynchronize(c->stream);
+  for (auto& kv : c->agg) c->drop(kv.second);
+  c->agg.clear();
+  c->kcache.clear();
   for (auto& kv : c->ch) {
-    (void)hipFree(kv.second.d_keys);
-    (void)hipFree(kv.second.d_vals);
+    c->dev_put(kv.second.d_keys, kv.second.kbytes);
+    c->dev_put(kv.second.d_vals, kv.second.nvals * vsize(c->dtype));
   }
+  c->ch.clear();
+  if (c->stream) (void)hipStreamSynchronize(c->stream);
+  for (auto& f : c->fly) c->free_ev.push_back(f.ev);
+  c->fly.clear();
   c->table.release();
   c->pool_release();
-  (void)hipFree(c->d_counter);
+  if (c->ring) (void)hipHostFree(c->ring);
+  (void)hipFree(c->d_small);
+  if (c->h_small) (void)hipHostFree(c->h_small);
   (void)hipFree(c->scratch);
-  (void)hipStreamDestroy(c->stream);
+  if (c->copy_ev) (void)hipEventDestroy(c->copy_ev);
+  if (c->copy) (void)hipStreamDestroy(c->copy);
+  if (c->stream) (void)hipStreamDestroy(c->stream);
   delete c;
   return PSG_OK;
 }
@@ -698,47 +918,143 @@ int psg_set_match_flags(psg_ctx* c, unsigned flags) {
   return PSG_OK;
 }
 
+namespace {
+
+// key_[chl] = key_[chl].setUnion(keys); val_[chl].clear()  (kv_vector.h:
+// 177-182).  `keys` (host, n > 0) is merged into the host mirror on the CPU
+// and `d_new` (the same keys, resident) into the device key set.
+int key_union_impl(psg_ctx* c, int chl, const uint64_t* keys, size_t n, uint64_t* d_new) {
+  Channel& C = c->ch[chl];
+  // Pending value pushes of this channel were matched against the current
+  // key_[chl] in the reference (setValue matches at arrival,
+  // kv_vector.h:171-204): enqueue their merge before the key set (and so
+  // every position) changes.  The old key array goes back to the pool after
+  // those kernels.
+  for (auto& kv : c->agg)
+    if (kv.second.chl == chl && !kv.second.pending.empty())
+      if (int rc = c->flush(kv.second)) return rc;
+  if (int rc = c->join_copy()) return rc;
+  if (int rc = c->ensure_scratch(psg::union_scratch_bytes(n))) return rc;
+  uint64_t* d_out = nullptr;
+  if (int rc = c->dev_get(8 * (C.n + n), (void**)&d_out, c->stream)) return rc;
+  HIP_TRY(hipMemsetAsync(c->d_small, 0, 16, c->stream));
+  HIP_TRY(psg::launch_check_sorted(d_new, n, c->d_small, c->stream));
+  HIP_TRY(psg::launch_union(C.d_keys, C.n, d_new, n, d_out, c->scratch,
+                            (uint64_t*)(c->d_small + 1), c->stream));
+  HIP_TRY(hipMemcpyAsync(c->h_small, c->d_small, 16, hipMemcpyDeviceToHost, c->stream));
+  HIP_TRY(hipStreamSynchronize(c->stream));
+  const unsigned long long bad = c->h_small[0], nu = c->h_small[1];
+  if (bad) {
+    c->dev_put(d_out, 8 * (C.n + n));
+    return fail(PSG_ERR_UNSORTED, "key-only push: %llu order violations", bad);
+  }
+  // the host mirror: the same union on the CPU from the caller's keys (no
+  // device-to-host copy of the key set)
+  std::vector<uint64_t> merged;
+  merged.reserve(C.n + n);
+  std::set_union(C.h_keys.begin(), C.h_keys.end(), keys, keys + n, std::back_inserter(merged));
+  if (merged.size() != nu) {
+    c->dev_put(d_out, 8 * (C.n + n));
+    return fail(PSG_ERR_DEVICE, "key union: device %llu keys, host mirror %zu", nu,
+                merged.size());
+  }
+  c->dev_put(C.d_keys, C.kbytes);
+  C.d_keys = d_out;
+  C.kbytes = 8 * (C.n + n);
+  C.n = (size_t)nu;
+  C.h_keys.swap(merged);
+  // val_[chl].clear()  (kv_vector.h:180)
+  c->dev_put(C.d_vals, C.nvals * vsize(c->dtype));
+  C.d_vals = nullptr;
+  C.nvals = 0;
+  return PSG_OK;
+}
+
+// findRange of a push and the consistency checks of setValue, before any
+// data is staged
+int check_push(psg_ctx* c, int chl, int time, uint64_t kb, uint64_t ke, size_t n, int m,
+               size_t* lo, size_t* hi) {
+  if (m < 1 || m > PSG_MAX_VALUE_ARRAYS) return fail(PSG_ERR_ARG, "m=%d", m);
+  if (ke < kb) return fail(PSG_ERR_ARG, "invalid key range");
+  auto cit = c->ch.find(chl);
+  if (cit == c->ch.end() || cit->second.n == 0)
+    return fail(PSG_ERR_EMPTY_KEYS, "channel %d has no server keys", chl);
+  const Channel& C = cit->second;
+  *lo = std::lower_bound(C.h_keys.begin(), C.h_keys.end(), kb) - C.h_keys.begin();
+  *hi = std::lower_bound(C.h_keys.begin(), C.h_keys.end(), ke) - C.h_keys.begin();
+  if (*hi - *lo < n)  // pigeonhole: some key cannot match (CHECK_GE, kv_vector.h:121,191)
+    return fail(PSG_ERR_UNMATCHED, "push of %zu keys into a range of %zu server keys", n,
+                *hi - *lo);
+  auto ait = c->agg.find(time);
+  if (ait != c->agg.end()) {
+    const Aggregate& A = ait->second;
+    if (A.chl != chl) return fail(PSG_ERR_CHANNEL, "time %d: channel %d != %d", time, chl, A.chl);
+    if (A.lo != *lo || A.hi != *hi)  // CHECK_EQ(aligned.first, stored) kv_vector.h:199
+      return fail(PSG_ERR_RANGE, "time %d: range [%zu,%zu) != [%zu,%zu)", time, *lo, *hi,
+                  A.lo, A.hi);
+    if (A.m != m) return fail(PSG_ERR_ARG, "time %d: %d value arrays != %d", time, m, A.m);
+  }
+  return PSG_OK;
+}
+
+}  // namespace
+
+int psg_ctx::push_values(int chl, int time, uint64_t kb, uint64_t ke, const KeyRef& keys, int m,
+                         const void* const* vals) {
+  (void)kb;
+  (void)ke;
+  size_t lo = 0, hi = 0;
+  auto ait = agg.find(time);
+  {
+    // (re-derived: the caller checked before staging the keys)
+    const Channel& C = ch[chl];
+    lo = std::lower_bound(C.h_keys.begin(), C.h_keys.end(), kb) - C.h_keys.begin();
+    hi = std::lower_bound(C.h_keys.begin(), C.h_keys.end(), ke) - C.h_keys.begin();
+  }
+  const size_t sv = vsize(dtype), n = keys->n;
+  PendingPush pp;
+  pp.n = n;
+  pp.keys = keys;
+  const size_t vb = align_up(sv * n, 256);
+  pp.vbytes = m * vb;
+  if (int rc = dev_get(pp.vbytes, &pp.vblock, copy)) return rc;
+  for (int i = 0; i < m; ++i) {
+    pp.d_vals[i] = (char*)pp.vblock + i * vb;
+    if (int rc = h2d(pp.d_vals[i], vals[i], sv * n)) {
+      release_push(pp);
+      return rc;
+    }
+  }
+  if (ait == agg.end()) {
+    Aggregate A;
+    A.chl = chl;
+    A.m = m;
+    A.lo = lo;
+    A.hi = hi;
+    for (int i = 0; i < m; ++i)
+      if (int rc = dev_get((hi - lo) * sv, &A.d_out[i], stream)) return rc;
+    if (int rc = dev_get(8, (void**)&A.d_bad, stream)) return rc;
+    HIP_TRY(hipMemsetAsync(A.d_bad, 0, 8, stream));
+    ait = agg.emplace(time, A).first;
+  }
+  Aggregate& A = ait->second;
+  A.pending.push_back(pp);
+  A.expected_total += n;
+  if (A.pending.size() >= flush_pushes) return flush(A);
+  return PSG_OK;
+}
+
 int psg_key_union(psg_ctx* c, int chl, const uint64_t* keys, size_t n) {
   if (!c || (n && !keys)) return fail(PSG_ERR_ARG, "null argument");
   std::lock_guard<std::mutex> l(c->mu);
   if (n == 0) return PSG_OK;  // kv_vector.h:177: empty key list is ignored
   if (int rc = set_dev(c->device)) return rc;
-  Channel& C = c->ch[chl];
-  // Pending value pushes of this channel were matched against the current
-  // key_[chl] in the reference (setValue matches at arrival,
-  // kv_vector.h:171-204): merge them before the key set (and so every
-  // position) changes.
-  for (auto& kv : c->agg)
-    if (kv.second.chl == chl && !kv.second.pending.empty())
-      if (int rc = c->flush(kv.second)) return rc;
-  const size_t sb = psg::union_scratch_bytes(n);
-  if (int rc = c->ensure_scratch(align_up(sb, 256) + 8 * n)) return rc;
-  uint64_t* d_new = (uint64_t*)((char*)c->scratch + align_up(sb, 256));
-  HIP_TRY(hipMemcpyAsync(d_new, keys, 8 * n, hipMemcpyHostToDevice, c->stream));
-  HIP_TRY(hipMemsetAsync(c->d_counter, 0, 16, c->stream));
-  HIP_TRY(psg::launch_check_sorted(d_new, n, c->d_counter, c->stream));
-  uint64_t* d_out = nullptr;
-  HIP_TRY(hipMalloc(&d_out, 8 * (C.n + n)));
-  HIP_TRY(psg::launch_union(C.d_keys, C.n, d_new, n, d_out, c->scratch,
-                            (uint64_t*)(c->d_counter + 1), c->stream));
-  unsigned long long h[2];
-  HIP_TRY(hipMemcpyAsync(h, c->d_counter, 16, hipMemcpyDeviceToHost, c->stream));
-  HIP_TRY(hipStreamSynchronize(c->stream));
-  if (h[0]) {
-    (void)hipFree(d_out);
-    return fail(PSG_ERR_UNSORTED, "key-only push: %llu order violations", h[0]);
-  }
-  HIP_TRY(hipFree(C.d_keys));
-  C.d_keys = d_out;
-  C.n = (size_t)h[1];
-  C.cap = C.n;
-  C.h_keys.resize(C.n);
-  HIP_TRY(hipMemcpy(C.h_keys.data(), C.d_keys, 8 * C.n, hipMemcpyDeviceToHost));
-  // val_[chl].clear()  (kv_vector.h:180)
-  HIP_TRY(hipFree(C.d_vals));
-  C.d_vals = nullptr;
-  C.nvals = 0;
-  return PSG_OK;
+  KeyRef k;
+  if (int rc = c->new_keys(n, &k)) return rc;
+  int rc = c->h2d(k->d, keys, 8 * n);
+  if (rc == PSG_OK) rc = key_union_impl(c, chl, keys, n, k->d);
+  const int rf = c->h2d_finish();
+  return rc ? rc : rf;
 }
 
 int psg_key_size(psg_ctx* c, int chl, size_t* n) {
@@ -780,16 +1096,18 @@ int psg_value_assign(psg_ctx* c, int chl, const void* vals, size_t n) {
   std::lock_guard<std::mutex> l(c->mu);
   if (int rc = set_dev(c->device)) return rc;
   Channel& C = c->ch[chl];
-  const size_t b = n * vsize(c->dtype);
-  if (n != C.nvals) {
-    HIP_TRY(hipFree(C.d_vals));
-    C.d_vals = nullptr;
-    if (n) HIP_TRY(hipMalloc(&C.d_vals, b));
+  const size_t sv = vsize(c->dtype);
+  // the old array goes back to the pool (after any kernel reading it); the
+  // new one is written on the copy stream once it is free
+  c->dev_put(C.d_vals, C.nvals * sv);
+  C.d_vals = nullptr;
+  C.nvals = 0;
+  if (n) {
+    if (int rc = c->dev_get(n * sv, &C.d_vals, c->copy)) return rc;
     C.nvals = n;
+    if (int rc = c->h2d(C.d_vals, vals, n * sv)) return rc;
   }
-  if (n) HIP_TRY(hipMemcpyAsync(C.d_vals, vals, b, hipMemcpyHostToDevice, c->stream));
-  HIP_TRY(hipStreamSynchronize(c->stream));
-  return PSG_OK;
+  return c->h2d_finish();
 }
 
 int psg_value_size(psg_ctx* c, int chl, size_t* n) {
@@ -807,10 +1125,12 @@ int psg_value_copy(psg_ctx* c, int chl, size_t off, size_t n, void* out) {
   const size_t have = it == c->ch.end() ? 0 : it->second.nvals;
   if (off + n > have) return fail(PSG_ERR_ARG, "value copy out of range");
   if (int rc = set_dev(c->device)) return rc;
+  if (int rc = c->join_copy()) return rc;
   const size_t sv = vsize(c->dtype);
   if (n)
-    HIP_TRY(hipMemcpy(out, (char*)it->second.d_vals + off * sv, n * sv,
-                      hipMemcpyDeviceToHost));
+    HIP_TRY(hipMemcpyAsync(out, (char*)it->second.d_vals + off * sv, n * sv,
+                           hipMemcpyDeviceToHost, c->stream));
+  HIP_TRY(hipStreamSynchronize(c->stream));
   return PSG_OK;
 }
 
@@ -819,58 +1139,127 @@ int psg_push(psg_ctx* c, int chl, int time, uint64_t kb, uint64_t ke,
   if (!c) return fail(PSG_ERR_ARG, "null ctx");
   if (n == 0) return PSG_OK;  // kv_vector.h:90,177 -- empty push ignored
   if (!keys || !vals) return fail(PSG_ERR_ARG, "null keys/values");
-  if (m < 1 || m > PSG_MAX_VALUE_ARRAYS) return fail(PSG_ERR_ARG, "m=%d", m);
-  for (int i = 0; i < m; ++i)
+  for (int i = 0; i < m && i < PSG_MAX_VALUE_ARRAYS; ++i)
     if (!vals[i]) return fail(PSG_ERR_ARG, "null value array %d", i);
-  if (ke < kb) return fail(PSG_ERR_ARG, "invalid key range");
   std::lock_guard<std::mutex> l(c->mu);
   if (int rc = set_dev(c->device)) return rc;
-  auto cit = c->ch.find(chl);
-  if (cit == c->ch.end() || cit->second.n == 0)
-    return fail(PSG_ERR_EMPTY_KEYS, "channel %d has no server keys", chl);
-  Channel& C = cit->second;
-  const size_t lo = std::lower_bound(C.h_keys.begin(), C.h_keys.end(), kb) - C.h_keys.begin();
-  const size_t hi = std::lower_bound(C.h_keys.begin(), C.h_keys.end(), ke) - C.h_keys.begin();
-  if (hi - lo < n)  // pigeonhole: some key cannot match (CHECK_GE, kv_vector.h:121,191)
-    return fail(PSG_ERR_UNMATCHED, "push of %zu keys into a range of %zu server keys",
-                n, hi - lo);
-  auto ait = c->agg.find(time);
-  if (ait != c->agg.end()) {
-    Aggregate& A = ait->second;
-    if (A.chl != chl) return fail(PSG_ERR_CHANNEL, "time %d: channel %d != %d", time, chl, A.chl);
-    if (A.lo != lo || A.hi != hi)  // CHECK_EQ(aligned.first, stored) kv_vector.h:199
-      return fail(PSG_ERR_RANGE, "time %d: range [%zu,%zu) != [%zu,%zu)", time, lo, hi,
-                  A.lo, A.hi);
-    if (A.m != m) return fail(PSG_ERR_ARG, "time %d: %d value arrays != %d", time, m, A.m);
+  size_t lo, hi;
+  if (int rc = check_push(c, chl, time, kb, ke, n, m, &lo, &hi)) return rc;
+  KeyRef k;
+  int rc = c->new_keys(n, &k);
+  if (rc == PSG_OK) rc = c->h2d(k->d, keys, 8 * n);
+  if (rc == PSG_OK) rc = c->push_values(chl, time, kb, ke, k, m, vals);
+  const int rf = c->h2d_finish();
+  return rc ? rc : rf;
+}
+
+namespace {
+int push_cached_impl(psg_ctx* c, int sender, int chl, int time, uint64_t kb, uint64_t ke,
+                     unsigned kc, uint32_t sig, const uint64_t* keys, size_t nkeys, int m,
+                     const void* const* vals, size_t nvals);
+}
+
+int psg_push_cached(psg_ctx* c, int sender, int chl, int time, uint64_t kb, uint64_t ke,
+                    unsigned kc, uint32_t sig, const uint64_t* keys, size_t nkeys, int m,
+                    const void* const* vals, size_t nvals) {
+  if (!c) return fail(PSG_ERR_ARG, "null ctx");
+  std::lock_guard<std::mutex> l(c->mu);
+  const int rc = push_cached_impl(c, sender, chl, time, kb, ke, kc, sig, keys, nkeys, m, vals,
+                                  nvals);
+  const int rf = c->h2d_finish();
+  return rc ? rc : rf;
+}
+
+namespace {
+int push_cached_impl(psg_ctx* c, int sender, int chl, int time, uint64_t kb, uint64_t ke,
+                     unsigned kc, uint32_t sig, const uint64_t* keys, size_t nkeys, int m,
+                     const void* const* vals, size_t nvals) {
+  if ((kc & PSG_KC_KEYS) && nkeys && !keys) return fail(PSG_ERR_ARG, "null keys");
+  if (m < 0 || m > PSG_MAX_VALUE_ARRAYS || (m > 0 && !vals)) return fail(PSG_ERR_ARG, "m=%d", m);
+  for (int i = 0; i < m; ++i)
+    if (nvals && !vals[i]) return fail(PSG_ERR_ARG, "null value array %d", i);
+  if (int rc = set_dev(c->device)) return rc;
+  const CacheKey ck{sender, chl, kb, ke};
+  KeyRef k;  // the message's keys, resident
+  std::vector<uint64_t> hk;  // host keys when the message carried them
+  if (!(kc & PSG_KC_SIG)) {
+    // no signature: the cache entry of (channel, range) is dropped
+    // (remote_node.cc:143-156) and the message's own keys are used
+    c->kcache.erase(ck);
+    if ((kc & PSG_KC_KEYS) && nkeys) {
+      if (int rc = c->new_keys(nkeys, &k)) return rc;
+      if (int rc = c->h2d(k->d, keys, 8 * nkeys)) return rc;
+    }
+  } else if (kc & PSG_KC_KEYS) {
+    // keys carried: check the signature, store them (remote_node.cc:161-171)
+    if (nkeys) {
+      if (int rc = c->new_keys(nkeys, &k)) return rc;
+      if (int rc = c->h2d(k->d, keys, 8 * nkeys)) return rc;
+    }
+    uint32_t got = 0;  // crc32c::Value of no bytes
+    if (nkeys) {
+      c->h_small[8] = 0;
+      c->h_small[9] = 8 * nkeys;
+      HIP_TRY(hipMemcpyAsync(c->d_small + 8, c->h_small + 8, 16, hipMemcpyHostToDevice, c->copy));
+      HIP_TRY(psg::launch_crc32c((const uint8_t*)k->d, (const uint64_t*)(c->d_small + 8), 1,
+                                 PSG_MAX_SIG_LEN, nullptr, (uint32_t*)(c->d_small + 10), c->copy));
+      HIP_TRY(hipMemcpyAsync(c->h_small + 10, c->d_small + 10, 8, hipMemcpyDeviceToHost, c->copy));
+      HIP_TRY(hipStreamSynchronize(c->copy));
+      got = (uint32_t)c->h_small[10];
+    }
+    if (got != sig)  // CHECK_EQ(crc32c(key), sig) remote_node.cc:163
+      return fail(PSG_ERR_SIGNATURE, "key signature %08x != carried %08x", got, sig);
+    CacheEntry& e = c->kcache[ck];
+    e.sig = sig;
+    e.keys = k;
+  } else {
+    // keys restored from the cache (remote_node.cc:172-176)
+    auto it = c->kcache.find(ck);
+    const uint32_t have = it == c->kcache.end() ? 0u : it->second.sig;
+    if (sig != have)  // CHECK_EQ(sig, cache.first)
+      return fail(PSG_ERR_SIGNATURE, "key cache of channel %d [%llu,%llu): signature %08x != %08x",
+                  chl, (unsigned long long)kb, (unsigned long long)ke, sig, have);
+    if (it != c->kcache.end()) k = it->second.keys;
   }
-  const size_t sv = vsize(c->dtype);
-  PendingPush pp;
-  pp.n = n;
-  const size_t kbytes = align_up(8 * n, 256), vbytes = align_up(sv * n, 256);
-  pp.bytes = kbytes + m * vbytes;
-  if (int rc = c->dev_get(pp.bytes, (void**)&pp.d_keys)) return rc;
-  HIP_TRY(hipMemcpyAsync(pp.d_keys, keys, 8 * n, hipMemcpyHostToDevice, c->stream));
-  for (int i = 0; i < m; ++i) {
-    pp.d_vals[i] = (char*)pp.d_keys + kbytes + i * vbytes;
-    HIP_TRY(hipMemcpyAsync(pp.d_vals[i], vals[i], sv * n, hipMemcpyHostToDevice, c->stream));
+  if (kc & PSG_KC_ERASE) c->kcache.erase(ck);  // remote_node.cc:183
+  const size_t n = k ? k->n : 0;
+  if (n == 0) return PSG_OK;  // kv_vector.h:90,177: no keys, message ignored
+  if (m == 0 || nvals == 0) {
+    // key-only message: setUnion with the (possibly restored) keys
+    hk.resize(n);
+    if ((kc & PSG_KC_KEYS) && keys) {
+      memcpy(hk.data(), keys, 8 * n);
+    } else {
+      if (int rc = c->join_copy()) return rc;
+      HIP_TRY(hipMemcpyAsync(hk.data(), k->d, 8 * n, hipMemcpyDeviceToHost, c->stream));
+      HIP_TRY(hipStreamSynchronize(c->stream));
+    }
+    return key_union_impl(c, chl, hk.data(), n, k->d);
   }
-  // the caller's buffers are free after return
-  HIP_TRY(hipStreamSynchronize(c->stream));
-  if (ait == c->agg.end()) {
-    Aggregate A;
-    A.chl = chl;
-    A.m = m;
-    A.lo = lo;
-    A.hi = hi;
-    for (int i = 0; i < m; ++i)
-      if (hi > lo)
-        if (int rc = c->dev_get((hi - lo) * sv, &A.d_out[i])) return rc;
-    ait = c->agg.emplace(time, A).first;
-  }
-  Aggregate& A = ait->second;
-  A.pending.push_back(pp);
-  A.expected_total += n;
-  if (A.pending.size() >= c->flush_pushes) return c->flush(A);
+  if (nvals != n)  // CHECK_EQ(recv_data.size(), recv_key.size()) kv_vector.h:108,187
+    return fail(PSG_ERR_SIZE, "%zu values for %zu keys", nvals, n);
+  size_t lo, hi;
+  if (int rc = check_push(c, chl, time, kb, ke, n, m, &lo, &hi)) return rc;
+  return c->push_values(chl, time, kb, ke, k, m, vals);
+}
+
+}  // namespace
+
+int psg_key_cache_clear(psg_ctx* c, int sender) {
+  if (!c) return fail(PSG_ERR_ARG, "null ctx");
+  std::lock_guard<std::mutex> l(c->mu);
+  for (auto it = c->kcache.begin(); it != c->kcache.end();)
+    it = (sender < 0 || it->first.sender == sender) ? c->kcache.erase(it) : std::next(it);
+  return PSG_OK;
+}
+
+int psg_key_cache_bytes(psg_ctx* c, int sender, size_t* bytes) {
+  if (!c || !bytes) return fail(PSG_ERR_ARG, "null argument");
+  std::lock_guard<std::mutex> l(c->mu);
+  size_t b = 0;
+  for (const auto& kv : c->kcache)
+    if ((sender < 0 || kv.first.sender == sender) && kv.second.keys) b += kv.second.keys->bytes;
+  *bytes = b;
   return PSG_OK;
 }
 
@@ -895,23 +1284,24 @@ int psg_received(psg_ctx* c, int time, int m, void* const* out) {
   if (m != A.m || !out) return fail(PSG_ERR_ARG, "expected %d output arrays", A.m);
   int rc = c->flush(A);
   const size_t len = A.hi - A.lo, sv = vsize(c->dtype);
-  if (rc == PSG_OK) {
-    for (int i = 0; i < A.m && len; ++i) {
-      hipError_t e = hipMemcpy(out[i], A.d_out[i], len * sv, hipMemcpyDeviceToHost);
-      if (e != hipSuccess) {
-        rc = fail(PSG_ERR_DEVICE, "D2H: %s", hipGetErrorString(e));
-        break;
-      }
-    }
+  for (int i = 0; rc == PSG_OK && i < A.m && len; ++i) {
+    hipError_t e = hipMemcpyAsync(out[i], A.d_out[i], len * sv, hipMemcpyDeviceToHost, c->stream);
+    if (e != hipSuccess) rc = fail(PSG_ERR_DEVICE, "D2H: %s", hipGetErrorString(e));
   }
-  const bool bad = A.unmatched;
-  const unsigned long long got = A.matched_total, want = A.expected_total;
-  for (auto& pp : A.pending) c->dev_put(pp.d_keys, pp.bytes);
-  for (int i = 0; i < A.m; ++i) c->dev_put(A.d_out[i], (A.hi - A.lo) * sv);
+  unsigned long long bad = 0;
+  if (rc == PSG_OK) {
+    hipError_t e = hipMemcpyAsync(c->h_small, A.d_bad, 8, hipMemcpyDeviceToHost, c->stream);
+    if (e == hipSuccess) e = hipStreamSynchronize(c->stream);
+    if (e != hipSuccess) rc = fail(PSG_ERR_DEVICE, "received: %s", hipGetErrorString(e));
+    bad = c->h_small[0];
+  }
+  const unsigned long long want = A.expected_total;
+  c->drop(A);
   c->agg.erase(it);
   if (rc) return rc;
   if (bad)
-    return fail(PSG_ERR_UNMATCHED, "time %d: matched %llu of %llu pushed keys", time, got, want);
+    return fail(PSG_ERR_UNMATCHED, "time %d: matched %llu of %llu pushed keys", time,
+                want - bad, want);
   return PSG_OK;
 }
 
@@ -929,15 +1319,20 @@ int psg_gather(psg_ctx* c, int chl, const uint64_t* keys, size_t n, void* out,
   if (int rc = c->ensure_scratch(align_up(8 * n, 256) + n * sv)) return rc;
   uint64_t* d_req = (uint64_t*)c->scratch;
   void* d_out = (char*)c->scratch + align_up(8 * n, 256);
-  HIP_TRY(hipMemcpyAsync(d_req, keys, 8 * n, hipMemcpyHostToDevice, c->stream));
-  HIP_TRY(hipMemsetAsync(c->d_counter, 0, 8, c->stream));
+  if (int rc = c->h2d(d_req, keys, 8 * n)) return rc;
+  if (int rc = c->join_copy()) return rc;
+  HIP_TRY(hipMemsetAsync(c->d_small, 0, 16, c->stream));
+  HIP_TRY(psg::launch_check_sorted(d_req, n, c->d_small + 1, c->stream, false));
   HIP_TRY(psg::launch_gather(c->dtype, C.d_keys, C.n, C.d_vals, d_req, n, d_out,
-                             c->d_counter, c->stream));
-  unsigned long long mt = 0;
+                             c->d_small, c->stream));
   HIP_TRY(hipMemcpyAsync(out, d_out, n * sv, hipMemcpyDeviceToHost, c->stream));
-  HIP_TRY(hipMemcpyAsync(&mt, c->d_counter, 8, hipMemcpyDeviceToHost, c->stream));
+  HIP_TRY(hipMemcpyAsync(c->h_small, c->d_small, 16, hipMemcpyDeviceToHost, c->stream));
   HIP_TRY(hipStreamSynchronize(c->stream));
-  if (matched) *matched = (size_t)mt;
+  // getValue walks the request with the merge of oldMatch (kv_vector.h:
+  // 222-224), whose contract is a sorted request (message.h:248-264)
+  if (int rc = c->h2d_finish()) return rc;
+  if (c->h_small[1]) return fail(PSG_ERR_UNSORTED, "gather: request keys not sorted");
+  if (matched) *matched = (size_t)c->h_small[0];
   return PSG_OK;
 }
 

@@ -44,6 +44,12 @@ class Message:
     request: bool = True
     key: np.ndarray = field(default_factory=lambda: np.zeros(0, np.uint64))
     value: List[np.ndarray] = field(default_factory=list)
+    # key cache fields (task.proto: key_signature, has_key, erase_key_cache;
+    # system/remote_node.cc:96-184); key_signature None = not set
+    key_signature: Optional[int] = None
+    has_key: bool = True
+    erase_key_cache: bool = False
+    sender: int = 0  # the remote node (each has its own key cache)
 
 
 class KVVector:
@@ -105,6 +111,8 @@ class KVVector:
 
     # -- setValue: kv_vector.h:75-82 ---------------------------------------
     def setValue(self, msg: Message) -> None:
+        if msg.key_signature is not None or not msg.has_key or msg.erase_key_cache:
+            return self._set_value_cached(msg)
         keys = np.ascontiguousarray(msg.key, dtype=np.uint64)
         if keys.size == 0:
             return
@@ -124,13 +132,46 @@ class KVVector:
                                     int(msg.key_range[0]), int(msg.key_range[1]),
                                     _ptr(keys), keys.size, len(vals), arr))
 
+    def _set_value_cached(self, msg: Message) -> None:
+        """RNode::cacheKeyRecver (remote_node.cc:139-184), then setValue: the
+        keys of a message without them are the resident cached copy."""
+        from ._lib import PSG_KC_ERASE, PSG_KC_KEYS, PSG_KC_SIG
+        kc = (PSG_KC_SIG if msg.key_signature is not None else 0) | \
+             (PSG_KC_KEYS if msg.has_key else 0) | (PSG_KC_ERASE if msg.erase_key_cache else 0)
+        keys = np.ascontiguousarray(msg.key if msg.has_key else np.zeros(0), dtype=np.uint64)
+        vals = [np.ascontiguousarray(v, dtype=self.np_dtype) for v in msg.value]
+        nv = vals[0].size if vals else 0
+        if any(v.size != nv for v in vals):
+            raise _lib.PSGError(_lib.PSG_ERR_SIZE, "value arrays of different sizes")
+        arr = _lib.ptr_array([_ptr(a) for a in vals]) if vals else None
+        _lib.check(self._L.psg_push_cached(
+            self._h, msg.sender, msg.key_channel, msg.time, int(msg.key_range[0]), int(msg.key_range[1]),
+            kc, int(msg.key_signature or 0) & 0xffffffff, _ptr(keys) if keys.size else None,
+            keys.size, len(vals), arr, nv))
+
+    def key_cache_bytes(self, sender: int = -1) -> int:
+        """RNode::memSize (remote_node.cc:186-195); -1: all senders."""
+        n = C.c_size_t()
+        _lib.check(self._L.psg_key_cache_bytes(self._h, sender, C.byref(n)))
+        return n.value
+
+    def clear_key_cache(self, sender: int = -1) -> None:
+        """RNode::clearCache (remote_node.h:54); -1: all senders."""
+        _lib.check(self._L.psg_key_cache_clear(self._h, sender))
+
     # -- received(t): kv_vector.h:65-73 ------------------------------------
-    def received(self, t: int):
-        """Returns [((lo, hi), values_i) for each value array], then erases t."""
+    def received(self, t: int, out: Optional[List[np.ndarray]] = None):
+        """Returns [((lo, hi), values_i) for each value array], then erases t.
+        `out`: caller arrays (e.g. pinned) of at least hi - lo entries."""
         m, lo, hi = C.c_int(), C.c_size_t(), C.c_size_t()
         _lib.check(self._L.psg_received_shape(self._h, t, C.byref(m), C.byref(lo),
                                               C.byref(hi)))
-        outs = [np.empty(hi.value - lo.value, self.np_dtype) for _ in range(m.value)]
+        n = hi.value - lo.value
+        if out is not None and len(out) == m.value and all(
+                o.dtype == self.np_dtype and o.size >= n and o.flags.c_contiguous for o in out):
+            outs = [o[:n] for o in out]
+        else:
+            outs = [np.empty(n, self.np_dtype) for _ in range(m.value)]
         arr = _lib.ptr_array([_ptr(o) for o in outs])
         _lib.check(self._L.psg_received(self._h, t, m.value, arr))
         return [((lo.value, hi.value), o) for o in outs]

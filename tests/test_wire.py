@@ -151,3 +151,187 @@ def test_gpu_key_signature_of_pushes():
     assert [int(x) for x in got] == [O.key_signature(k) for k, _ in pushes]
     if O.ref_crc_available():
         assert int(got[0]) == O.ref_crc32c(pushes[0][0].tobytes()[:2048])
+
+
+# --------------------------------------------------- key cache (GPU) ----
+def _kvv(dtype=np.float32):
+    from parameter_server_amd.kv_vector import KVVector
+    from parameter_server_amd._lib import PSG_F32, PSG_F64
+    return KVVector(0, PSG_F32 if dtype == np.float32 else PSG_F64)
+
+
+def _msg(keys=None, vals=None, t=0, sig=None, has_key=True, erase=False, sender=0,
+         rng=(0, (1 << 64) - 1)):
+    from parameter_server_amd.kv_vector import Message
+    return Message(time=t, key_range=rng, sender=sender,
+                   key=np.zeros(0, np.uint64) if keys is None else np.asarray(keys, np.uint64),
+                   value=[] if vals is None else [np.asarray(v) for v in vals],
+                   key_signature=sig, has_key=has_key, erase_key_cache=erase)
+
+
+def _bits(a):
+    a = np.asarray(a)
+    return a.view(np.uint32 if a.dtype == np.float32 else np.uint64)
+
+
+@pytest.mark.gpu
+def test_key_cache_store_then_restore_bitexact():
+    """Iteration 1: each worker's push carries keys + signature (stored in
+    that sender's cache); iteration 2: pushes carry only the signature and
+    the values, the keys are the resident cached copy.  Both aggregates are
+    bit-exact against the oracle and identical to plain pushes."""
+    import torch
+    assert torch.cuda.is_available()
+    from parameter_server_amd import synth
+    D, pushes = synth.overlap_pushes(seed=21, npush=6, n=20000)
+    v = _kvv()
+    v.setValue(_msg(D))
+    for t in (1, 2):
+        for w, (k, vals) in enumerate(pushes):
+            sig = O.key_signature(k)
+            vv = [x * t for x in vals]
+            if t == 1:
+                v.setValue(_msg(k, vv, t=t, sig=sig, sender=w))
+            else:
+                v.setValue(_msg(None, vv, t=t, sig=sig, has_key=False, sender=w))
+        (rng, got), = v.received(t)
+        rc, lo, hi, want, _ = O.aggregate(D, 0, (1 << 64) - 1, [(k, [x * t for x in vals])
+                                                                for k, vals in pushes])
+        assert rc == 0 and (lo, hi) == tuple(rng)
+        assert np.array_equal(_bits(got), _bits(want[0]))
+    assert v.key_cache_bytes() == sum(8 * k.size for k, _ in pushes)
+    assert v.key_cache_bytes(2) == 8 * pushes[2][0].size
+    v.clear_key_cache(2)
+    assert v.key_cache_bytes() == sum(8 * k.size for i, (k, _) in enumerate(pushes) if i != 2)
+    v.close()
+
+
+@pytest.mark.gpu
+def test_key_cache_signature_errors_and_erase():
+    import torch
+    assert torch.cuda.is_available()
+    from parameter_server_amd._lib import PSGError, PSG_ERR_SIGNATURE, PSG_ERR_NO_TIME
+    rng = np.random.default_rng(4)
+    D = np.unique(rng.integers(0, 1 << 40, 5000, dtype=np.uint64))
+    k = np.sort(rng.choice(D, 700, replace=False))
+    x = rng.standard_normal(k.size).astype(np.float32)
+    v = _kvv()
+    v.setValue(_msg(D))
+    sig = O.key_signature(k)
+    # carried keys whose crc32c differs from the carried signature: CHECK_EQ (:163)
+    with pytest.raises(PSGError) as e:
+        v.setValue(_msg(k, [x], t=1, sig=sig ^ 1))
+    assert e.value.status == PSG_ERR_SIGNATURE
+    # restore without an entry, signature != 0: CHECK_EQ(sig, cache.first) (:174)
+    with pytest.raises(PSGError) as e:
+        v.setValue(_msg(None, [x], t=1, sig=sig, has_key=False))
+    assert e.value.status == PSG_ERR_SIGNATURE
+    # restore without an entry, signature 0: no keys -> message ignored (kv_vector.h:177)
+    v.setValue(_msg(None, [x], t=1, sig=0, has_key=False))
+    with pytest.raises(PSGError) as e:
+        v.received(1)
+    assert e.value.status == PSG_ERR_NO_TIME
+    # store, then a message without signature drops the entry (:143-146)
+    v.setValue(_msg(k, [x], t=2, sig=sig))
+    assert v.key_cache_bytes() == 8 * k.size
+    v.setValue(_msg(k, [x], t=2))  # plain keys, no signature
+    v.setValue(_msg(k, [x], t=2, sig=None, erase=True))
+    assert v.key_cache_bytes() == 0
+    (_, got), = v.received(2)
+    rc, _, _, want, _ = O.aggregate(D, 0, (1 << 64) - 1, [(k, [x])] * 3)
+    assert np.array_equal(_bits(got), _bits(want[0]))
+    # erase_key_cache after a restore (:183)
+    v.setValue(_msg(k, [x], t=3, sig=sig))
+    v.setValue(_msg(None, [x], t=3, sig=sig, has_key=False, erase=True))
+    assert v.key_cache_bytes() == 0
+    with pytest.raises(PSGError):
+        v.setValue(_msg(None, [x], t=3, sig=sig, has_key=False))
+    (_, got), = v.received(3)
+    want2 = O.aggregate(D, 0, (1 << 64) - 1, [(k, [x])] * 2)[3][0]
+    assert np.array_equal(_bits(got), _bits(want2))
+    v.close()
+
+
+@pytest.mark.gpu
+def test_key_cache_replaced_while_pushes_pending_and_key_only():
+    """An entry replaced (new keys, same channel/range) while pushes restored
+    from the old one are still pending: those pushes keep the old resident
+    keys.  A key-only message restored from the cache is a setUnion."""
+    import torch
+    assert torch.cuda.is_available()
+    rng = np.random.default_rng(8)
+    D = np.unique(rng.integers(0, 1 << 40, 8000, dtype=np.uint64))
+    k1 = np.sort(rng.choice(D, 900, replace=False))
+    k2 = np.sort(rng.choice(D, 1300, replace=False))
+    x1 = rng.standard_normal(k1.size).astype(np.float64)
+    x2 = rng.standard_normal(k2.size).astype(np.float64)
+    v = _kvv(np.float64)
+    v.setValue(_msg(D))
+    v.setValue(_msg(k1, [x1], t=5, sig=O.key_signature(k1)))
+    v.setValue(_msg(None, [x1], t=5, sig=O.key_signature(k1), has_key=False))
+    v.setValue(_msg(k2, [x2], t=5, sig=O.key_signature(k2)))  # replaces the entry
+    v.setValue(_msg(None, [x2], t=5, sig=O.key_signature(k2), has_key=False))
+    (_, got), = v.received(5)
+    _, _, _, want, _ = O.aggregate(D, 0, (1 << 64) - 1, [(k1, [x1]), (k1, [x1]), (k2, [x2]),
+                                                         (k2, [x2])], dtype=np.float64)
+    assert np.array_equal(_bits(got), _bits(want[0]))
+    extra = np.sort(rng.integers(1 << 41, 1 << 42, 50, dtype=np.uint64))
+    v.setValue(_msg(extra, None, sig=O.key_signature(extra), sender=3))
+    assert np.array_equal(v.key(0), O.set_union(D, extra))
+    v.setValue(_msg(None, None, sig=O.key_signature(extra), has_key=False, sender=3))
+    assert np.array_equal(v.key(0), O.set_union(D, extra))
+    v.close()
+
+
+@pytest.mark.gpu
+def test_pinned_and_pageable_pushes_agree():
+    """Pushes from pinned host memory (direct DMA) and from pageable memory
+    (staging ring) give the same bits; the caller may overwrite its buffers
+    right after psg_push returns."""
+    import torch
+    assert torch.cuda.is_available()
+    from parameter_server_amd import synth
+    D, pushes = synth.overlap_pushes(seed=13, npush=8, n=131072)
+    outs = []
+    for pinned in (False, True):
+        v = _kvv()
+        v.setValue(_msg(D))
+        kbuf = torch.empty(131072, dtype=torch.int64, pin_memory=pinned).numpy().view(np.uint64)
+        vbuf = torch.empty(131072, dtype=torch.float32, pin_memory=pinned).numpy()
+        for k, vals in pushes:
+            kb, vb = kbuf[: k.size], vbuf[: k.size]
+            kb[:] = k
+            vb[:] = vals[0]
+            v.setValue(_msg(kb, [vb], t=9))
+            kb[:] = 0  # reuse the buffers at once
+            vb[:] = np.nan
+        (_, got), = v.received(9)
+        outs.append(got)
+        v.close()
+    _, _, _, want, _ = O.aggregate(D, 0, (1 << 64) - 1, pushes)
+    for got in outs:
+        assert np.array_equal(_bits(got), _bits(want[0]))
+
+
+@pytest.mark.gpu
+def test_hold_buffers_option():
+    """PSG_HOLD_BUFFERS: pinned push buffers are DMA'd without a wait per
+    push and must stay valid until received(t); the result is unchanged."""
+    import ctypes as C
+    import torch
+    assert torch.cuda.is_available()
+    from parameter_server_amd import synth, _lib
+    from parameter_server_amd.kv_vector import KVVector
+    D, pushes = synth.overlap_pushes(seed=17, npush=8, n=60000)
+    v = KVVector(0)
+    _lib.check(v._L.psg_set_match_flags(v._h, _lib.PSG_SERIAL_MATCH | _lib.PSG_HOLD_BUFFERS))
+    v.setValue(_msg(D))
+    held = [(torch.from_numpy(k.view(np.int64)).pin_memory().numpy().view(np.uint64),
+             torch.from_numpy(x[0]).pin_memory().numpy()) for k, x in pushes]
+    for t in (1, 2):
+        for k, x in held:
+            v.setValue(_msg(k, [x * 1.0 if t == 2 else x], t=t))
+        (_, got), = v.received(t)
+        _, _, _, want, _ = O.aggregate(D, 0, (1 << 64) - 1, pushes)
+        assert np.array_equal(_bits(got), _bits(want[0]))
+    v.close()
