@@ -208,6 +208,66 @@ int psg_slice_dev(const uint64_t* keys, uint64_t n, uint64_t kb, uint64_t ke,
                   const uint64_t* sep, int nsep, uint64_t* pos, void* stream);
 
 /* ------------------------------------------------------------------ */
+/* Server model update fused on the resident aggregate (Darling, L1-LR */
+/* block coordinate descent; src/linear_method/darling.cc)             */
+/* ------------------------------------------------------------------ */
+typedef struct psg_darling_param {
+  double eta;                  /* conf_.learning_rate().eta() */
+  double lambda;               /* conf_.penalty().lambda(0) */
+  double kkt_filter_threshold; /* Darling::KKT_filter_threshold_ */
+  double delta_max;            /* conf_.darling().delta_max_value() */
+} psg_darling_param;
+
+/* Darling::preprocessData server state of channel grp (darling.cc:
+ * 111-117): active_set all true, delta = delta_init, sized to key(chl).
+ * Requires a PSG_F64 context (KVVector<Key,double>). */
+int psg_darling_init(psg_ctx* ctx, int chl, double delta_init);
+/* kkt_filter_reset: active_set.fill(true) (darling.cc:167-169). */
+int psg_darling_reset_active(psg_ctx* ctx, int chl);
+/* The server's UPDATE_MODEL step (darling.cc:251-262): received(time) must
+ * hold m = 2 aggregates (G, U) of channel chl; updateWeight
+ * (darling.cc:437-477) runs on the device over value(chl), delta and the
+ * active set at the aggregate's positions, and the aggregate is erased.
+ * Nothing crosses PCIe but *violation = max vio of this block (the caller
+ * folds it into violation_ with std::max).  PSG_ERR_UNMATCHED leaves the
+ * model untouched. */
+int psg_darling_update(psg_ctx* ctx, int chl, int time, const psg_darling_param* p,
+                       double* violation);
+/* Copies of delta[off, off+n) and the active bits (one byte each, 0/1);
+ * *nnz_active = active_set.nnz() (darling.cc:549).  Any output may be NULL. */
+int psg_darling_state(psg_ctx* ctx, int chl, size_t off, size_t n, double* delta,
+                      uint8_t* active, size_t* nnz_active);
+
+/* ------------------------------------------------------------------ */
+/* Tail-feature filter: FreqencyFilter<uint64> of channel chl          */
+/* (SharedParameter::key_filter_, shared_parameter.h:82,114-133) over  */
+/* CountMin<uint64, uint8> (src/base/countmin.h), resident in HBM.     */
+/* ------------------------------------------------------------------ */
+/* CountMin::resize (countmin.h:14-19): n_ = max(n, 64) byte counters,
+ * k_ = min(30, max(1, k)) probes, all zero. */
+int psg_freq_resize(psg_ctx* ctx, int chl, int n, int k);
+int psg_freq_clear(psg_ctx* ctx, int chl);                 /* clear() */
+int psg_freq_empty(psg_ctx* ctx, int chl, int* empty);     /* empty() */
+/* insertKeys (frequency_filter.h:36-43): counts[i] is added as uint8 to
+ * every probe of keys[i] (byte arithmetic wraps).  Host arrays; async. */
+int psg_freq_insert(psg_ctx* ctx, int chl, const uint64_t* keys,
+                    const uint32_t* counts, size_t n);
+/* queryKeys (frequency_filter.h:27-34): out[0, *nout) = the keys whose
+ * count estimate is > freq, in input order (out holds n).  freq < 255. */
+int psg_freq_query(psg_ctx* ctx, int chl, const uint64_t* keys, size_t n,
+                   int freq, uint64_t* out, size_t* nout);
+/* Device-resident forms on `stream`: *nout is a device word; scratch holds
+ * psg_freq_query_scratch_bytes(n) device bytes. */
+int psg_freq_insert_dev(psg_ctx* ctx, int chl, const uint64_t* keys,
+                        const uint32_t* counts, size_t n, void* stream);
+size_t psg_freq_query_scratch_bytes(size_t n);
+int psg_freq_query_dev(psg_ctx* ctx, int chl, const uint64_t* keys, size_t n,
+                       int freq, uint64_t* out, unsigned long long* nout,
+                       void* scratch, void* stream);
+/* The n_ counters as CountMin's uint8 data_ (tests, checkpoints). */
+int psg_freq_table(psg_ctx* ctx, int chl, uint8_t* out, size_t n);
+
+/* ------------------------------------------------------------------ */
 /* Wire ingress: key signatures of the key cache                       */
 /* ------------------------------------------------------------------ */
 /* CRC-32C of device-resident byte segments: out[i] = crc32c::Extend(

@@ -10,6 +10,7 @@
 #include <pthread.h>
 #include <stdlib.h>
 #include <string.h>
+#include <math.h>
 
 /* std::lower_bound / upper_bound over uint64 */
 static size_t lb_u64(const uint64_t* a, size_t n, uint64_t k) {
@@ -402,4 +403,103 @@ uint32_t orc_crc32c_mask(uint32_t crc) {
 uint32_t orc_crc32c_unmask(uint32_t masked) {
   const uint32_t rot = masked - 0xa282ead8u;
   return (rot >> 17) | (rot << 15);
+}
+
+/* ---------------------------------------------------------------------- */
+/* Darling::updateWeight (linear_method/darling.cc:437-477) with newDelta  */
+/* (darling.h:31-33) and kInactiveValue_ = all-ones bits (darling.cc:13-15)*/
+/* over positions [lo, lo+n) of the server weights.  *violation is folded  */
+/* with std::max as violation_ is (darling.cc:466).  PARITY UNPINNED: the  */
+/* reference ships no test of this function and darling.cc cannot be      */
+/* built here (protobuf/glog/Eigen); this is a line-by-line restatement.   */
+/* ---------------------------------------------------------------------- */
+static double std_min_d(double a, double b) { return b < a ? b : a; }
+static double std_max_d(double a, double b) { return a < b ? b : a; }
+
+void orc_darling_update_weight(double* value, double* delta, uint8_t* active,
+                               size_t lo, size_t n, const double* G,
+                               const double* U, double eta, double lambda,
+                               double kkt, double delta_max,
+                               double* violation) {
+  double inactive_value;
+  const uint64_t ones = ~(uint64_t)0;
+  memcpy(&inactive_value, &ones, sizeof(double));
+  for (size_t i = 0; i < n; ++i) {
+    const size_t k = i + lo;
+    if (!active[k]) continue;
+    double g = G[i], u = U[i] / eta + 1e-10;
+    double g_pos = g + lambda, g_neg = g - lambda;
+    double* w = &value[k];
+    double d = -*w, vio = 0;
+    if (*w == 0) {
+      if (g_pos < 0) {
+        vio = -g_pos;
+      } else if (g_neg > 0) {
+        vio = g_neg;
+      } else if (g_pos > kkt && g_neg < -kkt) {
+        active[k] = 0;
+        *w = inactive_value;
+        continue;
+      }
+    }
+    *violation = std_max_d(*violation, vio);
+    if (g_pos <= u * *w) {
+      d = -g_pos / u;
+    } else if (g_neg >= u * *w) {
+      d = -g_neg / u;
+    }
+    d = std_min_d(delta[k], std_max_d(-delta[k], d));
+    delta[k] = std_min_d(delta_max, 2 * fabs(d) + .1);
+    *w += d;
+  }
+}
+
+/* ---------------------------------------------------------------------- */
+/* CountMin<uint64, uint8> (base/countmin.h:14-67) and FreqencyFilter      */
+/* insertKeys / queryKeys (parameter/frequency_filter.h:27-43), restated   */
+/* on a caller-held table of n uint8 counters (n = max(n, 64) and          */
+/* k = min(30, max(1, k)) already applied by the caller, as resize() does).*/
+/* PARITY UNPINNED: src/test/countmin_test.cc is entirely commented out    */
+/* and countmin.h cannot be compiled here (glog via shared_array_inl.h).   */
+/* ---------------------------------------------------------------------- */
+static uint32_t cm_hash(uint64_t key) {
+  const uint32_t seed = 0xbc9f1d34u, m = 0xc6a4a793u, n = 8;
+  uint32_t h = seed ^ (n * m);
+  uint32_t w = (uint32_t)key;
+  h += w; h *= m; h ^= (h >> 16);
+  w = (uint32_t)(key >> 32);
+  h += w; h *= m; h ^= (h >> 16);
+  return h;
+}
+
+void orc_cm_insert(uint8_t* data, uint32_t n, int k, const uint64_t* keys,
+                   const uint32_t* counts, size_t nk) {
+  for (size_t i = 0; i < nk; ++i) {
+    const uint8_t c = (uint8_t)counts[i]; /* insert(key, V count): uint32 -> uint8 */
+    uint32_t h = cm_hash(keys[i]);
+    const uint32_t delta = (h >> 17) | (h << 15);
+    for (int j = 0; j < k; ++j) {
+      data[h % n] = (uint8_t)(data[h % n] + c);
+      h += delta;
+    }
+  }
+}
+
+uint8_t orc_cm_query(const uint8_t* data, uint32_t n, int k, uint64_t key) {
+  uint8_t res = (uint8_t)0xff;
+  uint32_t h = cm_hash(key);
+  const uint32_t delta = (h >> 17) | (h << 15);
+  for (int j = 0; j < k; ++j) {
+    if (data[h % n] < res) res = data[h % n];
+    h += delta;
+  }
+  return res;
+}
+
+size_t orc_ff_query(const uint8_t* data, uint32_t n, int k, const uint64_t* keys,
+                    size_t nk, int freq, uint64_t* out) {
+  size_t m = 0;
+  for (size_t i = 0; i < nk; ++i)
+    if ((int)orc_cm_query(data, n, k, keys[i]) > freq) out[m++] = keys[i];
+  return m;
 }

@@ -116,6 +116,23 @@ uint32_t orc_crc32c_extend(uint32_t init, const void* data, size_t n);
 uint32_t orc_crc32c_mask(uint32_t crc);
 uint32_t orc_crc32c_unmask(uint32_t masked);
 
+/* Darling::updateWeight (linear_method/darling.cc:437-477), parity
+ * unpinned (no reference test; darling.cc not buildable here).  active is
+ * one byte per position (0/1); *violation is folded with std::max. */
+void orc_darling_update_weight(double* value, double* delta, uint8_t* active,
+                               size_t lo, size_t n, const double* G,
+                               const double* U, double eta, double lambda,
+                               double kkt, double delta_max,
+                               double* violation);
+
+/* CountMin<uint64,uint8> insert/query and FreqencyFilter::queryKeys
+ * (countmin.h:33-51, frequency_filter.h:27-34), parity unpinned. */
+void orc_cm_insert(uint8_t* data, uint32_t n, int k, const uint64_t* keys,
+                   const uint32_t* counts, size_t nk);
+uint8_t orc_cm_query(const uint8_t* data, uint32_t n, int k, uint64_t key);
+size_t orc_ff_query(const uint8_t* data, uint32_t n, int k, const uint64_t* keys,
+                    size_t nk, int freq, uint64_t* out);
+
 #ifdef __cplusplus
 }
 #endif

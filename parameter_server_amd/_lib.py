@@ -102,6 +102,19 @@ SIGNATURES = {
     "psg_shard_bounds": (C.c_int, [_sz, _pu64]),
     "psg_slice_dev": (C.c_int, [_p, _u64, _u64, _u64, _p, C.c_int, _p, _p]),
     "psg_crc32c_dev": (C.c_int, [_p, _p, _u64, _u64, _p, _p, _p]),
+    "psg_freq_resize": (C.c_int, [_p, C.c_int, C.c_int, C.c_int]),
+    "psg_freq_clear": (C.c_int, [_p, C.c_int]),
+    "psg_freq_empty": (C.c_int, [_p, C.c_int, C.POINTER(C.c_int)]),
+    "psg_freq_insert": (C.c_int, [_p, C.c_int, _p, _p, _sz]),
+    "psg_freq_query": (C.c_int, [_p, C.c_int, _p, _sz, C.c_int, _p, _psz]),
+    "psg_freq_insert_dev": (C.c_int, [_p, C.c_int, _p, _p, _sz, _p]),
+    "psg_freq_query_scratch_bytes": (_sz, [_sz]),
+    "psg_freq_query_dev": (C.c_int, [_p, C.c_int, _p, _sz, C.c_int, _p, _p, _p, _p]),
+    "psg_freq_table": (C.c_int, [_p, C.c_int, _p, _sz]),
+    "psg_darling_init": (C.c_int, [_p, C.c_int, C.c_double]),
+    "psg_darling_reset_active": (C.c_int, [_p, C.c_int]),
+    "psg_darling_update": (C.c_int, [_p, C.c_int, C.c_int, _p, C.POINTER(C.c_double)]),
+    "psg_darling_state": (C.c_int, [_p, C.c_int, _sz, _sz, _p, _p, _psz]),
 }
 
 _LIB = None

@@ -1,0 +1,176 @@
+// psg_countmin.hip -- the server's tail-feature filter on the device:
+// FreqencyFilter<uint64>::insertKeys / queryKeys
+// (src/parameter/frequency_filter.h:27-43) over CountMin<uint64, uint8>
+// (src/base/countmin.h:14-67), called from SharedParameter::process for
+// insert_key_freq / query_key_freq tasks (shared_parameter.h:114-133).
+//
+// CountMin<K, uint8>: n_ byte counters, k_ probes per key; probe j of key x
+// is data_[h_j % n_] with h_0 = hash(x), h_{j+1} = h_j + rotr(h_0, 17)
+// (uint32 wrap).  insert adds (uint8)count to each probe (byte wrap);
+// query = min over probes, starting from 255; queryKeys keeps, in input
+// order, the keys whose query is > freqency.
+//
+// GPU form.  Byte counters under concurrent inserts need a byte-wide
+// atomic add that wraps inside its byte: the table is held as uint32
+// counters instead, added with native 32-bit atomics, and read through
+// their low byte -- exact, since (sum mod 2^32) mod 2^8 = sum mod 2^8 and
+// addition mod 2^8 does not depend on order, so any interleaving of inserts
+// gives the reference's table.  Each counter costs one random 4-byte
+// read-modify-write in L2/HBM either way.  queryKeys is a flag pass and an
+// order-preserving compaction (workgroup scan + one scan of block totals).
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include "psg_device.h"
+#include "psg_internal.h"
+
+namespace psg {
+
+namespace {
+
+constexpr int kNT = 256;
+constexpr int kIPT = 8;                 // keys per thread in the query passes
+constexpr int kQTile = kNT * kIPT;      // keys per workgroup
+
+// CountMin::hash (countmin.h:53-64)
+__device__ __forceinline__ uint32_t cm_hash(uint64_t key) {
+  const uint32_t seed = 0xbc9f1d34u, m = 0xc6a4a793u, n = 8;
+  uint32_t h = seed ^ (n * m);
+  uint32_t w = (uint32_t)key;
+  h += w;
+  h *= m;
+  h ^= (h >> 16);
+  w = (uint32_t)(key >> 32);
+  h += w;
+  h *= m;
+  h ^= (h >> 16);
+  return h;
+}
+
+__device__ __forceinline__ uint32_t cm_query(const uint32_t* __restrict__ t, uint32_t n, int k,
+                                             uint64_t key) {
+  uint32_t res = 255u;  // (uint8)kuint64max
+  uint32_t h = cm_hash(key);
+  const uint32_t delta = (h >> 17) | (h << 15);
+  for (int j = 0; j < k; ++j) {
+    const uint32_t v = t[h % n] & 0xffu;
+    res = v < res ? v : res;
+    h += delta;
+  }
+  return res;
+}
+
+__global__ __launch_bounds__(kNT) void cm_insert_kernel(const uint64_t* __restrict__ keys,
+                                                        const uint32_t* __restrict__ counts,
+                                                        uint64_t nk, uint32_t* __restrict__ t,
+                                                        uint32_t n, int k) {
+  const uint64_t i = (uint64_t)blockIdx.x * kNT + threadIdx.x;
+  if (i >= nk) return;
+  const uint32_t c = counts[i] & 0xffu;  // insert(key, (uint8)count)
+  if (!c) return;
+  uint32_t h = cm_hash(keys[i]);
+  const uint32_t delta = (h >> 17) | (h << 15);
+  for (int j = 0; j < k; ++j) {
+    __hip_atomic_fetch_add(t + h % n, c, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    h += delta;
+  }
+}
+
+// pass 1: keys kept per workgroup tile
+__global__ __launch_bounds__(kNT) void cm_count_kernel(const uint64_t* __restrict__ keys,
+                                                       uint64_t nk, const uint32_t* __restrict__ t,
+                                                       uint32_t n, int k, int freq,
+                                                       uint32_t* __restrict__ tile_cnt) {
+  __shared__ uint32_t ws[kNT / 64];
+  const uint64_t base = (uint64_t)blockIdx.x * kQTile;
+  uint32_t c = 0;
+#pragma unroll
+  for (int r = 0; r < kIPT; ++r) {
+    const uint64_t i = base + (uint64_t)r * kNT + threadIdx.x;
+    if (i < nk && (int)cm_query(t, n, k, keys[i]) > freq) ++c;
+  }
+  for (int s = 32; s >= 1; s >>= 1) c += (uint32_t)__shfl_xor((int)c, s, 64);
+  if ((threadIdx.x & 63) == 0) ws[threadIdx.x >> 6] = c;
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    uint32_t tot = 0;
+    for (int w = 0; w < kNT / 64; ++w) tot += ws[w];
+    tile_cnt[blockIdx.x] = tot;
+  }
+}
+
+// pass 2: exclusive scan of the tile counts (one workgroup, sequential chunks)
+__global__ __launch_bounds__(kNT) void cm_scan_kernel(uint32_t* __restrict__ tile_cnt,
+                                                      uint32_t ntiles,
+                                                      unsigned long long* __restrict__ total) {
+  __shared__ uint32_t ws[kNT / 64];
+  __shared__ uint32_t carry;
+  if (threadIdx.x == 0) carry = 0;
+  __syncthreads();
+  for (uint32_t b = 0; b < ntiles; b += kNT) {
+    const uint32_t i = b + threadIdx.x;
+    const uint32_t v = i < ntiles ? tile_cnt[i] : 0u;
+    uint32_t tot;
+    const uint32_t ex = dev::block_excl_scan<kNT>(v, ws, &tot);
+    const uint32_t c0 = carry;
+    if (i < ntiles) tile_cnt[i] = c0 + ex;
+    __syncthreads();
+    if (threadIdx.x == 0) carry = c0 + tot;
+    __syncthreads();
+  }
+  if (threadIdx.x == 0) *total = carry;
+}
+
+// pass 3: scatter the kept keys in input order
+__global__ __launch_bounds__(kNT) void cm_scatter_kernel(const uint64_t* __restrict__ keys,
+                                                         uint64_t nk,
+                                                         const uint32_t* __restrict__ t,
+                                                         uint32_t n, int k, int freq,
+                                                         const uint32_t* __restrict__ tile_off,
+                                                         uint64_t* __restrict__ out) {
+  __shared__ uint32_t ws[kNT / 64];
+  const uint64_t base = (uint64_t)blockIdx.x * kQTile;
+  // thread-contiguous runs keep the output in input order
+  uint32_t keep = 0;
+  uint64_t kk[kIPT];
+#pragma unroll
+  for (int r = 0; r < kIPT; ++r) {
+    const uint64_t i = base + (uint64_t)threadIdx.x * kIPT + r;
+    kk[r] = i < nk ? keys[i] : 0;
+    if (i < nk && (int)cm_query(t, n, k, kk[r]) > freq) keep |= 1u << r;
+  }
+  uint32_t tot;
+  uint32_t pos = tile_off[blockIdx.x] + dev::block_excl_scan<kNT>(__popc(keep), ws, &tot);
+#pragma unroll
+  for (int r = 0; r < kIPT; ++r)
+    if ((keep >> r) & 1u) out[pos++] = kk[r];
+}
+
+}  // namespace
+
+hipError_t launch_cm_insert(const uint64_t* keys, const uint32_t* counts, uint64_t nk,
+                            uint32_t* table, uint32_t n, int k, hipStream_t s) {
+  if (nk == 0) return hipSuccess;
+  hipLaunchKernelGGL(cm_insert_kernel, dim3((uint32_t)((nk + kNT - 1) / kNT)), dim3(kNT), 0, s,
+                     keys, counts, nk, table, n, k);
+  return hipGetLastError();
+}
+
+size_t cm_query_scratch_bytes(uint64_t nk) { return 4 * ((nk + kQTile - 1) / kQTile) + 64; }
+
+hipError_t launch_cm_query(const uint64_t* keys, uint64_t nk, const uint32_t* table, uint32_t n,
+                           int k, int freq, uint64_t* out, unsigned long long* nout,
+                           void* scratch, hipStream_t s) {
+  const uint32_t ntiles = (uint32_t)((nk + kQTile - 1) / kQTile);
+  uint32_t* cnt = (uint32_t*)scratch;
+  if (ntiles)
+    hipLaunchKernelGGL(cm_count_kernel, dim3(ntiles), dim3(kNT), 0, s, keys, nk, table, n, k,
+                       freq, cnt);
+  hipLaunchKernelGGL(cm_scan_kernel, dim3(1), dim3(kNT), 0, s, cnt, ntiles, nout);
+  if (ntiles)
+    hipLaunchKernelGGL(cm_scatter_kernel, dim3(ntiles), dim3(kNT), 0, s, keys, nk, table, n, k,
+                       freq, cnt, out);
+  return hipGetLastError();
+}
+
+}  // namespace psg

@@ -99,6 +99,29 @@ hipError_t launch_slice(const uint64_t* keys, uint64_t n, uint64_t kb,
 hipError_t launch_unmatched(const JobDev* jobs, uint32_t job, uint32_t npush,
                             unsigned long long* bad, hipStream_t stream);
 
+// Darling::updateWeight fused on the resident aggregate (psg_darling.hip)
+struct DarlingParam {
+  double eta, lambda, kkt, delta_max;
+};
+hipError_t launch_darling(const double* G, const double* U, double* w, double* delta,
+                          uint32_t* active, uint64_t lo, uint64_t n, const DarlingParam& P,
+                          const unsigned long long* bad, unsigned long long* vio,
+                          hipStream_t stream);
+hipError_t launch_darling_init(double* delta, uint32_t* active, uint64_t n, double delta_init,
+                               hipStream_t stream);
+hipError_t launch_bitmap_fill(uint32_t* active, uint64_t n, hipStream_t stream);
+hipError_t launch_popcount(const uint32_t* a, uint64_t nw, unsigned long long* out,
+                           hipStream_t stream);
+
+// FreqencyFilter / CountMin<uint64, uint8> (psg_countmin.hip); the table is
+// n uint32 counters read through their low byte
+hipError_t launch_cm_insert(const uint64_t* keys, const uint32_t* counts, uint64_t nk,
+                            uint32_t* table, uint32_t n, int k, hipStream_t stream);
+size_t cm_query_scratch_bytes(uint64_t nk);
+hipError_t launch_cm_query(const uint64_t* keys, uint64_t nk, const uint32_t* table, uint32_t n,
+                           int k, int freq, uint64_t* out, unsigned long long* nout,
+                           void* scratch, hipStream_t stream);
+
 // CRC-32C (psg_crc32c.hip): out[i] = crc32c::Extend(init ? init[i] : 0,
 // data + off[i], min(off[i+1] - off[i], max_len)); all pointers device
 uint64_t crc32c_chunks_per_segment(uint64_t max_len);

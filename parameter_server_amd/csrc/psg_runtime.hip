@@ -400,6 +400,10 @@ struct Channel {
   std::vector<uint64_t> h_keys;  // host mirror of key_[chl] (findRange)
   void* d_vals = nullptr;
   size_t nvals = 0;
+  // Darling server state (darling.h:38-39): delta_[grp], active_set_[grp]
+  double* d_delta = nullptr;
+  uint32_t* d_active = nullptr;
+  size_t dn = 0;
 };
 
 struct PendingPush {
@@ -444,6 +448,13 @@ bool host_pinned(const void* p) {
   return a.type == hipMemoryTypeHost;
 }
 
+// FreqencyFilter<uint64> of one channel (CountMin n_, k_, table)
+struct Filter {
+  uint32_t* d_table = nullptr;
+  uint32_t n = 0;
+  int k = 1;
+};
+
 }  // namespace
 
 struct psg_ctx {
@@ -457,6 +468,7 @@ struct psg_ctx {
   std::unordered_map<int, Channel> ch;
   std::map<int, Aggregate> agg;
   std::map<CacheKey, CacheEntry> kcache;
+  std::unordered_map<int, Filter> ff;
   JobTable table;
   unsigned long long* d_small = nullptr;  // 32 device words: counters, crc args
   unsigned long long* h_small = nullptr;  // 32 pinned host words
@@ -893,8 +905,12 @@ int psg_destroy(psg_ctx* c) {
   for (auto& kv : c->ch) {
     c->dev_put(kv.second.d_keys, kv.second.kbytes);
     c->dev_put(kv.second.d_vals, kv.second.nvals * vsize(c->dtype));
+    c->dev_put(kv.second.d_delta, 8 * kv.second.dn);
+    c->dev_put(kv.second.d_active, 4 * ((kv.second.dn + 31) / 32));
   }
   c->ch.clear();
+  for (auto& kv : c->ff) c->dev_put(kv.second.d_table, 4 * (size_t)kv.second.n);
+  c->ff.clear();
   if (c->stream) (void)hipStreamSynchronize(c->stream);
   for (auto& f : c->fly) c->free_ev.push_back(f.ev);
   c->fly.clear();
@@ -1302,6 +1318,250 @@ int psg_received(psg_ctx* c, int time, int m, void* const* out) {
   if (bad)
     return fail(PSG_ERR_UNMATCHED, "time %d: matched %llu of %llu pushed keys", time,
                 want - bad, want);
+  return PSG_OK;
+}
+
+int psg_darling_init(psg_ctx* c, int chl, double delta_init) {
+  if (!c) return fail(PSG_ERR_ARG, "null ctx");
+  std::lock_guard<std::mutex> l(c->mu);
+  if (c->dtype != PSG_F64) return fail(PSG_ERR_ARG, "Darling needs a PSG_F64 context");
+  if (int rc = set_dev(c->device)) return rc;
+  Channel& C = c->ch[chl];
+  if (C.dn != C.n) {
+    c->dev_put(C.d_delta, 8 * C.dn);
+    c->dev_put(C.d_active, 4 * ((C.dn + 31) / 32));
+    C.d_delta = nullptr;
+    C.d_active = nullptr;
+    C.dn = 0;
+    if (C.n) {
+      if (int rc = c->dev_get(8 * C.n, (void**)&C.d_delta, c->stream)) return rc;
+      if (int rc = c->dev_get(4 * ((C.n + 31) / 32), (void**)&C.d_active, c->stream)) return rc;
+    }
+    C.dn = C.n;
+  }
+  HIP_TRY(psg::launch_darling_init(C.d_delta, C.d_active, C.dn, delta_init, c->stream));
+  return PSG_OK;
+}
+
+int psg_darling_reset_active(psg_ctx* c, int chl) {
+  if (!c) return fail(PSG_ERR_ARG, "null ctx");
+  std::lock_guard<std::mutex> l(c->mu);
+  auto it = c->ch.find(chl);
+  if (it == c->ch.end() || !it->second.d_active)
+    return fail(PSG_ERR_ARG, "channel %d: no Darling state (psg_darling_init)", chl);
+  if (int rc = set_dev(c->device)) return rc;
+  HIP_TRY(psg::launch_bitmap_fill(it->second.d_active, it->second.dn, c->stream));
+  return PSG_OK;
+}
+
+int psg_darling_update(psg_ctx* c, int chl, int time, const psg_darling_param* p,
+                       double* violation) {
+  if (!c || !p) return fail(PSG_ERR_ARG, "null argument");
+  std::lock_guard<std::mutex> l(c->mu);
+  auto it = c->agg.find(time);
+  if (it == c->agg.end()) return fail(PSG_ERR_NO_TIME, "no data received at time %d", time);
+  if (int rc = set_dev(c->device)) return rc;
+  Aggregate& A = it->second;
+  if (A.chl != chl) return fail(PSG_ERR_CHANNEL, "time %d: channel %d != %d", time, A.chl, chl);
+  if (A.m != 2) return fail(PSG_ERR_ARG, "Darling needs 2 aggregates (G, U), time %d has %d",
+                            time, A.m);  // CHECK_EQ(data.size(), 2) darling.cc:253
+  Channel& C = c->ch[chl];
+  if (C.nvals != C.n || C.dn != C.n)
+    return fail(PSG_ERR_SIZE, "channel %d: %zu keys, %zu values, Darling state of %zu", chl,
+                C.n, C.nvals, C.dn);
+  int rc = c->flush(A);
+  if (rc == PSG_OK) {
+    const psg::DarlingParam P{p->eta, p->lambda, p->kkt_filter_threshold, p->delta_max};
+    unsigned long long* dv = c->d_small + 4;
+    hipError_t e = hipMemsetAsync(dv, 0, 8, c->stream);
+    if (e == hipSuccess)
+      e = psg::launch_darling((const double*)A.d_out[0], (const double*)A.d_out[1],
+                              (double*)C.d_vals, C.d_delta, C.d_active, A.lo, A.hi - A.lo, P,
+                              A.d_bad, dv, c->stream);
+    if (e == hipSuccess)
+      e = hipMemcpyAsync(c->h_small + 4, dv, 8, hipMemcpyDeviceToHost, c->stream);
+    if (e == hipSuccess)
+      e = hipMemcpyAsync(c->h_small + 5, A.d_bad, 8, hipMemcpyDeviceToHost, c->stream);
+    if (e == hipSuccess) e = hipStreamSynchronize(c->stream);
+    if (e != hipSuccess) rc = fail(PSG_ERR_DEVICE, "darling update: %s", hipGetErrorString(e));
+  }
+  const unsigned long long bad = rc == PSG_OK ? c->h_small[5] : 0, want = A.expected_total;
+  if (rc == PSG_OK && violation) memcpy(violation, c->h_small + 4, 8);
+  c->drop(A);
+  c->agg.erase(it);
+  if (rc) return rc;
+  if (bad)
+    return fail(PSG_ERR_UNMATCHED, "time %d: matched %llu of %llu pushed keys", time,
+                want - bad, want);
+  return PSG_OK;
+}
+
+int psg_darling_state(psg_ctx* c, int chl, size_t off, size_t n, double* delta, uint8_t* active,
+                      size_t* nnz_active) {
+  if (!c) return fail(PSG_ERR_ARG, "null ctx");
+  std::lock_guard<std::mutex> l(c->mu);
+  auto it = c->ch.find(chl);
+  if (it == c->ch.end() || !it->second.d_active)
+    return fail(PSG_ERR_ARG, "channel %d: no Darling state (psg_darling_init)", chl);
+  const Channel& C = it->second;
+  if (off + n > C.dn) return fail(PSG_ERR_ARG, "Darling state copy out of range");
+  if (int rc = set_dev(c->device)) return rc;
+  std::vector<uint32_t> bits;
+  if (active && n) bits.resize((off + n + 31) / 32 - off / 32);
+  if (delta && n)
+    HIP_TRY(hipMemcpyAsync(delta, C.d_delta + off, 8 * n, hipMemcpyDeviceToHost, c->stream));
+  if (!bits.empty())
+    HIP_TRY(hipMemcpyAsync(bits.data(), C.d_active + off / 32, 4 * bits.size(),
+                           hipMemcpyDeviceToHost, c->stream));
+  if (nnz_active) {
+    HIP_TRY(hipMemsetAsync(c->d_small + 6, 0, 8, c->stream));
+    HIP_TRY(psg::launch_popcount(C.d_active, (C.dn + 31) / 32, c->d_small + 6, c->stream));
+    HIP_TRY(hipMemcpyAsync(c->h_small + 6, c->d_small + 6, 8, hipMemcpyDeviceToHost, c->stream));
+  }
+  HIP_TRY(hipStreamSynchronize(c->stream));
+  for (size_t i = 0; active && i < n; ++i) {
+    const size_t k = off + i;
+    active[i] = (uint8_t)((bits[k / 32 - off / 32] >> (k % 32)) & 1u);
+  }
+  if (nnz_active) *nnz_active = (size_t)c->h_small[6];
+  return PSG_OK;
+}
+
+// ------------------------------------------------------ frequency filter --
+int psg_freq_resize(psg_ctx* c, int chl, int n, int k) {
+  if (!c) return fail(PSG_ERR_ARG, "null ctx");
+  std::lock_guard<std::mutex> l(c->mu);
+  if (int rc = set_dev(c->device)) return rc;
+  Filter& F = c->ff[chl];
+  const uint32_t nn = (uint32_t)std::max(n, 64);  // countmin.h:15
+  if (nn != F.n) {
+    c->dev_put(F.d_table, 4 * (size_t)F.n);
+    F.d_table = nullptr;
+    F.n = 0;
+    if (int rc = c->dev_get(4 * (size_t)nn, (void**)&F.d_table, c->stream)) return rc;
+    F.n = nn;
+  }
+  F.k = std::min(30, std::max(1, k));  // countmin.h:18
+  HIP_TRY(hipMemsetAsync(F.d_table, 0, 4 * (size_t)F.n, c->stream));
+  return PSG_OK;
+}
+
+int psg_freq_clear(psg_ctx* c, int chl) {
+  if (!c) return fail(PSG_ERR_ARG, "null ctx");
+  std::lock_guard<std::mutex> l(c->mu);
+  auto it = c->ff.find(chl);
+  if (it != c->ff.end()) {
+    c->dev_put(it->second.d_table, 4 * (size_t)it->second.n);
+    c->ff.erase(it);
+  }
+  return PSG_OK;
+}
+
+int psg_freq_empty(psg_ctx* c, int chl, int* empty) {
+  if (!c || !empty) return fail(PSG_ERR_ARG, "null argument");
+  std::lock_guard<std::mutex> l(c->mu);
+  auto it = c->ff.find(chl);
+  *empty = it == c->ff.end() || it->second.n == 0;
+  return PSG_OK;
+}
+
+namespace {
+int filter_of(psg_ctx* c, int chl, Filter** F) {
+  auto it = c->ff.find(chl);
+  if (it == c->ff.end() || it->second.n == 0)
+    return fail(PSG_ERR_ARG, "channel %d: frequency filter is empty (psg_freq_resize)", chl);
+  *F = &it->second;
+  return PSG_OK;
+}
+}  // namespace
+
+int psg_freq_insert_dev(psg_ctx* c, int chl, const uint64_t* keys, const uint32_t* counts,
+                        size_t n, void* stream) {
+  if (!c || (n && (!keys || !counts))) return fail(PSG_ERR_ARG, "null argument");
+  std::lock_guard<std::mutex> l(c->mu);
+  Filter* F;
+  if (int rc = filter_of(c, chl, &F)) return rc;
+  HIP_TRY(psg::launch_cm_insert(keys, counts, n, F->d_table, F->n, F->k, (hipStream_t)stream));
+  return PSG_OK;
+}
+
+size_t psg_freq_query_scratch_bytes(size_t n) { return psg::cm_query_scratch_bytes(n); }
+
+int psg_freq_query_dev(psg_ctx* c, int chl, const uint64_t* keys, size_t n, int freq,
+                       uint64_t* out, unsigned long long* nout, void* scratch, void* stream) {
+  if (!c || !nout || !scratch || (n && (!keys || !out))) return fail(PSG_ERR_ARG, "null argument");
+  if (freq >= 255) return fail(PSG_ERR_ARG, "freqency %d >= kuint8max", freq);  // :29
+  std::lock_guard<std::mutex> l(c->mu);
+  Filter* F;
+  if (int rc = filter_of(c, chl, &F)) return rc;
+  HIP_TRY(psg::launch_cm_query(keys, n, F->d_table, F->n, F->k, freq, out, nout, scratch,
+                               (hipStream_t)stream));
+  return PSG_OK;
+}
+
+int psg_freq_insert(psg_ctx* c, int chl, const uint64_t* keys, const uint32_t* counts,
+                    size_t n) {
+  if (!c || (n && (!keys || !counts))) return fail(PSG_ERR_ARG, "null argument");
+  std::lock_guard<std::mutex> l(c->mu);
+  Filter* F;
+  if (int rc = filter_of(c, chl, &F)) return rc;
+  if (n == 0) return PSG_OK;
+  if (int rc = set_dev(c->device)) return rc;
+  // one staging block for keys + counts, back to the pool after the kernel
+  const size_t kb = align_up(8 * n, 256), b = kb + 4 * n;
+  void* blk = nullptr;
+  if (int rc = c->dev_get(b, &blk, c->copy)) return rc;
+  int rc = c->h2d(blk, keys, 8 * n);
+  if (rc == PSG_OK) rc = c->h2d((char*)blk + kb, counts, 4 * n);
+  if (rc == PSG_OK) rc = c->join_copy();
+  if (rc == PSG_OK) {
+    hipError_t e = psg::launch_cm_insert((const uint64_t*)blk, (const uint32_t*)((char*)blk + kb),
+                                         n, F->d_table, F->n, F->k, c->stream);
+    if (e != hipSuccess) rc = fail(PSG_ERR_DEVICE, "freq insert: %s", hipGetErrorString(e));
+  }
+  c->dev_put(blk, b);
+  const int rf = c->h2d_finish();
+  return rc ? rc : rf;
+}
+
+int psg_freq_query(psg_ctx* c, int chl, const uint64_t* keys, size_t n, int freq, uint64_t* out,
+                   size_t* nout) {
+  if (!c || !nout || (n && (!keys || !out))) return fail(PSG_ERR_ARG, "null argument");
+  if (freq >= 255) return fail(PSG_ERR_ARG, "freqency %d >= kuint8max", freq);
+  std::lock_guard<std::mutex> l(c->mu);
+  Filter* F;
+  if (int rc = filter_of(c, chl, &F)) return rc;
+  *nout = 0;
+  if (n == 0) return PSG_OK;
+  if (int rc = set_dev(c->device)) return rc;
+  const size_t kb = align_up(8 * n, 256), sb = psg::cm_query_scratch_bytes(n);
+  if (int rc = c->ensure_scratch(2 * kb + sb)) return rc;
+  uint64_t* d_keys = (uint64_t*)c->scratch;
+  uint64_t* d_out = (uint64_t*)((char*)c->scratch + kb);
+  void* d_s = (char*)c->scratch + 2 * kb;
+  if (int rc = c->h2d(d_keys, keys, 8 * n)) return rc;
+  if (int rc = c->join_copy()) return rc;
+  HIP_TRY(psg::launch_cm_query(d_keys, n, F->d_table, F->n, F->k, freq, d_out, c->d_small + 7,
+                               d_s, c->stream));
+  HIP_TRY(hipMemcpyAsync(c->h_small + 7, c->d_small + 7, 8, hipMemcpyDeviceToHost, c->stream));
+  HIP_TRY(hipStreamSynchronize(c->stream));
+  const size_t m = (size_t)c->h_small[7];
+  if (m) HIP_TRY(hipMemcpy(out, d_out, 8 * m, hipMemcpyDeviceToHost));
+  *nout = m;
+  return c->h2d_finish();
+}
+
+int psg_freq_table(psg_ctx* c, int chl, uint8_t* out, size_t n) {
+  if (!c || (n && !out)) return fail(PSG_ERR_ARG, "null argument");
+  std::lock_guard<std::mutex> l(c->mu);
+  Filter* F;
+  if (int rc = filter_of(c, chl, &F)) return rc;
+  if (n > F->n) return fail(PSG_ERR_ARG, "table copy of %zu > %u counters", n, F->n);
+  if (int rc = set_dev(c->device)) return rc;
+  std::vector<uint32_t> t(n);
+  HIP_TRY(hipMemcpyAsync(t.data(), F->d_table, 4 * n, hipMemcpyDeviceToHost, c->stream));
+  HIP_TRY(hipStreamSynchronize(c->stream));
+  for (size_t i = 0; i < n; ++i) out[i] = (uint8_t)t[i];
   return PSG_OK;
 }
 

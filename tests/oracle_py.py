@@ -49,6 +49,11 @@ def orc() -> C.CDLL:
                                             _psz, _psz, _psz]),
             "orc_murmur3_x64_128": (None, [_p, C.c_int, C.c_uint32, _p]),
             "orc_shuffle_keys": (None, [_p, _sz, C.c_uint32, _p]),
+            "orc_darling_update_weight": (None, [_p, _p, _p, _sz, _sz, _p, _p, C.c_double,
+                                                 C.c_double, C.c_double, C.c_double, _p]),
+            "orc_cm_insert": (None, [_p, C.c_uint32, C.c_int, _p, _p, _sz]),
+            "orc_cm_query": (C.c_uint8, [_p, C.c_uint32, C.c_int, _u64]),
+            "orc_ff_query": (_sz, [_p, C.c_uint32, C.c_int, _p, _sz, C.c_int, _p]),
             "orc_crc32c_extend": (C.c_uint32, [C.c_uint32, _p, _sz]),
             "orc_crc32c_mask": (C.c_uint32, [C.c_uint32]),
             "orc_crc32c_unmask": (C.c_uint32, [C.c_uint32]),
@@ -197,3 +202,37 @@ def ref_crc32c(data: bytes, init: int = 0) -> int:
     L.ref_crc32c_extend.restype = C.c_uint
     L.ref_crc32c_extend.argtypes = [C.c_uint, C.c_char_p, _sz]
     return int(L.ref_crc32c_extend(init, data, len(data)))
+
+
+# ---- Darling::updateWeight (linear_method/darling.cc:437-477) ------------
+def darling_update_weight(value, delta, active, lo, G, U, eta, lam, kkt, delta_max,
+                          violation=0.0):
+    """In-place on copies: returns (value, delta, active, violation)."""
+    value = np.array(value, np.float64)
+    delta = np.array(delta, np.float64)
+    active = np.array(active, np.uint8)
+    G = np.ascontiguousarray(G, np.float64)
+    U = np.ascontiguousarray(U, np.float64)
+    vio = np.array([violation], np.float64)
+    orc().orc_darling_update_weight(_a(value), _a(delta), _a(active), lo, G.size, _a(G), _a(U),
+                                    eta, lam, kkt, delta_max, _a(vio))
+    return value, delta, active, float(vio[0])
+
+
+# ---- CountMin<uint64,uint8> / FreqencyFilter (countmin.h, frequency_filter.h)
+def cm_resize(n, k):
+    """CountMin::resize (countmin.h:14-19): (table, n_, k_)."""
+    n = max(int(n), 64)
+    return np.zeros(n, np.uint8), n, min(30, max(1, int(k)))
+
+
+def cm_insert(table, n, k, keys, counts):
+    keys, counts = u64(keys), np.ascontiguousarray(counts, np.uint32)
+    orc().orc_cm_insert(_a(table), n, k, _a(keys), _a(counts), keys.size)
+
+
+def ff_query(table, n, k, keys, freq):
+    keys = u64(keys)
+    out = np.empty(max(1, keys.size), np.uint64)
+    m = orc().orc_ff_query(_a(table), n, k, _a(keys), keys.size, freq, _a(out))
+    return out[:m].copy()
