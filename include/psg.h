@@ -199,6 +199,37 @@ int psg_key_union_dev(const uint64_t* a, uint64_t na, const uint64_t* b,
                       uint64_t nb, uint64_t* out, uint64_t* nout,
                       void* stream);
 
+/* ------------------------------------------------------------------ */
+/* Shard exchange over RCCL ("unsliced" ingress)          */
+/* ------------------------------------------------------------------ */
+/* One communicator per rank and GPU (RCCL = NCCL API over xGMI).  Rank 0
+ * makes the id and the caller broadcasts it (any channel). */
+#define PSG_COMM_ID_BYTES 128
+typedef struct psg_comm psg_comm;
+int psg_comm_unique_id(uint8_t* id);
+int psg_comm_init(int device, int nranks, const uint8_t* id, int rank,
+                  psg_comm** out);
+int psg_comm_destroy(psg_comm* comm);
+
+/* RNode::submit's slice-and-send (remote_node.cc:39-60: KVVector::slice ->
+ * sliceKeyOrderedMsg, message.h:89-123) for a batch of npush sorted
+ * device-resident pushes held by this rank, at the server ranges
+ * Range<uint64>::all().evenDivide(nranks, s) (linear_method.cc:137-145).
+ * Every rank passes the same npush, dtype and m.  Create (synchronous,
+ * collective): cut positions, piece counts exchanged, buffers sized.
+ * Run (collective, enqueued on `stream`): pack + one grouped send/recv per
+ * peer.  Afterwards psg_exchange_recv gives the received keys / m value
+ * arrays (device) and recv_cnt[src * npush + p] (host, may be NULL): the
+ * piece of push p of rank src starts after all earlier (src, p) pieces. */
+typedef struct psg_exchange psg_exchange;
+int psg_exchange_create(psg_comm* comm, int dtype, int m, int npush,
+                        const uint64_t* const* push_keys, const uint64_t* push_n,
+                        const void* const* push_vals, psg_exchange** out);
+int psg_exchange_run(psg_exchange* x, void* stream);
+int psg_exchange_recv(psg_exchange* x, const uint64_t** keys, void** vals,
+                      uint64_t* nrecv, uint64_t* recv_cnt, uint64_t* nsent);
+int psg_exchange_destroy(psg_exchange* x);
+
 /* Server shard boundaries: Range<uint64>::all().evenDivide(n, i)
  * (range.h:75-98, linear_method.cc:137-145); bounds[n+1]. */
 int psg_shard_bounds(size_t n, uint64_t* bounds);

@@ -111,6 +111,14 @@ SIGNATURES = {
     "psg_freq_query_scratch_bytes": (_sz, [_sz]),
     "psg_freq_query_dev": (C.c_int, [_p, C.c_int, _p, _sz, C.c_int, _p, _p, _p, _p]),
     "psg_freq_table": (C.c_int, [_p, C.c_int, _p, _sz]),
+    "psg_comm_unique_id": (C.c_int, [_p]),
+    "psg_comm_init": (C.c_int, [C.c_int, C.c_int, _p, C.c_int, C.POINTER(_p)]),
+    "psg_comm_destroy": (C.c_int, [_p]),
+    "psg_exchange_create": (C.c_int, [_p, C.c_int, C.c_int, C.c_int, _p, _p, _p,
+                                      C.POINTER(_p)]),
+    "psg_exchange_run": (C.c_int, [_p, _p]),
+    "psg_exchange_recv": (C.c_int, [_p, C.POINTER(_p), _p, _pu64, _p, _pu64]),
+    "psg_exchange_destroy": (C.c_int, [_p]),
     "psg_darling_init": (C.c_int, [_p, C.c_int, C.c_double]),
     "psg_darling_reset_active": (C.c_int, [_p, C.c_int]),
     "psg_darling_update": (C.c_int, [_p, C.c_int, C.c_int, _p, C.POINTER(C.c_double)]),

@@ -1,0 +1,368 @@
+// psg_exchange.hip -- re-homing of pushes to the key-range shards over RCCL
+// ("mode B" ingress): what RNode::submit does per push on the
+// worker side (src/system/remote_node.cc:39-60) -- KVVector::slice ->
+// sliceKeyOrderedMsg (src/system/message.h:89-123) at the server key ranges
+// Range<uint64>::all().evenDivide(nranks, s) (src/base/range.h:85-98,
+// linear_method.cc:137-145) and one message per server -- done for a batch
+// of device-resident pushes by one rank per GPU.
+//
+// Set-up (psg_exchange_create, synchronous): one wave per (push, boundary)
+// finds the cut positions (a sorted push's piece for shard s is the
+// contiguous run [lower_bound(b_s), lower_bound(b_s+1))); the piece counts
+// go to their shards with one grouped ncclSend/ncclRecv round; the send and
+// receive buffers are sized from them.  A step (psg_exchange_run, on a
+// stream, no host wait): one gather kernel packs every piece into
+// destination-major send buffers, then per peer one ncclSend/ncclRecv of
+// the keys and one per value array in a single group.  After a step,
+// shard `rank` holds, for each source rank src and push p, the piece at
+// recv offset off[src][p] with cnt[src][p] keys (the layout a psg_plan
+// job points at directly).
+#include <hip/hip_runtime.h>
+#include <rccl/rccl.h>
+
+#include <cstring>
+#include <vector>
+
+#include "psg_device.h"
+#include "psg_host.h"
+#include "psg_internal.h"
+
+using psg::fail;
+
+#define NCCL_TRY(expr)                                                           \
+  do {                                                                           \
+    ncclResult_t _r = (expr);                                                    \
+    if (_r != ncclSuccess)                                                       \
+      return fail(PSG_ERR_DEVICE, "%s: %s (%s:%d)", #expr, ncclGetErrorString(_r), \
+                  __FILE__, __LINE__);                                           \
+  } while (0)
+
+namespace {
+
+// pos[p * (S+1) + s] = lower_bound(push p, bounds[s]); one wave each
+__global__ __launch_bounds__(256) void cut_kernel(const uint64_t* const* __restrict__ keys,
+                                                  const uint64_t* __restrict__ n,
+                                                  const uint64_t* __restrict__ bounds, int S1,
+                                                  int P, uint64_t* __restrict__ pos) {
+  const int w = (int)((blockIdx.x * 256u + threadIdx.x) >> 6);
+  const int lane = threadIdx.x & 63;
+  if (w >= P * S1) return;
+  const int p = w / S1, s = w - p * S1;
+  // every separator, the last (2^64-1, the end of Range::all()) included:
+  // the reference's cut (message.h:96-99) leaves a key 2^64-1 in no shard
+  const uint64_t r = psg::dev::wave_search(keys[p], n[p], bounds[s], false, lane);
+  if (lane == 0) pos[w] = r;
+}
+
+// one piece of the send layout
+struct Piece {
+  uint64_t src;  // element offset inside push p
+  uint64_t dst;  // element offset in the send buffers
+  uint64_t len;
+  uint32_t p, pad;
+};
+
+// every piece into the destination-major send buffers: keys (8 B) and m
+// value arrays of `vb` bytes per element; a workgroup per 2048-element chunk
+__global__ __launch_bounds__(256) void pack_kernel(const Piece* __restrict__ pieces,
+                                                   const uint64_t* __restrict__ chunk_piece,
+                                                   uint64_t nchunks,
+                                                   const uint64_t* const* __restrict__ keys,
+                                                   const void* const* __restrict__ vals, int m,
+                                                   int vb, uint64_t* __restrict__ skeys,
+                                                   void* const* __restrict__ svals) {
+  constexpr uint64_t kChunk = 2048;
+  for (uint64_t c = blockIdx.x; c < nchunks; c += gridDim.x) {
+    const uint64_t e = chunk_piece[c];
+    const Piece pc = pieces[e >> 24];
+    const uint64_t c0 = (e & 0xffffffull) * kChunk;
+    const uint64_t len = pc.len - c0 < kChunk ? pc.len - c0 : kChunk;
+    const uint64_t* ks = keys[pc.p] + pc.src + c0;
+    uint64_t* kd = skeys + pc.dst + c0;
+    for (uint64_t i = threadIdx.x; i < len; i += 256) kd[i] = ks[i];
+    for (int a = 0; a < m; ++a) {
+      const char* vs = (const char*)vals[(size_t)pc.p * m + a] + (pc.src + c0) * vb;
+      char* vd = (char*)svals[a] + (pc.dst + c0) * vb;
+      if (vb == 4) {
+        for (uint64_t i = threadIdx.x; i < len; i += 256) ((uint32_t*)vd)[i] = ((const uint32_t*)vs)[i];
+      } else {
+        for (uint64_t i = threadIdx.x; i < len; i += 256) ((uint64_t*)vd)[i] = ((const uint64_t*)vs)[i];
+      }
+    }
+  }
+}
+
+}  // namespace
+
+struct psg_comm {
+  ncclComm_t nccl = nullptr;
+  int device = 0, nranks = 1, rank = 0;
+};
+
+struct psg_exchange {
+  psg_comm* comm = nullptr;
+  int dtype = 0, m = 1, P = 0, S = 1;
+  std::vector<uint64_t> send_cnt;   // [s][p]
+  std::vector<uint64_t> recv_cnt;   // [src][p]
+  std::vector<uint64_t> send_tot, send_off, recv_tot, recv_off;  // per peer
+  void* dev = nullptr;              // one device block for everything below
+  uint64_t* skeys = nullptr;
+  void* svals[psg::kMaxM] = {};
+  uint64_t* rkeys = nullptr;
+  void* rvals[psg::kMaxM] = {};
+  const uint64_t* const* d_keys = nullptr;
+  const void* const* d_vals = nullptr;
+  void* const* d_svals = nullptr;
+  Piece* d_pieces = nullptr;
+  uint64_t* d_chunks = nullptr;
+  uint64_t nchunks = 0, nsend = 0, nrecv = 0;
+};
+
+namespace {
+size_t al(size_t x) { return (x + 255) / 256 * 256; }
+}  // namespace
+
+extern "C" {
+
+int psg_comm_unique_id(uint8_t* id) {
+  if (!id) return fail(PSG_ERR_ARG, "null id");
+  ncclUniqueId u;
+  NCCL_TRY(ncclGetUniqueId(&u));
+  memcpy(id, u.internal, PSG_COMM_ID_BYTES);
+  return PSG_OK;
+}
+
+int psg_comm_init(int device, int nranks, const uint8_t* id, int rank, psg_comm** out) {
+  if (!id || !out || nranks < 1 || rank < 0 || rank >= nranks)
+    return fail(PSG_ERR_ARG, "bad communicator arguments");
+  HIP_TRY(hipSetDevice(device));
+  ncclUniqueId u;
+  memcpy(u.internal, id, PSG_COMM_ID_BYTES);
+  psg_comm* c = new psg_comm();
+  c->device = device;
+  c->nranks = nranks;
+  c->rank = rank;
+  ncclResult_t r = ncclCommInitRank(&c->nccl, nranks, u, rank);
+  if (r != ncclSuccess) {
+    delete c;
+    return fail(PSG_ERR_DEVICE, "ncclCommInitRank: %s", ncclGetErrorString(r));
+  }
+  *out = c;
+  return PSG_OK;
+}
+
+int psg_comm_destroy(psg_comm* c) {
+  if (!c) return PSG_OK;
+  if (c->nccl) (void)ncclCommDestroy(c->nccl);
+  delete c;
+  return PSG_OK;
+}
+
+int psg_exchange_create(psg_comm* comm, int dtype, int m, int npush,
+                        const uint64_t* const* push_keys, const uint64_t* push_n,
+                        const void* const* push_vals, psg_exchange** out) {
+  if (!comm || !out || npush < 0 || (npush && (!push_keys || !push_n || !push_vals)))
+    return fail(PSG_ERR_ARG, "null argument");
+  if (dtype != PSG_F32 && dtype != PSG_F64) return fail(PSG_ERR_ARG, "dtype %d", dtype);
+  if (m < 1 || m > PSG_MAX_VALUE_ARRAYS) return fail(PSG_ERR_ARG, "m=%d", m);
+  HIP_TRY(hipSetDevice(comm->device));
+  const int S = comm->nranks, P = npush, S1 = S + 1;
+  const int vb = dtype == PSG_F32 ? 4 : 8;
+  std::vector<uint64_t> bounds(S1);
+  if (int rc = psg_shard_bounds((size_t)S, bounds.data())) return rc;
+  hipStream_t st;
+  HIP_TRY(hipStreamCreateWithFlags(&st, hipStreamNonBlocking));
+  // ---- set-up block: bounds, push tables, cut positions, counts
+  const size_t o_b = 0, o_k = al(8 * S1), o_n = o_k + al(8 * P), o_pos = o_n + al(8 * P),
+               o_sc = o_pos + al(8 * (size_t)P * S1), o_rc = o_sc + al(8 * (size_t)P * S),
+               tot = o_rc + al(8 * (size_t)P * S);
+  char* setup = nullptr;
+  if (hipMalloc((void**)&setup, tot) != hipSuccess) {
+    (void)hipStreamDestroy(st);
+    return fail(PSG_ERR_OOM, "exchange set-up: %zu bytes", tot);
+  }
+  std::vector<uint64_t> pos((size_t)P * S1);
+  psg_exchange* x = new psg_exchange();
+  x->comm = comm;
+  x->dtype = dtype;
+  x->m = m;
+  x->P = P;
+  x->S = S;
+  auto done = [&](int r) {
+    (void)hipStreamSynchronize(st);
+    (void)hipFree(setup);
+    (void)hipStreamDestroy(st);
+    if (r != PSG_OK) psg_exchange_destroy(x);
+    return r;
+  };
+#define X_TRY(expr)                                                                  \
+  do {                                                                               \
+    hipError_t _e = (expr);                                                          \
+    if (_e != hipSuccess)                                                            \
+      return done(fail(PSG_ERR_DEVICE, "%s: %s", #expr, hipGetErrorString(_e)));   \
+  } while (0)
+  if (P) {
+    X_TRY(hipMemcpyAsync(setup + o_b, bounds.data(), 8 * S1, hipMemcpyHostToDevice, st));
+    X_TRY(hipMemcpyAsync(setup + o_k, push_keys, 8 * (size_t)P, hipMemcpyHostToDevice, st));
+    X_TRY(hipMemcpyAsync(setup + o_n, push_n, 8 * (size_t)P, hipMemcpyHostToDevice, st));
+    const uint64_t waves = (uint64_t)P * S1;
+    hipLaunchKernelGGL(cut_kernel, dim3((uint32_t)((waves + 3) / 4)), dim3(256), 0, st,
+                       (const uint64_t* const*)(setup + o_k), (const uint64_t*)(setup + o_n),
+                       (const uint64_t*)(setup + o_b), S1, P, (uint64_t*)(setup + o_pos));
+    X_TRY(hipGetLastError());
+    X_TRY(hipMemcpyAsync(pos.data(), setup + o_pos, 8 * pos.size(), hipMemcpyDeviceToHost, st));
+    X_TRY(hipStreamSynchronize(st));
+  }
+  // send counts [s][p]; pieces in destination-major, push order
+  x->send_cnt.assign((size_t)S * P, 0);
+  x->send_tot.assign(S, 0);
+  x->send_off.assign(S, 0);
+  std::vector<Piece> pieces;
+  std::vector<uint64_t> chunks;
+  uint64_t off = 0;
+  for (int s = 0; s < S; ++s) {
+    x->send_off[s] = off;
+    for (int p = 0; p < P; ++p) {
+      const uint64_t a = pos[(size_t)p * S1 + s], b = pos[(size_t)p * S1 + s + 1];
+      const uint64_t c = b > a ? b - a : 0;
+      x->send_cnt[(size_t)s * P + p] = c;
+      if (c) {
+        if (pieces.size() >= (1u << 24)) return done(fail(PSG_ERR_ARG, "too many pieces"));
+        for (uint64_t q = 0; q * 2048 < c; ++q) chunks.push_back((uint64_t)pieces.size() << 24 | q);
+        pieces.push_back(Piece{a, off, c, (uint32_t)p, 0});
+      }
+      off += c;
+    }
+    x->send_tot[s] = off - x->send_off[s];
+  }
+  x->nsend = off;
+  // counts to their shards: P words to and from every peer
+  X_TRY(hipMemcpyAsync(setup + o_sc, x->send_cnt.data(), 8 * x->send_cnt.size(),
+                       hipMemcpyHostToDevice, st));
+  {
+    ncclResult_t r = ncclGroupStart();
+    for (int s = 0; r == ncclSuccess && s < S && P; ++s) {
+      r = ncclSend(setup + o_sc + 8 * (size_t)s * P, P, ncclUint64, s, comm->nccl, st);
+      if (r == ncclSuccess)
+        r = ncclRecv(setup + o_rc + 8 * (size_t)s * P, P, ncclUint64, s, comm->nccl, st);
+    }
+    const ncclResult_t r2 = ncclGroupEnd();
+    if (r != ncclSuccess || r2 != ncclSuccess)
+      return done(fail(PSG_ERR_DEVICE, "count exchange: %s",
+                       ncclGetErrorString(r != ncclSuccess ? r : r2)));
+  }
+  x->recv_cnt.assign((size_t)S * P, 0);
+  if (P)
+    X_TRY(hipMemcpyAsync(x->recv_cnt.data(), setup + o_rc, 8 * x->recv_cnt.size(),
+                         hipMemcpyDeviceToHost, st));
+  X_TRY(hipStreamSynchronize(st));
+  x->recv_tot.assign(S, 0);
+  x->recv_off.assign(S, 0);
+  uint64_t roff = 0;
+  for (int s = 0; s < S; ++s) {
+    x->recv_off[s] = roff;
+    for (int p = 0; p < P; ++p) roff += x->recv_cnt[(size_t)s * P + p];
+    x->recv_tot[s] = roff - x->recv_off[s];
+  }
+  x->nrecv = roff;
+  x->nchunks = chunks.size();
+  // ---- the step's device block: send / receive buffers and the tables
+  size_t b = 0;
+  const size_t b_sk = b; b += al(8 * x->nsend);
+  size_t b_sv[psg::kMaxM];
+  for (int a = 0; a < m; ++a) { b_sv[a] = b; b += al((size_t)vb * x->nsend); }
+  const size_t b_rk = b; b += al(8 * x->nrecv);
+  size_t b_rv[psg::kMaxM];
+  for (int a = 0; a < m; ++a) { b_rv[a] = b; b += al((size_t)vb * x->nrecv); }
+  const size_t b_keys = b; b += al(8 * (size_t)P);
+  const size_t b_vals = b; b += al(8 * (size_t)P * m);
+  const size_t b_svp = b; b += al(8 * (size_t)m);
+  const size_t b_pc = b; b += al(sizeof(Piece) * pieces.size());
+  const size_t b_ch = b; b += al(8 * chunks.size());
+  X_TRY(hipMalloc(&x->dev, b ? b : 256));
+  char* d = (char*)x->dev;
+  x->skeys = (uint64_t*)(d + b_sk);
+  x->rkeys = (uint64_t*)(d + b_rk);
+  std::vector<uint64_t> svp(m);
+  for (int a = 0; a < m; ++a) {
+    x->svals[a] = d + b_sv[a];
+    x->rvals[a] = d + b_rv[a];
+    svp[a] = (uint64_t)x->svals[a];
+  }
+  x->d_keys = (const uint64_t* const*)(d + b_keys);
+  x->d_vals = (const void* const*)(d + b_vals);
+  x->d_svals = (void* const*)(d + b_svp);
+  x->d_pieces = (Piece*)(d + b_pc);
+  x->d_chunks = (uint64_t*)(d + b_ch);
+  if (P) {
+    X_TRY(hipMemcpyAsync(d + b_keys, push_keys, 8 * (size_t)P, hipMemcpyHostToDevice, st));
+    X_TRY(hipMemcpyAsync(d + b_vals, push_vals, 8 * (size_t)P * m, hipMemcpyHostToDevice, st));
+  }
+  X_TRY(hipMemcpyAsync(d + b_svp, svp.data(), 8 * (size_t)m, hipMemcpyHostToDevice, st));
+  if (!pieces.empty())
+    X_TRY(hipMemcpyAsync(d + b_pc, pieces.data(), sizeof(Piece) * pieces.size(),
+                         hipMemcpyHostToDevice, st));
+  if (!chunks.empty())
+    X_TRY(hipMemcpyAsync(d + b_ch, chunks.data(), 8 * chunks.size(), hipMemcpyHostToDevice, st));
+#undef X_TRY
+  *out = x;
+  return done(PSG_OK);
+}
+
+int psg_exchange_run(psg_exchange* x, void* stream) {
+  if (!x) return fail(PSG_ERR_ARG, "null exchange");
+  HIP_TRY(hipSetDevice(x->comm->device));
+  hipStream_t st = (hipStream_t)stream;
+  const int vb = x->dtype == PSG_F32 ? 4 : 8;
+  if (x->nchunks) {
+    const uint64_t blocks = x->nchunks < 4096 ? x->nchunks : 4096;
+    hipLaunchKernelGGL(pack_kernel, dim3((uint32_t)blocks), dim3(256), 0, st, x->d_pieces,
+                       x->d_chunks, x->nchunks, x->d_keys, x->d_vals, x->m, vb, x->skeys,
+                       x->d_svals);
+    HIP_TRY(hipGetLastError());
+  }
+  ncclResult_t r = ncclGroupStart();
+  for (int s = 0; r == ncclSuccess && s < x->S; ++s) {
+    if (x->send_tot[s]) {
+      r = ncclSend(x->skeys + x->send_off[s], x->send_tot[s], ncclUint64, s, x->comm->nccl, st);
+      for (int a = 0; r == ncclSuccess && a < x->m; ++a)
+        r = ncclSend((char*)x->svals[a] + x->send_off[s] * vb, x->send_tot[s] * vb, ncclUint8, s,
+                     x->comm->nccl, st);
+    }
+    if (r == ncclSuccess && x->recv_tot[s]) {
+      r = ncclRecv(x->rkeys + x->recv_off[s], x->recv_tot[s], ncclUint64, s, x->comm->nccl, st);
+      for (int a = 0; r == ncclSuccess && a < x->m; ++a)
+        r = ncclRecv((char*)x->rvals[a] + x->recv_off[s] * vb, x->recv_tot[s] * vb, ncclUint8, s,
+                     x->comm->nccl, st);
+    }
+  }
+  const ncclResult_t r2 = ncclGroupEnd();
+  if (r != ncclSuccess || r2 != ncclSuccess)
+    return fail(PSG_ERR_DEVICE, "payload exchange: %s",
+                ncclGetErrorString(r != ncclSuccess ? r : r2));
+  return PSG_OK;
+}
+
+int psg_exchange_recv(psg_exchange* x, const uint64_t** keys, void** vals, uint64_t* nrecv,
+                      uint64_t* recv_cnt, uint64_t* sent) {
+  if (!x) return fail(PSG_ERR_ARG, "null exchange");
+  if (keys) *keys = x->rkeys;
+  for (int a = 0; vals && a < x->m; ++a) vals[a] = x->rvals[a];
+  if (nrecv) *nrecv = x->nrecv;
+  if (recv_cnt) memcpy(recv_cnt, x->recv_cnt.data(), 8 * x->recv_cnt.size());
+  if (sent) *sent = x->nsend;
+  return PSG_OK;
+}
+
+int psg_exchange_destroy(psg_exchange* x) {
+  if (!x) return PSG_OK;
+  if (x->dev) {
+    (void)hipSetDevice(x->comm->device);
+    (void)hipDeviceSynchronize();
+    (void)hipFree(x->dev);
+  }
+  delete x;
+  return PSG_OK;
+}
+
+}  // extern "C"

@@ -24,15 +24,16 @@
 #include <vector>
 
 #include "../../include/psg.h"
+#include "psg_host.h"
 #include "psg_internal.h"
 
 using psg::JobDev;
 
 namespace {
-
 thread_local std::string g_err;
+}  // namespace
 
-int fail(int code, const char* fmt, ...) {
+int psg::fail(int code, const char* fmt, ...) {
   char buf[512];
   va_list ap;
   va_start(ap, fmt);
@@ -42,14 +43,9 @@ int fail(int code, const char* fmt, ...) {
   return code;
 }
 
-#define HIP_TRY(expr)                                                        \
-  do {                                                                       \
-    hipError_t _e = (expr);                                                  \
-    if (_e != hipSuccess)                                                    \
-      return fail(_e == hipErrorOutOfMemory ? PSG_ERR_OOM : PSG_ERR_DEVICE,  \
-                  "%s: %s (%s:%d)", #expr, hipGetErrorString(_e), __FILE__,  \
-                  __LINE__);                                                 \
-  } while (0)
+namespace {
+
+using psg::fail;
 
 size_t vsize(int dtype) { return dtype == PSG_F32 ? 4 : 8; }
 

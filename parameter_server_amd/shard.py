@@ -8,9 +8,12 @@ collective.
 
 Mode B ("unsliced"): every rank receives whole pushes; each push is cut at
 the shard boundaries (the same lower_bound rule, message.h:96-99) and the
-pieces are re-homed with one all-to-all of counts and one of payload
-(RCCL over xGMI on GPUs, gloo in the CPU tests), after which every rank
-merges the pieces it owns.
+pieces are re-homed with one exchange of counts and one of payload, after
+which every rank merges the pieces it owns.  On GPUs the exchange is the
+C ABI's psg_exchange_* over a psg_comm (RCCL over xGMI, hand-written cut
+and pack kernels; :class:`RcclExchange`); the torch.distributed forms below
+(:func:`exchange_pieces`, :class:`UnslicedExchange` on CPU tensors) restate
+the same layout for the gloo tests of the partition/exchange logic.
 """
 from __future__ import annotations
 
@@ -120,6 +123,24 @@ class UnslicedExchange:
         J, P = len(aggs), len(aggs[0])
         m = len(aggs[0][0][1])
         vdt = aggs[0][0][1][0].dtype
+        self.x = None
+        if torch.device(device).type == "cuda":
+            # GPUs: the C ABI's RCCL exchange (cut + pack kernels, grouped
+            # send/recv per peer); bounds are evenDivide(world) there too
+            from ._lib import PSG_F32, PSG_F64
+            dev = torch.device(device)
+            rank = dist.get_rank() if dist is not None else 0
+            self._dev_pushes = [(torch.from_numpy(k.view(np.int64)).to(dev),
+                                 [torch.from_numpy(np.ascontiguousarray(v)).to(dev) for v in vs])
+                                for agg in aggs for k, vs in agg]
+            self.comm = make_comm(dev.index or 0, rank, world, dist)
+            self.x = RcclExchange(self.comm, self._dev_pushes, world,
+                                  PSG_F32 if vdt == np.float32 else PSG_F64)
+            self.world, self.J, self.P, self.m = world, J, P, m
+            self.recv_cnt = self.x.recv_cnt.reshape(world, J, P)
+            self.recv_off = self.x.recv_off.reshape(world, J, P)
+            self.sent_bytes = int(self.x.nsent) * (8 + m * np.dtype(vdt).itemsize)
+            return
         flat_k, flat_v, perm_parts = [], [[] for _ in range(m)], []
         cnt = np.zeros((world, J, P), np.int64)  # send counts [dest, j, p]
         base = 0
@@ -168,6 +189,9 @@ class UnslicedExchange:
     def run(self):
         """One step's re-homing (enqueued on the current stream)."""
         import torch
+        if self.x is not None:
+            self.x.run(torch.cuda.current_stream().cuda_stream)
+            return
         if self.world == 1:  # one shard: the pushes are already in send order
             pairs = [(self.recv_keys, self.flat_keys)] + list(zip(self.recv_vals, self.flat_vals))
         else:
@@ -187,3 +211,87 @@ class UnslicedExchange:
         [(offset, count)] into recv_keys / recv_vals (empty pieces dropped)."""
         return [(int(self.recv_off[s, j, p]), int(self.recv_cnt[s, j, p]))
                 for s in range(self.world) for p in range(self.P) if self.recv_cnt[s, j, p]]
+
+
+# --------------------------------------------------------------------------
+# RCCL through the C ABI (include/psg.h: psg_comm_*, psg_exchange_*)
+# --------------------------------------------------------------------------
+def make_comm(device: int, rank: int = 0, world: int = 1, dist=None):
+    """A psg_comm for this rank: rank 0 makes the RCCL unique id and `dist`
+    (any initialised torch.distributed group) carries it to the others."""
+    import ctypes as C
+    from . import _lib
+    L = _lib.lib()
+    idb = (C.c_uint8 * 128)()
+    if rank == 0:
+        _lib.check(L.psg_comm_unique_id(idb))
+    if world > 1:
+        obj = [bytes(idb)]
+        dist.broadcast_object_list(obj, src=0)
+        C.memmove(idb, obj[0], 128)
+    h = C.c_void_p()
+    _lib.check(L.psg_comm_init(device, world, idb, rank, C.byref(h)))
+    return h
+
+
+def destroy_comm(h) -> None:
+    from . import _lib
+    _lib.lib().psg_comm_destroy(h)
+
+
+class RcclExchange:
+    """Mode B re-homing of this rank's device-resident pushes through
+    psg_exchange_* (one grouped RCCL send/recv per peer per step).
+
+    pushes: [(keys, [vals] * m)] torch CUDA tensors (keys int64 holding the
+    uint64 keys, sorted).  After run(), shard `rank` holds for each source
+    src and push p the piece (offset, count) = pieces()[src][p] in
+    recv_keys_ptr / recv_vals_ptr (device addresses)."""
+
+    def __init__(self, comm, pushes, world: int, dtype: int):
+        import ctypes as C
+        from . import _lib
+        self._L = _lib.lib()
+        self.world, self.P = world, len(pushes)
+        self.m = len(pushes[0][1]) if pushes else 1
+        self._keep = pushes
+        kp = (C.c_void_p * max(1, self.P))(*[k.data_ptr() for k, _ in pushes])
+        ns = (C.c_uint64 * max(1, self.P))(*[k.numel() for k, _ in pushes])
+        vp = (C.c_void_p * max(1, self.P * self.m))(*[v.data_ptr() for _, vs in pushes
+                                                      for v in vs])
+        h = C.c_void_p()
+        _lib.check(self._L.psg_exchange_create(comm, dtype, self.m, self.P, kp, ns, vp,
+                                               C.byref(h)))
+        self._h = h
+        keys = C.c_void_p()
+        vals = (C.c_void_p * self.m)()
+        nrecv, nsent = C.c_uint64(), C.c_uint64()
+        cnt = np.zeros(max(1, world * self.P), np.uint64)
+        _lib.check(self._L.psg_exchange_recv(h, C.byref(keys), vals, C.byref(nrecv),
+                                             cnt.ctypes.data, C.byref(nsent)))
+        self.recv_keys_ptr = keys.value
+        self.recv_vals_ptr = [vals[i] for i in range(self.m)]
+        self.nrecv, self.nsent = nrecv.value, nsent.value
+        self.recv_cnt = cnt[: world * self.P].reshape(world, self.P).astype(np.int64)
+        flat = self.recv_cnt.reshape(-1)
+        self.recv_off = (np.cumsum(flat) - flat).reshape(world, self.P)
+
+    def run(self, stream=None) -> None:
+        from . import _lib
+        _lib.check(self._L.psg_exchange_run(self._h, stream))
+
+    def pieces(self):
+        """[(offset, count)] per (source, push), arrival order, empties dropped."""
+        return [(int(self.recv_off[s, p]), int(self.recv_cnt[s, p]))
+                for s in range(self.world) for p in range(self.P) if self.recv_cnt[s, p]]
+
+    def close(self) -> None:
+        if getattr(self, "_h", None):
+            self._L.psg_exchange_destroy(self._h)
+            self._h = None
+
+    def __del__(self):  # pragma: no cover
+        try:
+            self.close()
+        except Exception:
+            pass
