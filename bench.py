@@ -389,7 +389,10 @@ def end_to_end(inst, device, reps=7):
       pinned_hold    pinned, PSG_HOLD_BUFFERS (buffers held until received,
                      as a MessagePtr holds its SArrays): no wait per push;
       pinned_cached  pinned_hold, and each worker's keys come from the key
-                     cache (RNode::cacheKeyRecver): only values cross PCIe.
+                     cache (RNode::cacheKeyRecver): only values cross PCIe;
+      darling_fused  the Darling server step on the same keys: f64 (G, U)
+                     pushes from the key cache, then the fused updateWeight
+                     on the device (psg_darling_update): no aggregate D2H.
     Reported beside `value`, never as it."""
     import ctypes as C
     import torch
@@ -434,6 +437,23 @@ def end_to_end(inst, device, reps=7):
         _lib.check(rc)
         t = float(np.median(ms[1:])) * 1e-3
         out[mode] = {"value": kv / t, "ms_per_aggregate": t * 1e3}
+    # the Darling server step on the same keys (f64 G and U from pinned
+    # memory, keys from the key cache, fused updateWeight: nothing D2H)
+    rng = np.random.default_rng(77)
+    GU = [(torch.from_numpy(rng.standard_normal(k.size)).pin_memory().numpy(),
+           torch.from_numpy(rng.random(k.size)).pin_memory().numpy()) for k, _ in pushes]
+    kp = (C.c_void_p * npush)(*[k.ctypes.data for k, _ in pushes])
+    ns = (C.c_size_t * npush)(*[k.size for k, _ in pushes])
+    gp = (C.c_void_p * npush)(*[g.ctypes.data for g, _ in GU])
+    up = (C.c_void_p * npush)(*[u.ctypes.data for _, u in GU])
+    ms = np.zeros(reps + 1, np.float64)
+    vio = C.c_double()
+    _lib.check(E.psg_e2e_darling(C.c_int(device), C.c_uint(_lib.PSG_HOLD_BUFFERS),
+                                 C.c_void_p(D.ctypes.data), C.c_size_t(D.size), C.c_int(npush),
+                                 kp, ns, gp, up, C.c_void_p(sigs.ctypes.data), C.c_int(reps + 1),
+                                 C.c_void_p(ms.ctypes.data), C.byref(vio)))
+    t = float(np.median(ms[1:])) * 1e-3
+    out["darling_fused"] = {"value": kv / t, "ms_per_aggregate": t * 1e3, "dtype": "f64", "m": 2}
     # the link itself: pinned <-> device copies of 64 MB (torch, same streams)
     link = {}
     hbuf = torch.empty(64 << 20, dtype=torch.uint8, pin_memory=True)
@@ -451,8 +471,9 @@ def end_to_end(inst, device, reps=7):
     del hbuf, dbuf
     # bytes that must cross the link per aggregate in each mode
     vb, kb, ob = 4 * kv, 8 * kv, 4 * D.size
-    for mode, b in (("pageable", kb + vb + ob), ("pinned", kb + vb + ob),
-                    ("pinned_hold", kb + vb + ob), ("pinned_cached", vb + ob)):
+    for mode, b, ob in (("pageable", kb + vb + ob, ob), ("pinned", kb + vb + ob, ob),
+                        ("pinned_hold", kb + vb + ob, ob), ("pinned_cached", vb + ob, ob),
+                        ("darling_fused", 16 * kv, 0)):
         bound = (b - ob) / (link["h2d_GBps"] * 1e9) + ob / (link["d2h_GBps"] * 1e9)
         out[mode]["link_bytes"] = b
         out[mode]["frac_of_link"] = bound * 1e3 / out[mode]["ms_per_aggregate"]
