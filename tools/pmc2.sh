@@ -8,7 +8,7 @@ export TMPDIR=/tmp
 OUT=$1
 BARGS=${2:-}
 mkdir -p $OUT
-BENCH="python3 bench.py --profile-steps 1 --steps 3 --warmup 1 $BARGS"
+BENCH="python3 bench.py --profile-steps 1 --steps 3 --warmup 1 --no-cpu-baseline --no-check $BARGS"
 ALL=("FETCH_SIZE" "WRITE_SIZE" "TCC_HIT_sum TCC_MISS_sum" "SQ_INSTS_VALU SQ_INSTS_SALU SQ_INSTS_LDS SQ_INSTS_SMEM" \
      "SQ_WAVE_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY" \
      "SQ_ACTIVE_INST_VALU SQ_ACTIVE_INST_LDS SQ_ACTIVE_INST_SCA SQ_ACTIVE_INST_MISC" \

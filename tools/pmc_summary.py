@@ -16,8 +16,9 @@ def rows(pattern):
 
 
 def short(name):
-    for k in ("tile_kernel", "splitter_kernel", "partition_kernel", "gather_kernel", "union",
-              "slice_kernel"):
+    for k in ("tile_packed_kernel", "tile_kernel", "splitter_kernel", "partition_kernel",
+              "unmatched_kernel", "gather_kernel", "union", "slice_kernel", "crc_kernel",
+              "darling_kernel", "cm_"):
         if k in name:
             return k
     return None

@@ -8,13 +8,19 @@ import json
 import sys
 
 
-def main(src, bpl, kernel="tile_kernel", out="profiles/pmc_summary.json"):
-    d = json.load(open(src))["counters"][kernel]
+def main(src, bpl, kernel="tile_kernel", out="profiles/pmc_summary.json", workload="cfg2"):
+    allc = json.load(open(src))["counters"]
+    d = allc[kernel]
     hbm = (2 * d["FETCH_SIZE"] + d["WRITE_SIZE"]) * 1024
-    res = {"kernel": kernel, "bytes_per_launch": int(bpl), "hbm_bytes_per_launch": hbm,
+    res = {"kernel": kernel, "workload": workload, "bytes_per_launch": int(bpl),
+           "hbm_bytes_per_launch": hbm,
            "read_bytes": 2 * d["FETCH_SIZE"] * 1024, "write_bytes": d["WRITE_SIZE"] * 1024,
            "ratio_to_algorithmic": hbm / int(bpl),
            "counters": d, "source": src}
+    p = allc.get("partition_kernel")
+    if p and "FETCH_SIZE" in p:
+        res["partition_hbm_bytes_per_launch"] = (2 * p["FETCH_SIZE"] + p["WRITE_SIZE"]) * 1024
+        res["step_ratio_to_algorithmic"] = (hbm + res["partition_hbm_bytes_per_launch"]) / int(bpl)
     json.dump(res, open(out, "w"), indent=1)
     print(json.dumps(res))
 
