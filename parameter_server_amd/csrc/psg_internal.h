@@ -61,6 +61,17 @@ struct TileDesc {
   uint32_t stride;                // the job's segq
   uint32_t flags;
   uint32_t segb;                  // the job's segb
+  const uint64_t* dpos;           // dense jobs: job position of each push's first key
+};
+
+// dense check of one push against the server keys (psg_tile_dense.hip):
+// out[0] = lower_bound(D, keys[0]), out[1] != 0 unless keys == D[out0, +n)
+struct DenseCheck {
+  const uint64_t* keys;
+  uint64_t n;
+  const uint64_t* D;
+  uint64_t nd;
+  unsigned long long* out;
 };
 
 // ---- kernel launchers; all enqueue on `stream` only ----
@@ -77,6 +88,12 @@ hipError_t launch_aggregate_tile(int dtype, int m, const TileDesc* d_tiles, uint
                                  hipStream_t stream);
 hipError_t launch_aggregate_tile_packed(int dtype, int m, const TileDesc* d_tiles,
                                         uint32_t ntiles, hipStream_t stream);
+// psg_tile_dense.hip: every push of every job a contiguous slice of D
+hipError_t launch_aggregate_dense(int dtype, int m, const TileDesc* d_tiles, uint32_t ntiles,
+                                  hipStream_t stream);
+// items: check index << 32 | 4096-key chunk
+hipError_t launch_dense_check(const DenseCheck* checks, uint32_t nchecks, const uint64_t* items,
+                              uint64_t nitems, hipStream_t stream);
 hipError_t launch_gather(int dtype, const uint64_t* dkeys, uint64_t nd,
                          const void* dvals, const uint64_t* req, uint64_t nreq,
                          void* out, unsigned long long* matched,

@@ -63,6 +63,9 @@ struct JobSpec {
   std::vector<uint64_t> pn;
   std::vector<void*> out;
   uint32_t flags;
+  // dense job: every non-empty push p is D[dpos[p], dpos[p] + pn[p])
+  bool dense = false;
+  std::vector<uint64_t> dpos;
 };
 
 // Mean piece length (keys per push per tile) below which a job's partition
@@ -85,6 +88,72 @@ int forced_part_mode() {
   return -1;
 }
 
+// PSG_DENSE=0 turns the dense check of psg_plan_create off (A/B
+// measurements); read once per plan creation.
+bool dense_enabled() {
+  const char* e = getenv("PSG_DENSE");
+  return !(e && e[0] == '0');
+}
+
+// Marks the jobs whose every non-empty push is a contiguous slice of the
+// job's server keys (psg_tile_dense.hip), with each push's start position.
+// One synchronous check on the device per plan.
+int detect_dense(std::vector<JobSpec>& specs) {
+  std::vector<psg::DenseCheck> hc;
+  std::vector<std::pair<size_t, size_t>> at;  // (job, push) of each check
+  std::vector<uint64_t> items;
+  for (size_t j = 0; j < specs.size(); ++j) {
+    const JobSpec& s = specs[j];
+    if (s.nslots == 0) continue;
+    for (size_t p = 0; p < s.pn.size(); ++p) {
+      if (s.pn[p] == 0) continue;
+      if (s.pn[p] > s.nslots) goto next_job;  // cannot be a slice
+      at.emplace_back(j, p);
+      hc.push_back(psg::DenseCheck{s.pkeys[p], s.pn[p], s.keys, s.nslots, nullptr});
+    }
+  next_job:;
+  }
+  if (hc.empty()) return PSG_OK;
+  for (size_t c = 0; c < hc.size(); ++c)
+    for (uint64_t q = 0; q * 4096 < hc[c].n; ++q) items.push_back((uint64_t)c << 32 | q);
+  const size_t ob = align_up(16 * hc.size(), 256), cb = align_up(sizeof(psg::DenseCheck) * hc.size(), 256);
+  char* tmp = nullptr;
+  HIP_TRY(hipMalloc((void**)&tmp, ob + cb + 8 * items.size()));
+  unsigned long long* outs = (unsigned long long*)tmp;
+  for (size_t c = 0; c < hc.size(); ++c) hc[c].out = outs + 2 * c;
+  std::vector<unsigned long long> ho(2 * hc.size());
+  hipError_t e = hipMemset(outs, 0, 16 * hc.size());
+  if (e == hipSuccess) e = hipMemcpy(tmp + ob, hc.data(), sizeof(psg::DenseCheck) * hc.size(),
+                                     hipMemcpyHostToDevice);
+  if (e == hipSuccess) e = hipMemcpy(tmp + ob + cb, items.data(), 8 * items.size(),
+                                     hipMemcpyHostToDevice);
+  if (e == hipSuccess)
+    e = psg::launch_dense_check((const psg::DenseCheck*)(tmp + ob), (uint32_t)hc.size(),
+                                (const uint64_t*)(tmp + ob + cb), items.size(), nullptr);
+  if (e == hipSuccess) e = hipMemcpy(ho.data(), outs, 16 * hc.size(), hipMemcpyDeviceToHost);
+  (void)hipFree(tmp);
+  if (e != hipSuccess) return fail(PSG_ERR_DEVICE, "dense check: %s", hipGetErrorString(e));
+  std::vector<int> ok(specs.size(), -1);  // -1 unchecked, 1 dense so far, 0 not
+  for (size_t c = 0; c < hc.size(); ++c) {
+    const size_t j = at[c].first;
+    if (ok[j] < 0) {
+      ok[j] = 1;
+      specs[j].dpos.assign(specs[j].pn.size(), 0);
+    }
+    if (ho[2 * c + 1]) ok[j] = 0;
+    specs[j].dpos[at[c].second] = ho[2 * c];
+  }
+  for (size_t j = 0; j < specs.size(); ++j) {
+    // every non-empty push was checked (none skipped by the size test)
+    size_t nonempty = 0, checked = 0;
+    for (uint64_t n : specs[j].pn) nonempty += n != 0;
+    for (const auto& a : at) checked += a.first == j;
+    specs[j].dense = ok[j] == 1 && checked == nonempty && nonempty > 0;
+    if (!specs[j].dense) specs[j].dpos.clear();
+  }
+  return PSG_OK;
+}
+
 // PSG_PACK=0|1 forces the round form (A/B measurements); read once per
 // job-table build, never inside a launch.
 int forced_pack() {
@@ -95,6 +164,7 @@ int forced_pack() {
 struct JobTable {
   int device = -1;
   bool pack = false;  // rounds may hold several pushes
+  bool dense = false;  // every job dense: psg_tile_dense.hip, no partition
   int dtype = 0, m = 1;
   std::vector<JobDev> h;
   // per job (host): pushes kept (non-empty) and where their matched counts go
@@ -153,10 +223,12 @@ struct JobTable {
     const int forced = forced_part_mode();
     h.assign(jobs.size(), JobDev{});
     info.assign(jobs.size(), JobInfo{});
-    struct Offs { size_t pk, pv, pn, out, fail, seg, split; };
+    struct Offs { size_t pk, pv, pn, out, fail, seg, split, dpos; };
     std::vector<Offs> offs(jobs.size());
     uint64_t tiles = 0, items = 0, sitems = 0;
     double kv_all = 0, pieces_all = 0;
+    dense = !jobs.empty();
+    for (const JobSpec& s : jobs) dense = dense && s.dense;
     for (size_t j = 0; j < jobs.size(); ++j) {
       const JobSpec& s = jobs[j];
       JobInfo& I = info[j];
@@ -185,12 +257,14 @@ struct JobTable {
       const double piece = I.np && I.ntiles ? (double)kv / ((double)I.np * I.ntiles) : 1e9;
       kv_all += (double)kv;
       pieces_all += (double)I.np * I.ntiles;
-      d.mode = forced >= 0 ? (uint32_t)forced : (piece < kStreamBelow ? psg::kStream : psg::kSearch);
+      d.mode = s.dense ? psg::kSearch
+                       : forced >= 0 ? (uint32_t)forced
+                                     : (piece < kStreamBelow ? psg::kStream : psg::kSearch);
       d.segq = d.mode == psg::kStream ? I.ntiles + 1 : 1u;
       d.segb = d.mode == psg::kStream ? 1u : I.np;
       I.segq = d.segq;
       tiles += I.ntiles;
-      if (I.ntiles && I.np) {
+      if (I.ntiles && I.np && !s.dense) {  // dense: seg filled here, nothing to search
         if (d.mode == psg::kSearch) {
           items += (uint64_t)((I.ntiles + 64) / 64) * I.np;
         } else {
@@ -225,6 +299,8 @@ struct JobTable {
       o.seg = off; off = align_up(off + 4 * (nt + 1) * np, 256);
       o.split = off;
       if (h[j].mode == psg::kStream) off = align_up(off + 8 * (nt + 1), 256);
+      o.dpos = off;
+      if (jobs[j].dense) off = align_up(off + 8 * np, 256);
     }
     if (off > blob_bytes) {
       if (async) HIP_TRY(hipStreamSynchronize(strm));  // the old blob may be in use
@@ -263,6 +339,20 @@ struct JobTable {
         for (int i = 0; i < m; ++i) hv[(size_t)p * m + i] = (uint64_t)s.pvals[(size_t)c * m + i];
       }
       memcpy(img + o.pn, I.pn.data(), 8 * np);
+      if (s.dense) {
+        // seg(p, t) = clamp(t * tile - dpos[p], 0, n_p), tile-major (segq 1, segb np)
+        uint64_t* hd = (uint64_t*)(img + o.dpos);
+        uint32_t* hs = (uint32_t*)(img + o.seg);
+        for (uint32_t p = 0; p < np; ++p) {
+          const uint64_t dp = s.dpos[I.slot[p]], n = I.pn[p];
+          hd[p] = dp;
+          for (uint32_t t = 0; t <= nt; ++t) {
+            const uint64_t edge = (uint64_t)t * tile;
+            const uint64_t v = edge <= dp ? 0 : std::min<uint64_t>(edge - dp, n);
+            hs[(size_t)t * np + p] = (uint32_t)v;
+          }
+        }
+      }
       memcpy(img + o.out, s.out.data(), 8 * m);
       JobDev& d = h[j];
       d.dkeys = s.keys;
@@ -305,6 +395,7 @@ struct JobTable {
         T.stride = d.segq;
         T.segb = d.segb;
         T.flags = s.flags;
+        T.dpos = s.dense ? (const uint64_t*)(base + o.dpos) : nullptr;
       }
     }
     memcpy(img, h.data(), sizeof(JobDev) * h.size());
@@ -323,8 +414,10 @@ struct JobTable {
 
   int run_stage(int stage, hipStream_t s) const {
     if (h.empty()) return PSG_OK;
-    if (stage == 0)
-      HIP_TRY(psg::launch_partition(d_jobs, d_split_items, nsplit, d_items, nitems, s));
+    if (stage == 0) {
+      if (!dense) HIP_TRY(psg::launch_partition(d_jobs, d_split_items, nsplit, d_items, nitems, s));
+    } else if (dense)
+      HIP_TRY(psg::launch_aggregate_dense(dtype, m, d_tiles, ntiles, s));
     else if (pack)
       HIP_TRY(psg::launch_aggregate_tile_packed(dtype, m, d_tiles, ntiles, s));
     else
@@ -754,6 +847,8 @@ int psg_plan_create(int device, int dtype, int m, unsigned flags,
     for (int i = 0; i < m; ++i) s.out.push_back(J.out[i]);
     bytes += J.nslots * (8 + m * sv);
   }
+  if (dense_enabled())
+    if (int rc = detect_dense(specs)) return rc;
   psg_plan* p = new psg_plan();
   int rc = p->table.build(device, dtype, m, specs);
   if (rc) {

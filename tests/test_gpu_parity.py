@@ -308,6 +308,41 @@ def test_plan_cfg4_full_dense(torch_cuda):
     assert_bitexact(keep[3][0].cpu().numpy(), want[0])
 
 
+@pytest.mark.parametrize("dtype,parallel", [(np.float32, False), (np.float64, True),
+                                            (np.float64, False)])
+def test_plan_dense_slices(torch_cuda, dtype, parallel):
+    """The dense fast path (psg_tile_dense.hip): pushes that are contiguous
+    slices of D (whole, inner, tail, single key, empty) fold without key
+    reads, bit-exact with the oracle (m = 2, -0.0 values, pushes starting
+    mid-tile); a job with one near-slice push (one key missing) and a mixed
+    plan take the general kernels and agree too; a second run repeats."""
+    torch = torch_cuda
+    rng = np.random.default_rng(91)
+    D = (np.arange(1, 100001, dtype=np.uint64) * np.uint64(3))
+    sl = [(0, 100000), (500, 70000), (99000, 100000), (0, 0), (12345, 12346), (1023, 4097)]
+
+    def vals(n):
+        v = [rng.standard_normal(n).astype(dtype) for _ in range(2)]
+        v[0][::7] = -0.0
+        return v
+
+    dense = (D, [(D[a:b], vals(b - a)) for a, b in sl])
+    near_k = np.delete(D[200:5200], 77)
+    near = (D, [(D[0:3000], vals(3000)), (near_k, vals(near_k.size))])
+    for cases in ([dense], [dense, near]):
+        plan, keep = plan_for(torch, cases, dtype=dtype, parallel=parallel)
+        for rep in range(2):
+            plan.run()
+            mt = plan.matched().tolist()
+            want_mt = [k.size for _, ps in cases for k, _ in ps]
+            assert mt == want_mt
+            for j, (Dj, pushes) in enumerate(cases):
+                _, _, _, want, _ = O.aggregate(Dj, *ALL, pushes, parallel=parallel, dtype=dtype)
+                for i in range(2):
+                    assert_bitexact(keep[4 * j + 3][i].cpu().numpy()[: Dj.size], want[i])
+        plan.close()
+
+
 @pytest.mark.parametrize("mode", ["search", "stream"])
 def test_plan_partition_modes_agree(torch_cuda, mode, monkeypatch):
     """Both partition modes on dense and sparse jobs, forced
