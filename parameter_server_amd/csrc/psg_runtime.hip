@@ -363,7 +363,7 @@ struct JobTable {
       d.split = d.mode == psg::kStream ? (uint64_t*)(base + o.split) : nullptr;
       I.seg = d.seg;
       I.fail = d.fail;
-      if (nt && np) {
+      if (nt && np && !s.dense) {  // as counted above: dense jobs have no items
         if (d.mode == psg::kSearch) {
           const uint64_t ng = (nt + 64) / 64;
           for (uint64_t g = 0; g < ng; ++g)  // group-major: a boundary group's pushes adjacent
@@ -398,6 +398,13 @@ struct JobTable {
         T.dpos = s.dense ? (const uint64_t*)(base + o.dpos) : nullptr;
       }
     }
+    // the fill must match the sizing pass exactly (the image regions are
+    // packed back to back): a mismatch is a bug, never launched
+    if (icur != items || scur != sitems || tcur != tiles)
+      return fail(PSG_ERR_DEVICE, "job table: %llu/%llu items, %llu/%llu split items, "
+                  "%llu/%llu tiles", (unsigned long long)icur, (unsigned long long)items,
+                  (unsigned long long)scur, (unsigned long long)sitems,
+                  (unsigned long long)tcur, (unsigned long long)tiles);
     memcpy(img, h.data(), sizeof(JobDev) * h.size());
     ntiles = (uint32_t)tiles;
     nitems = (uint32_t)items;

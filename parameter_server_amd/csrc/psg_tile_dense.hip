@@ -58,51 +58,71 @@ __global__ __launch_bounds__(kNT) void dense_kernel(const TileDesc* __restrict__
 #pragma unroll
     for (int j = 0; j < 4; ++j)
       acc[mi][j] = (cont && s0 + j < nt) ? G((const V*)T.out[mi] + T.slot0)[s0 + j] : V(0);
-  for (uint32_t q = 0; q < np; ++q) {
-    // piece [a, b) of push q in this tile; its first element sits on slot
-    // dpos[q] + a (job positions), i.e. tile slot ps
-    const uint32_t* sg = T.seg + (size_t)q * T.stride;
-    const uint32_t a = uni(G(sg)[0]), b = uni(G(sg)[T.segb]);
-    if (b <= a) continue;
-    const int64_t ps = (int64_t)(G(T.dpos)[q] + a) - (int64_t)T.slot0;
-    const int64_t pe = ps + (int64_t)(b - a);
-    const bool first = q == 0 && !cont;
+  // pushes in batches of kB: all of a batch's value loads are issued before
+  // its fold, so kB loads per thread are in flight instead of one
+  constexpr int kB = (int)(32 / (M * sizeof(V))) > 0 ? (int)(32 / (M * sizeof(V))) : 1;
+  for (uint32_t q0 = 0; q0 < np; q0 += kB) {
+    int64_t ps[kB], pe[kB];
+    V v[kB][M][4];
 #pragma unroll
-    for (int mi = 0; mi < M; ++mi) {
-      const V* vp = (const V*)G(T.pvals)[(size_t)q * M + mi] + a;  // element of slot ps
-      V v[4];
-      const int64_t e0 = (int64_t)s0 - ps;  // element index of this thread's first slot
-      if (e0 >= 0 && (int64_t)s0 + 3 < pe && (((uintptr_t)(vp + e0)) & (4 * sizeof(V) - 1)) == 0) {
-        if constexpr (sizeof(V) == 4) {
-          typedef float f4 __attribute__((ext_vector_type(4)));
-          const f4 x = *(const AS1 f4*)(vp + e0);
-          v[0] = x.x; v[1] = x.y; v[2] = x.z; v[3] = x.w;
-        } else {
-          typedef double d2 __attribute__((ext_vector_type(2)));
-          const d2 x0 = ((const AS1 d2*)(vp + e0))[0], x1 = ((const AS1 d2*)(vp + e0))[1];
-          v[0] = x0.x; v[1] = x0.y; v[2] = x1.x; v[3] = x1.y;
+    for (int u = 0; u < kB; ++u) {
+      const uint32_t q = q0 + u;
+      ps[u] = 0;
+      pe[u] = 0;  // empty: no slot
+      if (q < np) {
+        // piece [a, b) of push q in this tile; its first element sits on
+        // slot dpos[q] + a (job positions), i.e. tile slot ps
+        const uint32_t* sg = T.seg + (size_t)q * T.stride;
+        const uint32_t a = uni(G(sg)[0]), b = uni(G(sg)[T.segb]);
+        if (b > a) {
+          ps[u] = (int64_t)(G(T.dpos)[q] + a) - (int64_t)T.slot0;
+          pe[u] = ps[u] + (int64_t)(b - a);
         }
-      } else {
 #pragma unroll
-        for (int j = 0; j < 4; ++j) {
-          const int64_t s = (int64_t)s0 + j;
-          v[j] = (s >= ps && s < pe) ? G(vp)[s - ps] : V(0);
-        }
-      }
+        for (int mi = 0; mi < M; ++mi) {
+          const V* vp = (const V*)G(T.pvals)[(size_t)q * M + mi] + a;  // element of slot ps
+          const int64_t e0 = (int64_t)s0 - ps[u];  // element index of this thread's first slot
+          if (e0 >= 0 && (int64_t)s0 + 3 < pe[u] &&
+              (((uintptr_t)(vp + e0)) & (4 * sizeof(V) - 1)) == 0) {
+            // read once: nontemporal (the measured copy ceiling is with them)
+            if constexpr (sizeof(V) == 4) {
+              typedef float f4 __attribute__((ext_vector_type(4)));
+              const f4 x = __builtin_nontemporal_load((const AS1 f4*)(vp + e0));
+              v[u][mi][0] = x.x; v[u][mi][1] = x.y; v[u][mi][2] = x.z; v[u][mi][3] = x.w;
+            } else {
+              typedef double d2 __attribute__((ext_vector_type(2)));
+              const d2 x0 = __builtin_nontemporal_load((const AS1 d2*)(vp + e0));
+              const d2 x1 = __builtin_nontemporal_load((const AS1 d2*)(vp + e0) + 1);
+              v[u][mi][0] = x0.x; v[u][mi][1] = x0.y; v[u][mi][2] = x1.x; v[u][mi][3] = x1.y;
+            }
+          } else {
 #pragma unroll
-      for (int j = 0; j < 4; ++j) {
-        const int64_t s = (int64_t)s0 + j;
-        if (s >= ps && s < pe) {
-          const bool gap = !parallel && last[j] < (int)q - 1;
-          const V ag = gap ? acc[mi][j] + V(0) : acc[mi][j];
-          acc[mi][j] = first ? v[j] : ag + v[j];
+            for (int j = 0; j < 4; ++j) {
+              const int64_t sl = (int64_t)s0 + j;
+              v[u][mi][j] = (sl >= ps[u] && sl < pe[u]) ? G(vp)[sl - ps[u]] : V(0);
+            }
+          }
         }
       }
     }
+    // fold the batch in push order
 #pragma unroll
-    for (int j = 0; j < 4; ++j) {
-      const int64_t s = (int64_t)s0 + j;
-      if (s >= ps && s < pe) last[j] = (int)q;
+    for (int u = 0; u < kB; ++u) {
+      const int q = (int)(q0 + u);
+      const bool first = q == 0 && !cont;
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        const int64_t sl = (int64_t)s0 + j;
+        if (sl >= ps[u] && sl < pe[u]) {
+          const bool gap = !parallel && last[j] < q - 1;
+#pragma unroll
+          for (int mi = 0; mi < M; ++mi) {
+            const V ag = gap ? acc[mi][j] + V(0) : acc[mi][j];
+            acc[mi][j] = first ? v[u][mi][j] : ag + v[u][mi][j];
+          }
+          last[j] = q;
+        }
+      }
     }
   }
   // trailing "+0.0" of absent last pushes (serial), stores
