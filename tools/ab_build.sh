@@ -19,5 +19,5 @@ for f in $SRC/*.hip; do
     -ffp-contract=off $F -c $f -o $O/$(basename $f .hip).o &
 done
 wait
-/opt/rocm/bin/hipcc -shared -fPIC --offload-arch=gfx950 -o $O/libpsg.so $O/*.o
+/opt/rocm/bin/hipcc -shared -fPIC --offload-arch=gfx950 -o $O/libpsg.so $O/*.o -L/opt/rocm/lib -lrccl
 rm -f $O/*.o
