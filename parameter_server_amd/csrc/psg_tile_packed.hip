@@ -411,7 +411,11 @@ __global__ __launch_bounds__(kNT, (occupancy<V, M>())) void tile_packed_kernel(
       }
     }
     // ---- rounds holding several pushes: do two of them hit one slot?
-    uint32_t cmask = 0;  // wave-uniform: bit r = round r needs the push-ordered fold
+    // cl[r] (wave-uniform): the lanes of round r that found their slot's bit
+    // already set -- each names a slot hit more than once in the round
+    unsigned long long cl[kCap];
+#pragma unroll
+    for (int r = 0; r < kCap; ++r) cl[r] = 0;
     if (mmask) {
 #pragma unroll
       for (int r = 0; r < kCap; ++r) {
@@ -421,7 +425,7 @@ __global__ __launch_bounds__(kNT, (occupancy<V, M>())) void tile_packed_kernel(
           uint32_t old = 0;
           if (ok) old = __hip_atomic_fetch_or(&cbits[w][s >> 5], bit, __ATOMIC_RELAXED,
                                               __HIP_MEMORY_SCOPE_WAVEFRONT);
-          cmask |= (__ballot(ok && (old & bit)) != 0 ? 1u : 0u) << r;
+          cl[r] = __ballot(ok && (old & bit));
           if (ok) cbits[w][s >> 5] = 0u;
         }
       }
@@ -450,16 +454,35 @@ __global__ __launch_bounds__(kNT, (occupancy<V, M>())) void tile_packed_kernel(
               }
               lastl[s] = (uint8_t)(q + 2u);
             };
-            if (!((cmask >> r) & 1u)) {
+            const unsigned long long cm = cl[r];
+            if (!cm) {
               if (pend) apply();  // no two lanes of the round on one slot
             } else {
-              // push-ordered: the lowest pending push applies first
+              // lanes on a slot that cm names must go in lane order, which is
+              // push order (rounds cut the push-major concatenation); every
+              // other lane has a slot of its own and applies at once
+              bool inv = false;
+              for (unsigned long long t = cm; t; t &= t - 1) {
+                const uint32_t sl =
+                    (uint32_t)__builtin_amdgcn_readlane((int)s, (int)__builtin_ctzll(t));
+                inv |= s == sl;
+              }
+              if (pend && !inv) {
+                apply();
+                pend = false;
+              }
+              // then, per pass, the lowest pending lane of each shared slot
+              // (passes = the largest multiplicity, almost always 2)
               for (;;) {
-                const unsigned long long pm = __ballot(pend);
-                if (!pm) break;
-                const uint32_t qmin =
-                    (uint32_t)__builtin_amdgcn_readlane((int)q, (int)__builtin_ctzll(pm));
-                if (pend && q == qmin) {
+                const unsigned long long im = __ballot(pend);
+                if (!im) break;
+                bool lowest = pend;
+                for (unsigned long long t = im; t; t &= t - 1) {
+                  const int j = (int)__builtin_ctzll(t);
+                  const uint32_t sl = (uint32_t)__builtin_amdgcn_readlane((int)s, j);
+                  if (j < lane && s == sl) lowest = false;
+                }
+                if (lowest) {
                   apply();
                   pend = false;
                 }

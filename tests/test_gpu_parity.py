@@ -343,6 +343,35 @@ def test_plan_dense_slices(torch_cuda, dtype, parallel):
         plan.close()
 
 
+@pytest.mark.parametrize("pack", ["0", "1"])
+def test_plan_round_forms_agree(torch_cuda, pack, monkeypatch):
+    """Both aggregate kernels on the same jobs, forced with PSG_PACK (read at
+    plan creation): push-uniform rounds (psg_tile.hip) and packed multi-push
+    rounds (psg_tile_packed.hip), whose rounds hold several pushes that can
+    hit one slot (heavy overlap: many same-slot lanes per round, resolved in
+    push order) -- bit-exact either way, serial and parallel."""
+    torch = torch_cuda
+    from parameter_server_amd import synth
+    monkeypatch.setenv("PSG_PACK", pack)
+    rng = np.random.default_rng(5)
+    D = np.unique(rng.integers(0, 1 << 50, 20000, dtype=np.uint64))
+    tiny = [(np.sort(rng.choice(D, n, replace=False)),
+             [rng.standard_normal(n).astype(np.float32)]) for n in
+            [int(x) for x in rng.integers(1, 60, 150)]]
+    for p_ in tiny[::7]:
+        p_[1][0][::3] = -0.0
+    cases = [(D, tiny), synth.overlap_pushes(8, npush=70, n=2000, overlap=0.9),
+             synth.zipf_pushes(9, npush=24, n=3000)]
+    for parallel in (False, True):
+        plan, keep = plan_for(torch, cases, parallel=parallel)
+        plan.run()
+        assert plan.matched().tolist() == [k.size for _, ps in cases for k, _ in ps]
+        for j, (Dj, pushes) in enumerate(cases):
+            _, _, _, want, _ = O.aggregate(Dj, *ALL, pushes, parallel=parallel)
+            assert_bitexact(keep[4 * j + 3][0].cpu().numpy()[: Dj.size], want[0])
+        plan.close()
+
+
 @pytest.mark.parametrize("mode", ["search", "stream"])
 def test_plan_partition_modes_agree(torch_cuda, mode, monkeypatch):
     """Both partition modes on dense and sparse jobs, forced
