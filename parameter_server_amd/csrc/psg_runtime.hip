@@ -78,8 +78,10 @@ constexpr double kStreamBelow = 64.0;
 // push-uniform, which is faster while most rounds are full anyway.
 constexpr double kPackBelow = 16.0;
 
-// PSG_PART_MODE=search|stream forces the partition mode (A/B measurements);
-// read once per job-table build, never inside a launch.
+// A/B knobs (measurements and tests): read from the environment when a
+// context or a plan is created (JobTable::read_knobs), never per flush or
+// launch.
+// PSG_PART_MODE=search|stream forces the partition mode.
 int forced_part_mode() {
   const char* e = getenv("PSG_PART_MODE");
   if (!e) return -1;
@@ -88,8 +90,7 @@ int forced_part_mode() {
   return -1;
 }
 
-// PSG_DENSE=0 turns the dense check of psg_plan_create off (A/B
-// measurements); read once per plan creation.
+// PSG_DENSE=0 turns the dense check of psg_plan_create off.
 bool dense_enabled() {
   const char* e = getenv("PSG_DENSE");
   return !(e && e[0] == '0');
@@ -154,8 +155,7 @@ int detect_dense(std::vector<JobSpec>& specs) {
   return PSG_OK;
 }
 
-// PSG_PACK=0|1 forces the round form (A/B measurements); read once per
-// job-table build, never inside a launch.
+// PSG_PACK=0|1 forces the round form.
 int forced_pack() {
   const char* e = getenv("PSG_PACK");
   return e && (e[0] == '0' || e[0] == '1') ? e[0] - '0' : -1;
@@ -163,6 +163,11 @@ int forced_pack() {
 
 struct JobTable {
   int device = -1;
+  int knob_part = -1, knob_pack = -1;  // forced modes (read_knobs), -1 = chosen per build
+  void read_knobs() {
+    knob_part = forced_part_mode();
+    knob_pack = forced_pack();
+  }
   bool pack = false;  // rounds may hold several pushes
   bool dense = false;  // every job dense: psg_tile_dense.hip, no partition
   int dtype = 0, m = 1;
@@ -220,7 +225,7 @@ struct JobTable {
     dtype = dt;
     m = mm;
     const uint32_t tile = psg::kTileSlots;
-    const int forced = forced_part_mode();
+    const int forced = knob_part;
     h.assign(jobs.size(), JobDev{});
     info.assign(jobs.size(), JobInfo{});
     struct Offs { size_t pk, pv, pn, out, fail, seg, split, dpos; };
@@ -278,7 +283,7 @@ struct JobTable {
       if (j >= (1ull << 27)) return fail(PSG_ERR_ARG, "too many jobs");
     }
     {
-      const int fp = forced_pack();
+      const int fp = knob_pack;
       pack = fp >= 0 ? fp == 1 : (pieces_all > 0 && kv_all / pieces_all < kPackBelow);
     }
     size_t off = align_up(sizeof(JobDev) * jobs.size(), 256);
@@ -857,6 +862,7 @@ int psg_plan_create(int device, int dtype, int m, unsigned flags,
   if (dense_enabled())
     if (int rc = detect_dense(specs)) return rc;
   psg_plan* p = new psg_plan();
+  p->table.read_knobs();
   int rc = p->table.build(device, dtype, m, specs);
   if (rc) {
     p->table.release();
@@ -979,6 +985,7 @@ int psg_create(int device, int dtype, unsigned flags, psg_ctx** out) {
     const long v = atol(f);
     if (v >= 1 && v <= psg::kMaxPush) c->flush_pushes = (size_t)v;
   }
+  c->table.read_knobs();
   hipError_t e = hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking);
   if (e == hipSuccess) e = hipStreamCreateWithFlags(&c->copy, hipStreamNonBlocking);
   if (e == hipSuccess) e = hipEventCreateWithFlags(&c->copy_ev, hipEventDisableTiming);
