@@ -111,6 +111,16 @@ int psg_value_copy(psg_ctx* ctx, int chl, size_t off, size_t n, void* out);
 int psg_push(psg_ctx* ctx, int chl, int time, uint64_t kb, uint64_t ke,
              const uint64_t* keys, size_t n, int m, const void* const* vals);
 
+/* Value push of snappy-compressed parts, as they arrive off the wire
+ * (Van::recv with task.uncompressed_size set, van.cc:204-214): the key part
+ * (uint64 keys) and m value parts are DMA'd compressed and decompressed on
+ * the device (psg_snappy_uncompress_dev), then pushed like psg_push.
+ * Waits for its own decompression; a corrupt part is PSG_ERR_ARG, parts of
+ * inconsistent sizes PSG_ERR_SIZE (the reference's CHECKs). */
+int psg_push_compressed(psg_ctx* ctx, int chl, int time, uint64_t kb, uint64_t ke,
+                        const void* ckeys, size_t ckeys_bytes, int m,
+                        const void* const* cvals, const size_t* cvals_bytes);
+
 /* Value or key push through the receiver's key cache: RNode::cacheKeyRecver
  * (src/system/remote_node.cc:139-184) followed by setValue.  The server
  * keeps one cache per remote node (RNode::key_cache_, remote_node.h:92-93):
@@ -308,6 +318,20 @@ int psg_freq_table(psg_ctx* ctx, int chl, uint8_t* out, size_t n);
  * 163) is max_len = PSG_MAX_SIG_LEN over the key bytes.  off[nseg+1], init
  * (nullable) and out[nseg] are device arrays; enqueued on `stream`. */
 #define PSG_MAX_SIG_LEN 2048 /* RNode::max_sig_len_, remote_node.h:96 */
+
+/* snappy raw-format decompression of device-resident message parts: what
+ * Van::recv does per key/value part (van.cc:204-214,
+ * SArray::uncompressFrom, shared_array_inl.h:232-240), for nmsg parts in
+ * one launch.  Part i is src[soff[i], soff[i+1]) and decompresses into
+ * dst[doff[i], doff[i+1]), which must be its declared length
+ * (snappy::GetUncompressedLength; psg_snappy_uncompressed_length reads it
+ * from a host copy of the first bytes).  status[i] = 0, PSG_ERR_SIZE (the
+ * declared length differs) or PSG_ERR_ARG (corrupt stream: the reference's
+ * CHECK).  soff, doff, status: device arrays; enqueued on `stream`. */
+int psg_snappy_uncompress_dev(const uint8_t* src, const uint64_t* soff, uint64_t nmsg,
+                              uint8_t* dst, const uint64_t* doff, int32_t* status,
+                              void* stream);
+int psg_snappy_uncompressed_length(const void* src, size_t n, size_t* len);
 int psg_crc32c_dev(const void* data, const uint64_t* off, uint64_t nseg,
                    uint64_t max_len, const uint32_t* init, uint32_t* out,
                    void* stream);

@@ -503,3 +503,131 @@ size_t orc_ff_query(const uint8_t* data, uint32_t n, int k, const uint64_t* keys
     if ((int)orc_cm_query(data, n, k, keys[i]) > freq) out[m++] = keys[i];
   return m;
 }
+
+/* ---------------------------------------------------------------------- */
+/* snappy raw format (third-party dependency of the reference, absent from */
+/* /root/reference: google/snappy, used by SArray::uncompressFrom /        */
+/* compressTo, base/shared_array_inl.h:232-254, on Van payloads,           */
+/* system/van.cc:204-214).  Restated from snappy's published format        */
+/* description (format_description.txt): a little-endian varint of the     */
+/* uncompressed length, then elements -- tag & 3: 0 literal (length-1 in   */
+/* tag >> 2, or in 1..4 following bytes when that is 60..63), 1 copy of    */
+/* 4 + ((tag >> 2) & 7) bytes at offset (tag >> 5) << 8 | next byte, 2 / 3  */
+/* copy of 1 + (tag >> 2) bytes at a 2 / 4-byte little-endian offset.      */
+/* PARITY UNPINNED: no snappy test vectors ship in /root/reference; the    */
+/* tests use spec-derived hand-made streams and this file's compressor.    */
+/* ---------------------------------------------------------------------- */
+int orc_snappy_uncompressed_length(const uint8_t* src, size_t n, size_t* out) {
+  uint64_t v = 0;
+  for (size_t i = 0; i < n && i < 5; ++i) {
+    v |= (uint64_t)(src[i] & 0x7f) << (7 * i);
+    if (!(src[i] & 0x80)) {
+      if (v > 0xffffffffull) return -1;
+      *out = (size_t)v;
+      return (int)(i + 1);  /* preamble bytes */
+    }
+  }
+  return -1;
+}
+
+/* RawUncompress: 0, or -1 for a corrupt stream / length mismatch. */
+int orc_snappy_uncompress(const uint8_t* src, size_t n, uint8_t* dst, size_t cap) {
+  size_t ulen;
+  const int pre = orc_snappy_uncompressed_length(src, n, &ulen);
+  if (pre < 0 || ulen != cap) return -1;
+  size_t p = (size_t)pre, o = 0;
+  while (p < n) {
+    const uint32_t tag = src[p++];
+    size_t len, off = 0;
+    if ((tag & 3) == 0) {
+      len = (tag >> 2) + 1;
+      if (len > 60) {
+        const size_t nb = len - 60;
+        if (p + nb > n) return -1;
+        len = 0;
+        for (size_t b = 0; b < nb; ++b) len |= (size_t)src[p + b] << (8 * b);
+        len += 1;
+        p += nb;
+      }
+      if (p + len > n || o + len > cap) return -1;
+      memcpy(dst + o, src + p, len);
+      p += len;
+      o += len;
+      continue;
+    }
+    if ((tag & 3) == 1) {
+      if (p + 1 > n) return -1;
+      len = 4 + ((tag >> 2) & 7);
+      off = ((size_t)(tag >> 5) << 8) | src[p];
+      p += 1;
+    } else if ((tag & 3) == 2) {
+      if (p + 2 > n) return -1;
+      len = 1 + (tag >> 2);
+      off = (size_t)src[p] | (size_t)src[p + 1] << 8;
+      p += 2;
+    } else {
+      if (p + 4 > n) return -1;
+      len = 1 + (tag >> 2);
+      off = (size_t)src[p] | (size_t)src[p + 1] << 8 | (size_t)src[p + 2] << 16 |
+            (size_t)src[p + 3] << 24;
+      p += 4;
+    }
+    if (off == 0 || off > o || o + len > cap) return -1;
+    for (size_t i = 0; i < len; ++i) dst[o + i] = dst[o - off + i]; /* overlap: byte order */
+    o += len;
+  }
+  return o == cap ? 0 : -1;
+}
+
+/* A greedy compressor producing a valid raw stream (test input only; not
+ * the reference's RawCompress, whose exact bytes differ): 64 KB blocks,
+ * 4-byte hash matches, copies of <= 64 bytes with 2-byte offsets, literals
+ * with every length encoding.  dst holds 32 + n + n / 6 bytes. */
+size_t orc_snappy_compress(const uint8_t* src, size_t n, uint8_t* dst) {
+  size_t o = 0;
+  size_t v = n;
+  do { uint8_t b = v & 0x7f; v >>= 7; dst[o++] = (uint8_t)(b | (v ? 0x80 : 0)); } while (v);
+  static int table[1 << 14];
+  for (size_t blk = 0; blk < n; blk += 65536) {
+    const size_t end = blk + 65536 < n ? blk + 65536 : n;
+    for (int i = 0; i < (1 << 14); ++i) table[i] = -1;
+    size_t lit = blk, i = blk;
+#define EMIT_LIT(from, to)                                                   \
+    do {                                                                     \
+      size_t L = (to) - (from);                                              \
+      if (L) {                                                               \
+        if (L <= 60) dst[o++] = (uint8_t)((L - 1) << 2);                     \
+        else {                                                               \
+          size_t x = L - 1, nb = x < 256 ? 1 : x < 65536 ? 2 : x < (1u << 24) ? 3 : 4; \
+          dst[o++] = (uint8_t)((59 + nb) << 2);                              \
+          for (size_t b = 0; b < nb; ++b) dst[o++] = (uint8_t)(x >> (8 * b)); \
+        }                                                                    \
+        memcpy(dst + o, src + (from), L);                                    \
+        o += L;                                                              \
+      }                                                                      \
+    } while (0)
+    while (i + 4 <= end) {
+      uint32_t w;
+      memcpy(&w, src + i, 4);
+      const uint32_t h = (w * 0x1e35a7bdu) >> 18;
+      const int c = table[h];
+      table[h] = (int)(i - blk);
+      if (c >= 0 && memcmp(src + blk + c, src + i, 4) == 0) {
+        size_t m = 4;
+        while (i + m < end && m < 64 && src[blk + c + m] == src[i + m]) ++m;
+        EMIT_LIT(lit, i);
+        const size_t off = i - (blk + (size_t)c);
+        dst[o++] = (uint8_t)(2 | ((m - 1) << 2));
+        dst[o++] = (uint8_t)off;
+        dst[o++] = (uint8_t)(off >> 8);
+        i += m;
+        lit = i;
+      } else {
+        ++i;
+      }
+    }
+    EMIT_LIT(lit, end);
+#undef EMIT_LIT
+  }
+  return o;
+}

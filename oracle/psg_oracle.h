@@ -133,6 +133,14 @@ uint8_t orc_cm_query(const uint8_t* data, uint32_t n, int k, uint64_t key);
 size_t orc_ff_query(const uint8_t* data, uint32_t n, int k, const uint64_t* keys,
                     size_t nk, int freq, uint64_t* out);
 
+/* snappy raw format (google/snappy, absent from the reference tree; the
+ * published format restated), parity unpinned.  uncompressed_length
+ * returns the preamble size or -1; uncompress returns 0 or -1; compress is
+ * a test-input generator (dst holds 32 + n + n / 6 bytes). */
+int orc_snappy_uncompressed_length(const uint8_t* src, size_t n, size_t* out);
+int orc_snappy_uncompress(const uint8_t* src, size_t n, uint8_t* dst, size_t cap);
+size_t orc_snappy_compress(const uint8_t* src, size_t n, uint8_t* dst);
+
 #ifdef __cplusplus
 }
 #endif

@@ -85,6 +85,8 @@ SIGNATURES = {
     "psg_push_cached": (C.c_int, [_p, C.c_int, C.c_int, C.c_int, _u64, _u64, C.c_uint,
                                   C.c_uint32, _p, _sz, C.c_int, _p, _sz]),
     "psg_key_cache_clear": (C.c_int, [_p, C.c_int]),
+    "psg_push_compressed": (C.c_int, [_p, C.c_int, C.c_int, _u64, _u64, _p, _sz, C.c_int,
+                                      _p, _p]),
     "psg_key_cache_bytes": (C.c_int, [_p, C.c_int, _psz]),
     "psg_received_shape": (C.c_int, [_p, C.c_int, C.POINTER(C.c_int), _psz, _psz]),
     "psg_received": (C.c_int, [_p, C.c_int, C.c_int, C.POINTER(_p)]),
@@ -102,6 +104,8 @@ SIGNATURES = {
     "psg_shard_bounds": (C.c_int, [_sz, _pu64]),
     "psg_slice_dev": (C.c_int, [_p, _u64, _u64, _u64, _p, C.c_int, _p, _p]),
     "psg_crc32c_dev": (C.c_int, [_p, _p, _u64, _u64, _p, _p, _p]),
+    "psg_snappy_uncompress_dev": (C.c_int, [_p, _p, _u64, _p, _p, _p, _p]),
+    "psg_snappy_uncompressed_length": (C.c_int, [_p, _sz, _psz]),
     "psg_freq_resize": (C.c_int, [_p, C.c_int, C.c_int, C.c_int]),
     "psg_freq_clear": (C.c_int, [_p, C.c_int]),
     "psg_freq_empty": (C.c_int, [_p, C.c_int, C.POINTER(C.c_int)]),

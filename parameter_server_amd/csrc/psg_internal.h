@@ -139,6 +139,12 @@ hipError_t launch_cm_query(const uint64_t* keys, uint64_t nk, const uint32_t* ta
                            int k, int freq, uint64_t* out, unsigned long long* nout,
                            void* scratch, hipStream_t stream);
 
+// snappy raw-format decompression (psg_snappy.hip), one wave per message:
+// part i -> dst + doff[i], of dcap[i] bytes (dcap NULL: doff[i+1] - doff[i])
+hipError_t launch_snappy(const uint8_t* src, const uint64_t* soff, uint64_t nmsg, uint8_t* dst,
+                         const uint64_t* doff, const uint64_t* dcap, int32_t* status,
+                         hipStream_t stream);
+
 // CRC-32C (psg_crc32c.hip): out[i] = crc32c::Extend(init ? init[i] : 0,
 // data + off[i], min(off[i+1] - off[i], max_len)); all pointers device
 uint64_t crc32c_chunks_per_segment(uint64_t max_len);

@@ -784,9 +784,11 @@ struct psg_ctx {
     dev_put(a.d_bad, 8);
   }
 
-  // the value push behind psg_push / psg_push_cached: keys already resident
+  // the value push behind psg_push / psg_push_cached / psg_push_compressed:
+  // keys already resident; values staged from the host, or (vblock) already
+  // resident in a pool block of m arrays of align_up(n * s_V, 256) bytes
   int push_values(int chl, int time, uint64_t kb, uint64_t ke, const KeyRef& keys, int m,
-                  const void* const* vals);
+                  const void* const* vals, void* vblock = nullptr);
 };
 
 namespace {
@@ -972,6 +974,31 @@ int psg_crc32c_dev(const void* data, const uint64_t* off, uint64_t nseg, uint64_
   return PSG_OK;
 }
 
+int psg_snappy_uncompress_dev(const uint8_t* src, const uint64_t* soff, uint64_t nmsg,
+                              uint8_t* dst, const uint64_t* doff, int32_t* status,
+                              void* stream) {
+  if (nmsg == 0) return PSG_OK;
+  if (!src || !soff || !dst || !doff || !status) return fail(PSG_ERR_ARG, "null argument");
+  HIP_TRY(psg::launch_snappy(src, soff, nmsg, dst, doff, nullptr, status, (hipStream_t)stream));
+  return PSG_OK;
+}
+
+int psg_snappy_uncompressed_length(const void* src, size_t n, size_t* len) {
+  if (!len || (n && !src)) return fail(PSG_ERR_ARG, "null argument");
+  // the preamble: a little-endian base-128 varint of at most 32 bits
+  const uint8_t* p = (const uint8_t*)src;
+  uint64_t v = 0;
+  for (size_t i = 0; i < n && i < 5; ++i) {
+    v |= (uint64_t)(p[i] & 0x7f) << (7 * i);
+    if (!(p[i] & 0x80)) {
+      if (v > 0xffffffffull) break;
+      *len = (size_t)v;
+      return PSG_OK;
+    }
+  }
+  return fail(PSG_ERR_ARG, "snappy: bad length preamble");
+}
+
 // --------------------------------------------------------------- context --
 int psg_create(int device, int dtype, unsigned flags, psg_ctx** out) {
   if (!out) return fail(PSG_ERR_ARG, "null out");
@@ -1121,7 +1148,7 @@ int check_push(psg_ctx* c, int chl, int time, uint64_t kb, uint64_t ke, size_t n
 }  // namespace
 
 int psg_ctx::push_values(int chl, int time, uint64_t kb, uint64_t ke, const KeyRef& keys, int m,
-                         const void* const* vals) {
+                         const void* const* vals, void* vblock) {
   (void)kb;
   (void)ke;
   size_t lo = 0, hi = 0;
@@ -1138,12 +1165,17 @@ int psg_ctx::push_values(int chl, int time, uint64_t kb, uint64_t ke, const KeyR
   pp.keys = keys;
   const size_t vb = align_up(sv * n, 256);
   pp.vbytes = m * vb;
-  if (int rc = dev_get(pp.vbytes, &pp.vblock, copy)) return rc;
-  for (int i = 0; i < m; ++i) {
-    pp.d_vals[i] = (char*)pp.vblock + i * vb;
-    if (int rc = h2d(pp.d_vals[i], vals[i], sv * n)) {
-      release_push(pp);
-      return rc;
+  if (vblock) {
+    pp.vblock = vblock;
+    for (int i = 0; i < m; ++i) pp.d_vals[i] = (char*)pp.vblock + i * vb;
+  } else {
+    if (int rc = dev_get(pp.vbytes, &pp.vblock, copy)) return rc;
+    for (int i = 0; i < m; ++i) {
+      pp.d_vals[i] = (char*)pp.vblock + i * vb;
+      if (int rc = h2d(pp.d_vals[i], vals[i], sv * n)) {
+        release_push(pp);
+        return rc;
+      }
     }
   }
   if (ait == agg.end()) {
@@ -1278,6 +1310,82 @@ namespace {
 int push_cached_impl(psg_ctx* c, int sender, int chl, int time, uint64_t kb, uint64_t ke,
                      unsigned kc, uint32_t sig, const uint64_t* keys, size_t nkeys, int m,
                      const void* const* vals, size_t nvals);
+}
+
+int psg_push_compressed(psg_ctx* c, int chl, int time, uint64_t kb, uint64_t ke,
+                        const void* ckeys, size_t ckeys_bytes, int m, const void* const* cvals,
+                        const size_t* cvals_bytes) {
+  if (!c) return fail(PSG_ERR_ARG, "null ctx");
+  if (m < 1 || m > PSG_MAX_VALUE_ARRAYS || !cvals || !cvals_bytes || (ckeys_bytes && !ckeys))
+    return fail(PSG_ERR_ARG, "bad compressed push arguments");
+  if (ckeys_bytes == 0) return PSG_OK;  // an empty key part: empty push, ignored
+  // declared lengths (GetUncompressedLength); whole elements (:236)
+  size_t klen = 0;
+  if (int rc = psg_snappy_uncompressed_length(ckeys, ckeys_bytes, &klen)) return rc;
+  if (klen % 8) return fail(PSG_ERR_SIZE, "key part of %zu bytes", klen);
+  const size_t n = klen / 8;
+  if (n == 0) return PSG_OK;
+  const size_t sv = vsize(c->dtype);
+  for (int i = 0; i < m; ++i) {
+    size_t vl = 0;
+    if (!cvals[i] || !cvals_bytes[i]) return fail(PSG_ERR_SIZE, "empty value part %d", i);
+    if (int rc = psg_snappy_uncompressed_length(cvals[i], cvals_bytes[i], &vl)) return rc;
+    if (vl != n * sv)  // CHECK_EQ(recv_data.size(), recv_key.size()) kv_vector.h:187
+      return fail(PSG_ERR_SIZE, "value part %d: %zu bytes for %zu keys", i, vl, n);
+  }
+  std::lock_guard<std::mutex> l(c->mu);
+  if (int rc = set_dev(c->device)) return rc;
+  size_t lo, hi;
+  if (int rc = check_push(c, chl, time, kb, ke, n, m, &lo, &hi)) return rc;
+  // staging block: compressed parts, then source offsets, destinations,
+  // capacities and statuses of the m + 1 parts
+  const int np = m + 1;
+  std::vector<uint64_t> soff(np + 1, 0);
+  soff[1] = ckeys_bytes;
+  for (int i = 0; i < m; ++i) soff[i + 2] = soff[i + 1] + cvals_bytes[i];
+  const size_t tb = align_up(soff[np], 256), meta = 8 * (size_t)(np + 1) + 16 * np + 4 * np;
+  void* blk = nullptr;
+  if (int rc = c->dev_get(tb + meta, &blk, c->copy)) return rc;
+  KeyRef k;
+  void* vblock = nullptr;
+  const size_t vb = align_up(sv * n, 256);
+  int rc = c->new_keys(n, &k);
+  if (rc == PSG_OK) rc = c->dev_get(m * vb, &vblock, c->copy);
+  char* b = (char*)blk;
+  uint64_t* d_soff = (uint64_t*)(b + tb);
+  uint64_t* d_dst = d_soff + (np + 1);
+  uint64_t* d_cap = d_dst + np;
+  int32_t* d_st = (int32_t*)(d_cap + np);
+  std::vector<uint64_t> hm(np + 1 + 2 * np);
+  if (rc == PSG_OK) {
+    std::copy(soff.begin(), soff.end(), hm.begin());
+    hm[np + 1] = (uint64_t)k->d;
+    hm[np + 1 + np] = klen;
+    for (int i = 0; i < m; ++i) {
+      hm[np + 2 + i] = (uint64_t)((char*)vblock + i * vb);
+      hm[np + 1 + np + 1 + i] = n * sv;
+    }
+    rc = c->h2d(b, ckeys, ckeys_bytes);
+    for (int i = 0; rc == PSG_OK && i < m; ++i) rc = c->h2d(b + soff[i + 1], cvals[i], cvals_bytes[i]);
+    if (rc == PSG_OK) rc = c->h2d(d_soff, hm.data(), 8 * hm.size());
+  }
+  std::vector<int32_t> st(np, 0);
+  if (rc == PSG_OK) {
+    hipError_t e = psg::launch_snappy((const uint8_t*)b, d_soff, np, nullptr, d_dst, d_cap, d_st,
+                                      c->copy);
+    if (e == hipSuccess) e = hipMemcpyAsync(st.data(), d_st, 4 * np, hipMemcpyDeviceToHost, c->copy);
+    if (e == hipSuccess) e = hipStreamSynchronize(c->copy);
+    if (e != hipSuccess) rc = fail(PSG_ERR_DEVICE, "snappy: %s", hipGetErrorString(e));
+  }
+  c->pinned_wait = false;  // the copy stream is idle
+  c->dev_put(blk, tb + meta);
+  for (int i = 0; rc == PSG_OK && i < np; ++i)
+    if (st[i]) rc = fail(st[i], "compressed part %d: %s", i, psg_status_string(st[i]));
+  if (rc != PSG_OK) {
+    c->dev_put(vblock, m * vb);
+    return rc;
+  }
+  return c->push_values(chl, time, kb, ke, k, m, nullptr, vblock);
 }
 
 int psg_push_cached(psg_ctx* c, int sender, int chl, int time, uint64_t kb, uint64_t ke,

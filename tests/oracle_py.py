@@ -54,6 +54,9 @@ def orc() -> C.CDLL:
             "orc_cm_insert": (None, [_p, C.c_uint32, C.c_int, _p, _p, _sz]),
             "orc_cm_query": (C.c_uint8, [_p, C.c_uint32, C.c_int, _u64]),
             "orc_ff_query": (_sz, [_p, C.c_uint32, C.c_int, _p, _sz, C.c_int, _p]),
+            "orc_snappy_uncompressed_length": (C.c_int, [_p, _sz, _psz]),
+            "orc_snappy_uncompress": (C.c_int, [_p, _sz, _p, _sz]),
+            "orc_snappy_compress": (_sz, [_p, _sz, _p]),
             "orc_crc32c_extend": (C.c_uint32, [C.c_uint32, _p, _sz]),
             "orc_crc32c_mask": (C.c_uint32, [C.c_uint32]),
             "orc_crc32c_unmask": (C.c_uint32, [C.c_uint32]),
@@ -236,3 +239,23 @@ def ff_query(table, n, k, keys, freq):
     out = np.empty(max(1, keys.size), np.uint64)
     m = orc().orc_ff_query(_a(table), n, k, _a(keys), keys.size, freq, _a(out))
     return out[:m].copy()
+
+
+# ---- snappy raw format (google/snappy; absent from the reference tree) -----
+def snappy_compress(data: bytes) -> bytes:
+    src = np.frombuffer(data, np.uint8) if data else np.zeros(1, np.uint8)
+    out = np.zeros(32 + len(data) + len(data) // 6, np.uint8)
+    n = orc().orc_snappy_compress(_a(src), len(data), _a(out))
+    return out[:n].tobytes()
+
+
+def snappy_uncompress(data: bytes):
+    """bytes, or None for a corrupt stream (RawUncompress false)."""
+    src = np.frombuffer(data, np.uint8) if data else np.zeros(1, np.uint8)
+    ln = C.c_size_t()
+    if orc().orc_snappy_uncompressed_length(_a(src), len(data), C.byref(ln)) < 0:
+        return None
+    out = np.zeros(max(1, ln.value), np.uint8)
+    if orc().orc_snappy_uncompress(_a(src), len(data), _a(out), ln.value) != 0:
+        return None
+    return out[: ln.value].tobytes()

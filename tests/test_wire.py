@@ -335,3 +335,128 @@ def test_hold_buffers_option():
         _, _, _, want, _ = O.aggregate(D, 0, (1 << 64) - 1, pushes)
         assert np.array_equal(_bits(got), _bits(want[0]))
     v.close()
+
+
+# ------------------------------------------------------------- snappy ----
+# Spec-derived known answers (snappy format_description.txt; no snappy
+# vectors ship with the reference): preamble varint, literal, copy-1,
+# overlapping copy-2 (run length), a 4-byte-offset copy, long literals.
+SNAPPY_KNOWN = [
+    (bytes([0x0b, 0x28]) + b"hello world", b"hello world"),
+    # "abc" literal + copy of 9 at offset 3 (1-byte offset tag 0x15)
+    (bytes([0x0c, 0x08]) + b"abc" + bytes([0x15, 0x03]), b"abcabcabcabc"),
+    # "a" + copy-2 of 20 at offset 1 (run of 'a'), tag 2 | (19 << 2)
+    (bytes([0x15, 0x00]) + b"a" + bytes([2 | (19 << 2), 0x01, 0x00]), b"a" * 21),
+    # "xy" + copy-4 of 6 at offset 2, tag 3 | (5 << 2)
+    (bytes([0x08, 0x04]) + b"xy" + bytes([3 | (5 << 2), 2, 0, 0, 0]), b"xyxyxyxy"),
+    # a 61..256-byte literal: tag 60 << 2, one length byte (len - 1)
+    (bytes([0xc8, 0x01, 60 << 2, 199]) + bytes(range(200)), bytes(range(200))),
+]
+
+
+def test_snappy_oracle_known_and_roundtrip():
+    for comp, want in SNAPPY_KNOWN:
+        assert O.snappy_uncompress(comp) == want
+    rng = np.random.default_rng(2)
+    keys = np.sort(rng.integers(0, 1 << 40, 20000, dtype=np.uint64)).tobytes()
+    nanrun = np.full(5000, np.nan).view(np.uint64)
+    nanrun[:] = np.uint64(0xFFFFFFFFFFFFFFFF)  # Darling's inactive sentinel compresses
+    for data in (b"", b"a", keys, nanrun.tobytes(), rng.integers(0, 256, 200000, dtype=np.uint8).tobytes(),
+                 b"abcd" * 70000):
+        c = O.snappy_compress(data)
+        assert O.snappy_uncompress(c) == data
+    assert len(O.snappy_compress(nanrun.tobytes())) < 4000
+    # corrupt: offset beyond the output, truncated literal, length mismatch
+    assert O.snappy_uncompress(bytes([0x04, 0x01, 0x05])) is None
+    assert O.snappy_uncompress(bytes([0x05, 0x10, 0x61])) is None
+    assert O.snappy_uncompress(bytes([0x06, 0x04]) + b"ab") is None
+
+
+def _gpu_snappy(parts, caps):
+    import torch
+    from parameter_server_amd import _lib
+    L = _lib.lib()
+    soff = np.concatenate([[0], np.cumsum([len(p) for p in parts])]).astype(np.uint64)
+    doff = np.concatenate([[0], np.cumsum(caps)]).astype(np.uint64)
+    blob = b"".join(parts) + b"\0"
+    ds = torch.tensor(np.frombuffer(blob, np.uint8).copy(), device="cuda")
+    dd = torch.zeros(int(doff[-1]) + 1, dtype=torch.uint8, device="cuda")
+    dso = torch.tensor(soff.view(np.int64), device="cuda")
+    ddo = torch.tensor(doff.view(np.int64), device="cuda")
+    st = torch.full((len(parts),), 7, dtype=torch.int32, device="cuda")
+    _lib.check(L.psg_snappy_uncompress_dev(ds.data_ptr(), dso.data_ptr(), len(parts),
+                                           dd.data_ptr(), ddo.data_ptr(), st.data_ptr(), None))
+    out = dd.cpu().numpy().tobytes()
+    return [out[int(doff[i]):int(doff[i + 1])] for i in range(len(parts))], st.cpu().tolist()
+
+
+@pytest.mark.gpu
+def test_gpu_snappy_batched_parts_vs_oracle():
+    """Many message parts in one launch: the spec-derived streams, the
+    oracle compressor's output for key arrays, f32/f64 values, NaN-sentinel
+    runs, random bytes (literals of every length encoding), multi-block
+    (> 64 KB) parts and an empty part -- byte-exact; corrupt parts report
+    PSG_ERR_ARG / PSG_ERR_SIZE without disturbing their neighbours."""
+    import torch
+    assert torch.cuda.is_available()
+    from parameter_server_amd import _lib
+    rng = np.random.default_rng(4)
+    datas = [w for _, w in SNAPPY_KNOWN]
+    parts = [c for c, _ in SNAPPY_KNOWN]
+    extra = [np.sort(rng.integers(0, 1 << 40, 30000, dtype=np.uint64)).tobytes(),
+             rng.standard_normal(40000).astype(np.float32).tobytes(),
+             np.full(70000, 0xFFFFFFFFFFFFFFFF, np.uint64).tobytes(),
+             rng.integers(0, 256, 300000, dtype=np.uint8).tobytes(),
+             (b"parameter server " * 20000),
+             b""]
+    for d in extra:
+        datas.append(d)
+        parts.append(O.snappy_compress(d))
+    got, st = _gpu_snappy(parts, [len(d) for d in datas])
+    assert st == [0] * len(parts)
+    for g, d in zip(got, datas):
+        assert g == d
+    # corrupt parts among good ones
+    bad = [bytes([0x04, 0x01, 0x05]), parts[1], bytes([0x06, 0x04]) + b"ab", parts[0]]
+    got, st = _gpu_snappy(bad, [4, 12, 6, 11])
+    assert st[0] == _lib.PSG_ERR_ARG and st[2] == _lib.PSG_ERR_ARG
+    assert st[1] == 0 and got[1] == datas[1] and st[3] == 0 and got[3] == datas[0]
+    got, st = _gpu_snappy([parts[0]], [12])  # declared 11 bytes, caller expects 12
+    assert st == [_lib.PSG_ERR_SIZE]
+
+
+@pytest.mark.gpu
+def test_gpu_push_compressed_matches_plain_push():
+    """psg_push_compressed: snappy parts off the wire (keys + m value parts),
+    decompressed on the device and merged -- the same bits as plain pushes;
+    a corrupt part and inconsistent part sizes are refused."""
+    import ctypes as C
+    import torch
+    assert torch.cuda.is_available()
+    from parameter_server_amd import _lib, synth
+    from parameter_server_amd.kv_vector import KVVector, Message
+    D, pushes = synth.overlap_pushes(seed=33, npush=6, n=50000)
+    v = KVVector(0)
+    v.setValue(Message(key=D))
+    L = v._L
+
+    def cpush(t, k, vals, corrupt=False):
+        ck = O.snappy_compress(np.ascontiguousarray(k).tobytes())
+        if corrupt:
+            ck = ck[:len(ck) // 2]
+        cv = [O.snappy_compress(np.ascontiguousarray(x).tobytes()) for x in vals]
+        bufs = [C.create_string_buffer(b, len(b)) for b in cv]
+        arr = _lib.ptr_array([C.cast(b, C.c_void_p).value for b in bufs])
+        sizes = (C.c_size_t * len(cv))(*[len(b) for b in cv])
+        return L.psg_push_compressed(v._h, 0, t, 0, (1 << 64) - 1, ck, len(ck), len(cv), arr,
+                                     sizes)
+
+    for k, vals in pushes:
+        _lib.check(cpush(3, k, vals))
+    (_, got), = v.received(3)
+    _, _, _, want, _ = O.aggregate(D, 0, (1 << 64) - 1, pushes)
+    assert np.array_equal(got.view(np.uint32), want[0].view(np.uint32))
+    k, vals = pushes[0]
+    assert cpush(4, k, vals, corrupt=True) == _lib.PSG_ERR_ARG
+    assert cpush(4, k, [vals[0][:-1]]) == _lib.PSG_ERR_SIZE
+    v.close()
