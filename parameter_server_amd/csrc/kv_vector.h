@@ -65,11 +65,17 @@ struct Task {
   Range<Key> key_range = Range<Key>::all();
   bool request = true;
   bool push = true;  // CallSharedPara::PUSH vs PULL
+  // key cache fields (task.proto; RNode::cacheKeyRecver, remote_node.cc:139-184)
+  bool has_key_signature = false;
+  uint32_t key_signature = 0;
+  bool has_key = true;
+  bool erase_key_cache = false;
 };
 
 // PS::Message (message.h:17-87): task header + key bytes + value arrays.
 struct Message {
   Task task;
+  int sender = 0;  // the remote node (one key cache per node)
   std::vector<Key> key;
   std::vector<std::vector<char>> value;  // each: n * sizeof(V) bytes
   bool valid = true;
@@ -164,8 +170,26 @@ class KVVector {
     return out;
   }
 
-  // setValue (kv_vector.h:75-82 -> serialSetValue / parallelSetValue)
+  // setValue (kv_vector.h:75-82 -> serialSetValue / parallelSetValue); a
+  // message with key-cache fields goes through the receiver's key cache
+  // first (RNode::cacheKeyRecver): without keys it uses the resident copy
   void setValue(const MessagePtr& msg) {
+    const Task& t = msg->task;
+    if (t.has_key_signature || !t.has_key || t.erase_key_cache) {
+      const unsigned kc = (t.has_key_signature ? PSG_KC_SIG : 0u) |
+                          (t.has_key ? PSG_KC_KEYS : 0u) | (t.erase_key_cache ? PSG_KC_ERASE : 0u);
+      std::vector<const void*> vals;
+      size_t nv = 0;
+      for (const auto& v : msg->value) {
+        vals.push_back(v.data());
+        nv = v.size() / sizeof(V);
+      }
+      check(psg_push_cached(ctx_.get(), msg->sender, t.key_channel, t.time, t.key_range.begin(),
+                            t.key_range.end(), kc, t.key_signature,
+                            t.has_key ? msg->key.data() : nullptr, t.has_key ? msg->key.size() : 0,
+                            (int)vals.size(), vals.data(), nv));
+      return;
+    }
     const auto& k = msg->key;
     if (k.empty()) return;                                   // :90, :177
     if (msg->value.empty()) {                                // key-only push :178-182
@@ -192,6 +216,54 @@ class KVVector {
     check(psg_gather(ctx_.get(), msg->task.key_channel, k.data(), k.size(), out.data(),
                      &matched));
     msg->addValue(out);
+  }
+
+  // snappy-compressed parts off the wire (Van::recv, van.cc:204-214)
+  void setValueCompressed(const Task& t, const std::vector<char>& ckeys,
+                          const std::vector<std::vector<char>>& cvals) {
+    std::vector<const void*> p;
+    std::vector<size_t> n;
+    for (const auto& v : cvals) {
+      p.push_back(v.data());
+      n.push_back(v.size());
+    }
+    check(psg_push_compressed(ctx_.get(), t.key_channel, t.time, t.key_range.begin(),
+                              t.key_range.end(), ckeys.data(), ckeys.size(), (int)p.size(),
+                              p.data(), n.data()));
+  }
+
+  // tail-feature filter of a channel (SharedParameter::key_filter_,
+  // shared_parameter.h:114-133; FreqencyFilter / CountMin)
+  bool keyFilterEmpty(int channel) const {
+    int e = 1;
+    check(psg_freq_empty(ctx_.get(), channel, &e));
+    return e != 0;
+  }
+  void keyFilterResize(int channel, int n, int k) {
+    check(psg_freq_resize(ctx_.get(), channel, n, k));
+  }
+  void keyFilterInsert(int channel, const std::vector<Key>& key,
+                       const std::vector<uint32_t>& count) {
+    if (key.size() != count.size()) throw Error(PSG_ERR_SIZE, "key/count sizes");  // :37
+    check(psg_freq_insert(ctx_.get(), channel, key.data(), count.data(), key.size()));
+  }
+  std::vector<Key> keyFilterQuery(int channel, const std::vector<Key>& key, int freq) {
+    std::vector<Key> out(key.size());
+    size_t n = 0;
+    check(psg_freq_query(ctx_.get(), channel, key.data(), key.size(), freq, out.data(), &n));
+    out.resize(n);
+    return out;
+  }
+
+  // Darling's server update on the resident aggregate (darling.cc:245-262,
+  // 437-477); value arrays are double (KVVector<Key,double>)
+  void darlingInit(int channel, double delta_init) {
+    check(psg_darling_init(ctx_.get(), channel, delta_init));
+  }
+  double darlingUpdate(int channel, int time, const psg_darling_param& p) {
+    double vio = 0;
+    check(psg_darling_update(ctx_.get(), channel, time, &p, &vio));
+    return vio;
   }
 
   // slice (kv_vector.h:230-235 -> sliceKeyOrderedMsg, message.h:89-123):

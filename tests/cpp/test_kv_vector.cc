@@ -170,6 +170,107 @@ static void random_vs_oracle(bool parallel, unsigned seed) {
   EXPECT(status == PSG_ERR_UNMATCHED);
 }
 
+// ---- GPU: the rows around the merge, through the adapter ----
+// the receiver's key cache: iteration 1 carries keys + signature, iteration
+// 2 only the signature; both merges equal plain pushes (oracle)
+static void key_cache_and_filter() {
+  std::mt19937_64 rng(7);
+  std::set<Key> ks;
+  while (ks.size() < 6000) ks.insert(rng() >> 20);
+  std::vector<Key> D(ks.begin(), ks.end());
+  KVVector<float> kv;
+  kv.setValue(key_msg(D));
+  std::vector<std::vector<Key>> pk;
+  std::vector<std::vector<float>> pv;
+  for (int w = 0; w < 3; ++w) {
+    std::vector<Key> k;
+    for (size_t i = w; i < D.size(); i += 2 + w) k.push_back(D[i]);
+    std::vector<float> v(k.size());
+    for (auto& x : v) x = (float)((int)(rng() % 2001) - 1000) / 256.0f;
+    pk.push_back(k);
+    pv.push_back(v);
+  }
+  for (int t = 1; t <= 2; ++t) {
+    for (int w = 0; w < 3; ++w) {
+      MessagePtr m(new Message());
+      m->task.time = t;
+      m->sender = w;
+      m->task.has_key_signature = true;
+      m->task.key_signature = orc_crc32c_extend(0, pk[w].data(),
+                                                std::min<size_t>(8 * pk[w].size(), 2048));
+      m->task.has_key = t == 1;
+      if (t == 1) m->key = pk[w];
+      m->addValue(pv[w]);
+      kv.setValue(m);
+    }
+    auto got = kv.received(t);
+    std::vector<float> want(D.size());
+    const uint64_t* keys[3] = {pk[0].data(), pk[1].data(), pk[2].data()};
+    const size_t n[3] = {pk[0].size(), pk[1].size(), pk[2].size()};
+    const float* vals[3] = {pv[0].data(), pv[1].data(), pv[2].data()};
+    float* out[1] = {want.data()};
+    size_t lo, hi, matched[3];
+    orc_aggregate_f32(D.data(), D.size(), 0, ~0ull, 3, keys, n, 1, vals, 0, 1, out, &lo, &hi,
+                      matched);
+    EXPECT(got.size() == 1 && same_bits(got[0].second, want));
+  }
+  // FreqencyFilter: insertKeys then queryKeys against the oracle's CountMin
+  kv.keyFilterResize(0, 5000, 3);
+  EXPECT(!kv.keyFilterEmpty(0));
+  std::vector<uint32_t> cnt(D.size());
+  for (auto& c : cnt) c = (uint32_t)(rng() % 700);
+  kv.keyFilterInsert(0, D, cnt);
+  std::vector<uint8_t> table(5000, 0);
+  orc_cm_insert(table.data(), 5000, 3, D.data(), cnt.data(), D.size());
+  std::vector<Key> want(D.size());
+  want.resize(orc_ff_query(table.data(), 5000, 3, D.data(), D.size(), 100, want.data()));
+  EXPECT(kv.keyFilterQuery(0, D, 100) == want);
+}
+
+// Darling's fused server update against the oracle's updateWeight
+static void darling() {
+  std::mt19937_64 rng(11);
+  std::vector<Key> D;
+  for (Key k = 0; k < 3000; ++k) D.push_back(k * 977 + 5);
+  KVVector<double> kv;
+  kv.setValue(key_msg(D));
+  std::vector<double> w(D.size(), 0.0), delta(D.size(), 1.0);
+  std::vector<uint8_t> act(D.size(), 1);
+  kv.setValueArray(0, w);
+  kv.darlingInit(0, 1.0);
+  const psg_darling_param P = {0.7, 0.2, 1e20, 4.0};
+  for (int t = 1; t <= 3; ++t) {
+    std::vector<Key> k;
+    for (size_t i = t; i < D.size(); i += 3) k.push_back(D[i]);
+    std::vector<double> g(k.size()), u(k.size());
+    for (size_t i = 0; i < k.size(); ++i) {
+      g[i] = (double)((int)(rng() % 2001) - 1000) / 300.0;
+      u[i] = (double)(rng() % 1000) / 400.0;
+    }
+    MessagePtr m = key_msg(k);
+    m->task.time = t;
+    m->addValue(g);
+    m->addValue(u);
+    kv.setValue(m);
+    const double vio = kv.darlingUpdate(0, t, P);
+    // the oracle: aggregate (m = 2) then updateWeight over [0, n)
+    std::vector<double> G(D.size()), U(D.size());
+    const uint64_t* keys[1] = {k.data()};
+    const size_t n[1] = {k.size()};
+    const double* vals[2] = {g.data(), u.data()};
+    double* out[2] = {G.data(), U.data()};
+    size_t lo, hi, matched[1];
+    orc_aggregate_f64(D.data(), D.size(), 0, ~0ull, 1, keys, n, 2, vals, 0, 1, out, &lo, &hi,
+                      matched);
+    double want_vio = 0;
+    orc_darling_update_weight(w.data(), delta.data(), act.data(), 0, D.size(), G.data(),
+                              U.data(), P.eta, P.lambda, P.kkt_filter_threshold, P.delta_max,
+                              &want_vio);
+    EXPECT(std::memcmp(&vio, &want_vio, sizeof(double)) == 0);
+  }
+  EXPECT(same_bits(kv.value(0), w));
+}
+
 int main(int argc, char** argv) {
   const std::string mode = argc > 1 ? argv[1] : "host";
   try {
@@ -180,6 +281,8 @@ int main(int argc, char** argv) {
       random_vs_oracle<float>(false, 1);
       random_vs_oracle<float>(true, 2);
       random_vs_oracle<double>(false, 3);
+      key_cache_and_filter();
+      darling();
     }
   } catch (const std::exception& e) {
     std::fprintf(stderr, "uncaught: %s\n", e.what());
