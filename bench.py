@@ -271,6 +271,7 @@ def main():
         result["cfg5"] = cfg5_block(args, rank, world, bounds, dist, dev, local, stream)
     if rank == 0 and world == 1 and not args.no_cpu_baseline and wl == "cfg2":
         result["end_to_end"] = end_to_end(insts[0], local)
+        result["rows"] = bench_rows(local)
         result["cpu_baseline"] = cpu_baseline(insts[0], args.cpu_seconds)
     if rank == 0:
         print(json.dumps(result), flush=True)
@@ -498,6 +499,146 @@ def load_traffic(bytes_per_launch, workload):
     return {"tile": d.get("hbm_bytes_per_launch"),
             "partition": d.get("partition_hbm_bytes_per_launch"),
             "source": d.get("source")}
+
+
+def bench_rows(device, reps=5):
+    """The SURVEY 8(f) rows beside the merge, each on device-resident input
+    with its own HBM roofline: algorithmic bytes / mean kernel time (HIP
+    events on the stream the kernel runs on).  Shapes: the pull of a cfg2
+    shard, crc32c key signatures of 65,536 pushes and one 1 GiB stream,
+    snappy parts of 64 KB, Darling over 16.8 M f64 positions, CountMin
+    insert/query of 16.8 M keys into 2^26 counters."""
+    import ctypes as C
+    import torch
+    from parameter_server_amd import _lib, synth
+    L = _lib.lib()
+    dev = torch.device("cuda", device)
+    st = torch.cuda.current_stream()
+    out = {}
+
+    def timed(fn):
+        fn()
+        torch.cuda.synchronize()
+        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        e0.record(st)
+        for _ in range(reps):
+            fn()
+        e1.record(st)
+        torch.cuda.synchronize()
+        return e0.elapsed_time(e1) / reps  # ms
+
+    def row(name, ms, nbytes, unit_count, unit):
+        gbps = nbytes / (ms * 1e-3) / 1e9
+        out[name] = {"ms": ms, "algorithmic_bytes": nbytes, "GBps": gbps,
+                     "frac": gbps / HBM_PEAK_GBPS, "rate": unit_count / (ms * 1e-3),
+                     "unit": unit}
+
+    rng = np.random.default_rng(3)
+    # pull gather (getValue) of 1 M sorted request keys from a cfg2 shard
+    D, pushes = synth.overlap_pushes(1)
+    req = np.sort(np.concatenate([k for k, _ in pushes[:8]]))[::1]
+    dD = torch.from_numpy(D.view(np.int64)).to(dev)
+    dW = torch.from_numpy(rng.standard_normal(D.size).astype(np.float32)).to(dev)
+    dR = torch.from_numpy(req.view(np.int64)).to(dev)
+    dO = torch.empty(req.size, dtype=torch.float32, device=dev)
+    dM = torch.zeros(1, dtype=torch.int64, device=dev)
+    ms = timed(lambda: _lib.check(L.psg_gather_dev(_lib.PSG_F32, dD.data_ptr(), D.size,
+                                                   dW.data_ptr(), dR.data_ptr(), req.size,
+                                                   dO.data_ptr(), dM.data_ptr(), None)))
+    row("gather", ms, req.size * (8 + 4 + 4), req.size, "keys/s")
+    del dD, dW, dR, dO
+    # crc32c: key signatures (2048 B of each of 65,536 pushes) and one 1 GiB stream
+    nsig = 65536
+    blob = torch.randint(0, 255, (nsig * 4096,), dtype=torch.uint8, device=dev)
+    off = torch.arange(0, nsig + 1, dtype=torch.int64, device=dev) * 4096
+    sig = torch.empty(nsig, dtype=torch.int32, device=dev)
+    ms = timed(lambda: _lib.check(L.psg_crc32c_dev(blob.data_ptr(), off.data_ptr(), nsig,
+                                                   _lib.PSG_MAX_SIG_LEN, None, sig.data_ptr(),
+                                                   None)))
+    row("crc32c_signatures", ms, nsig * 2048, nsig, "signatures/s")
+    big = torch.randint(0, 255, (1 << 30,), dtype=torch.uint8, device=dev)
+    off1 = torch.tensor([0, 1 << 30], dtype=torch.int64, device=dev)
+    ms = timed(lambda: _lib.check(L.psg_crc32c_dev(big.data_ptr(), off1.data_ptr(), 1, 1 << 30,
+                                                   None, sig.data_ptr(), None)))
+    row("crc32c_stream", ms, 1 << 30, 1 << 30, "bytes/s")
+    del blob, big
+    # snappy: 2048 parts of 64 KB, each a synthetic raw stream of alternating
+    # 16-byte literals and 16-byte copies (2-byte offsets): 4096 elements per
+    # part, the element density of typical snappy output
+    nparts, plen = 2048, 65536
+
+    def part(seed):
+        r = np.random.default_rng(seed)
+        b = bytearray([0x80, 0x80, 0x04])  # varint 65536
+        o = 0
+        while o < plen:
+            b.append(15 << 2)  # literal of 16
+            b += r.integers(0, 256, 16, dtype=np.uint8).tobytes()
+            o += 16
+            off = int(r.integers(1, min(o, 4096) + 1))
+            b += bytes([2 | (15 << 2), off & 0xff, off >> 8])  # copy of 16
+            o += 16
+        return bytes(b)
+
+    parts = [part(i % 16) for i in range(nparts)]
+    soff = np.concatenate([[0], np.cumsum([len(x) for x in parts])]).astype(np.uint64)
+    dsrc = torch.from_numpy(np.frombuffer(b"".join(parts), np.uint8).copy()).to(dev)
+    dso = torch.from_numpy(soff.view(np.int64)).to(dev)
+    ddo = torch.arange(0, nparts + 1, dtype=torch.int64, device=dev) * plen
+    ddst = torch.empty(nparts * plen, dtype=torch.uint8, device=dev)
+    dst_ = torch.empty(nparts, dtype=torch.int32, device=dev)
+    ms = timed(lambda: _lib.check(L.psg_snappy_uncompress_dev(
+        dsrc.data_ptr(), dso.data_ptr(), nparts, ddst.data_ptr(), ddo.data_ptr(),
+        dst_.data_ptr(), None)))
+    assert int(dst_.abs().sum().item()) == 0, "snappy row: a part failed to decode"
+    row("snappy_uncompress", ms, int(soff[-1]) + nparts * plen, nparts * plen,
+        "uncompressed bytes/s")
+    del dsrc, ddst
+    # CountMin: insertKeys / queryKeys of 16.8 M keys, 2^26 counters, k = 4
+    from parameter_server_amd.kv_vector import KVVector, Message
+    v = KVVector(device)
+    nk = 1 << 24
+    keys = torch.randint(0, 1 << 62, (nk,), dtype=torch.int64, device=dev)
+    cnt = torch.randint(1, 100, (nk,), dtype=torch.int32, device=dev)
+    _lib.check(L.psg_freq_resize(v._h, 0, 1 << 26, 4))
+    ms = timed(lambda: _lib.check(L.psg_freq_insert_dev(v._h, 0, keys.data_ptr(),
+                                                        cnt.data_ptr(), nk, None)))
+    row("countmin_insert", ms, nk * (8 + 4) + nk * 4 * 8, nk, "keys/s")
+    scratch = torch.empty(L.psg_freq_query_scratch_bytes(nk), dtype=torch.uint8, device=dev)
+    qo = torch.empty(nk, dtype=torch.int64, device=dev)
+    qn = torch.zeros(1, dtype=torch.int64, device=dev)
+    ms = timed(lambda: _lib.check(L.psg_freq_query_dev(v._h, 0, keys.data_ptr(), nk, 200,
+                                                       qo.data_ptr(), qn.data_ptr(),
+                                                       scratch.data_ptr(), None)))
+    kept = int(qn.item())
+    row("countmin_query", ms, nk * 8 * 2 + nk * 4 * 4 * 2 + kept * 8, nk, "keys/s")
+    v.close()
+    del keys, cnt, qo, scratch
+    # Darling's server step over 16.8 M f64 positions: the (G, U) aggregate of
+    # one resident push plus the fused updateWeight (nothing crosses PCIe)
+    n = 1 << 24
+    Dk = np.arange(n, dtype=np.uint64) * np.uint64(3)
+    v = KVVector(device, _lib.PSG_F64)
+    v.setValue(Message(key=Dk))
+    v.set_value_array(0, np.zeros(n))
+    _lib.check(L.psg_darling_init(v._h, 0, 1.0))
+    G = rng.standard_normal(n)
+    U = rng.random(n)
+    P = (C.c_double * 4)(1.0, 0.1, 1e20, 5.0)
+    vio = C.c_double()
+    times = []
+    for r in range(reps + 1):
+        v.setValue(Message(time=r, key=Dk, value=[G, U]))  # H2D here, untimed
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        _lib.check(L.psg_darling_update(v._h, 0, r, C.cast(P, C.c_void_p), C.byref(vio)))
+        if r:
+            times.append(time.perf_counter() - t0)
+    v.close()
+    ms = float(np.median(times)) * 1e3
+    # aggregate (dense: values in, sums out) + update (G, U, w, delta r/w)
+    row("darling_server_step", ms, n * 16 + n * 16 + n * (16 + 16 + 16), n, "positions/s")
+    return out
 
 
 def cpu_baseline(inst, seconds):
