@@ -26,26 +26,78 @@ namespace {
 // gather (pull reply): out[i] = W[pos(req[i])], 0 where absent or where
 // req[i] repeats req[i-1] (the reference merge walk advances past a match,
 // message.h:256-260, so a repeated request key reads 0).
+//
+// A workgroup takes kGR consecutive (sorted) requests.  Two 64-ary wave
+// searches bound their server positions, [lower_bound(first),
+// upper_bound(last)); when that span fits kGS keys (a dense pull) it is
+// staged in LDS with one coalesced read and every request searches there,
+// otherwise (a sparse pull) each searches the span in global memory.  Each
+// thread keeps kGR/256 requests in flight so their loads overlap.
 // ----------------------------------------------------------------------
+constexpr int kGR = 1024;  // requests per workgroup
+constexpr int kGS = 4096;  // server keys staged in LDS (32 KB)
+
 template <typename V>
 __global__ __launch_bounds__(256) void gather_kernel(
     const uint64_t* __restrict__ D, uint64_t nd, const V* __restrict__ W,
     const uint64_t* __restrict__ req, uint64_t nreq, V* __restrict__ out,
     unsigned long long* __restrict__ matched) {
-  const uint64_t i = (uint64_t)blockIdx.x * 256u + threadIdx.x;
-  bool found = false;
-  if (i < nreq) {
-    const uint64_t k = req[i];
-    const uint64_t pos = gl_lower_bound(D, nd, k);
-    V v = V(0);
-    if (pos < nd && D[pos] == k && (i == 0 || req[i - 1] != k)) {
-      v = W[pos];
-      found = true;
-    }
-    out[i] = v;
+  constexpr int kI = kGR / 256;
+  __shared__ uint64_t t[kGS];
+  __shared__ uint64_t rg[2];
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  const uint64_t r0 = (uint64_t)blockIdx.x * kGR;
+  const uint64_t r1 = nreq - r0 < (uint64_t)kGR ? nreq : r0 + kGR;
+  if (w < 2) {
+    const uint64_t r = wave_search(D, nd, req[w == 0 ? r0 : r1 - 1], w == 1, lane);
+    if (lane == 0) rg[w] = r;
   }
-  const unsigned long long m = __ballot(found);
-  if ((threadIdx.x & 63) == 0 && m) atomicAdd(matched, (unsigned long long)__popcll(m));
+  __syncthreads();
+  const uint64_t lo = rg[0], hi = rg[1] > rg[0] ? rg[1] : rg[0];
+  const uint64_t n = hi - lo;
+  const bool staged = n <= (uint64_t)kGS;
+  if (staged) {
+    for (int j = threadIdx.x; j < (int)n; j += 256) t[j] = __builtin_nontemporal_load(D + lo + j);
+    __syncthreads();
+  }
+  uint64_t k[kI], pos[kI];
+  bool ok[kI];
+#pragma unroll
+  for (int q = 0; q < kI; ++q) {
+    const uint64_t i = r0 + (uint64_t)(q * 256 + threadIdx.x);
+    k[q] = i < r1 ? req[i] : 0;
+  }
+#pragma unroll
+  for (int q = 0; q < kI; ++q) {
+    const uint64_t i = r0 + (uint64_t)(q * 256 + threadIdx.x);
+    uint64_t p;
+    bool hit;
+    if (staged) {
+      const int lp = lds_lower_bound<kGS>(t, (int)n, k[q]);
+      p = lo + (uint64_t)lp;
+      hit = (uint64_t)lp < n && t[lp] == k[q];
+    } else {
+      p = lo + gl_lower_bound(D + lo, n, k[q]);
+      hit = p < hi && D[p] == k[q];
+    }
+    const bool rep = i > 0 && i < r1 && req[i - 1] == k[q];
+    ok[q] = i < r1 && hit && !rep;
+    pos[q] = ok[q] ? p : 0;
+  }
+  int found = 0;
+#pragma unroll
+  for (int q = 0; q < kI; ++q) {
+    const uint64_t i = r0 + (uint64_t)(q * 256 + threadIdx.x);
+    if (i < r1) {
+      const V x = nd ? W[pos[q]] : V(0);  // W[0] stands in for a miss
+      out[i] = ok[q] ? x : V(0);
+      found += ok[q];
+    }
+  }
+  // per-wave total, one atomic per wave
+#pragma unroll
+  for (int d = 32; d > 0; d >>= 1) found += __shfl_xor(found, d, 64);
+  if (lane == 0 && found) atomicAdd(matched, (unsigned long long)found);
 }
 
 __global__ __launch_bounds__(256) void check_sorted_kernel(
@@ -224,7 +276,7 @@ hipError_t launch_gather(int dtype, const uint64_t* dkeys, uint64_t nd,
                          void* out, unsigned long long* matched,
                          hipStream_t stream) {
   if (nreq == 0) return hipSuccess;
-  const uint64_t blocks = (nreq + 255) / 256;
+  const uint64_t blocks = (nreq + kGR - 1) / kGR;
   if (dtype == 0)
     hipLaunchKernelGGL(gather_kernel<float>, dim3((uint32_t)blocks), dim3(256), 0,
                        stream, dkeys, nd, (const float*)dvals, req, nreq,

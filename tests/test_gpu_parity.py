@@ -236,6 +236,32 @@ def test_gather_vs_oracle(torch_cuda, dtype):
     assert_bitexact(m.value[0], want)
 
 
+def test_gather_tile_forms(torch_cuda):
+    """Both gather forms (1024 requests per workgroup): chunks whose server
+    span fits 4096 keys are staged in LDS, sparse chunks search global
+    memory; requests repeated, on 4096-key boundaries and outside D's
+    range."""
+    rng = np.random.default_rng(21)
+    D = np.unique(rng.integers(1 << 20, 1 << 44, 100000, dtype=np.uint64))
+    W = rng.standard_normal(D.size).astype(np.float32)
+    T = 4096
+    edges = D[T::T]
+    busy = D[3 * T:5 * T]  # two tiles with every key requested
+    quiet = rng.choice(D, 40)
+    req = np.sort(np.concatenate([
+        busy, quiet, edges, edges, edges - np.uint64(1),
+        np.array([0, 5, 1 << 60, (1 << 64) - 1], np.uint64),
+        rng.integers(0, 1 << 44, 300, dtype=np.uint64)]))
+    v = kvv(np.float32)
+    v.setValue(msg(D))
+    v.set_value_array(0, W)
+    m = msg(req)
+    got_m = v.getValue(m)
+    want, want_m = O.gather(D, W, req)
+    assert got_m == want_m
+    assert_bitexact(m.value[0], want)
+
+
 # ------------------------------------------- device-resident plans (bench path)
 def to_dev(torch, a):
     a = np.ascontiguousarray(a)
