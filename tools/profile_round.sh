@@ -2,6 +2,7 @@
 # GPU box: the round's committed evidence.  usage: tools/profile_round.sh r02
 #   ktrace/          rocprofv3 --kernel-trace --stats of the default bench (cfg2)
 #   ktrace_cfg5/     the same for --workload cfg5 (packed rounds, stream partition)
+#   ktrace_rows/     the same for the SURVEY 8(f) rows block (tools/run_rows.py)
 #   pmc/             cfg2 counters, one group per rocprofv3 --pmc pass (tools/pmc2.sh)
 #   pmc_cfg5/        cfg5 FETCH_SIZE / WRITE_SIZE / TCC passes
 #   pmc_summary.json HBM bytes per launch of the tile and partition kernels (cfg2;
@@ -16,6 +17,7 @@ mkdir -p $OUT
 timeout -k 10 600 rocprofv3 --kernel-trace --stats --output-format csv -d $OUT/ktrace -o run -- python3 bench.py --no-cpu-baseline > $OUT/ktrace.json 2> $OUT/ktrace.err || { echo "ktrace failed"; tail -5 $OUT/ktrace.err; exit 1; }
 BPL=$(python3 -c "import json;print(json.load(open('$OUT/ktrace.json'))['roofline']['bytes_per_launch'])") || exit 1
 timeout -k 10 600 rocprofv3 --kernel-trace --stats --output-format csv -d $OUT/ktrace_cfg5 -o run -- python3 bench.py --no-cpu-baseline --workload cfg5 > $OUT/ktrace_cfg5.json 2> $OUT/ktrace_cfg5.err || { echo "ktrace cfg5 failed"; tail -5 $OUT/ktrace_cfg5.err; exit 1; }
+timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d $OUT/ktrace_rows -o run -- python3 tools/run_rows.py > $OUT/rows.json 2> $OUT/rows.err || { echo "ktrace rows failed"; tail -5 $OUT/rows.err; exit 1; }
 ./tools/pmc2.sh $OUT/pmc "--no-cfg5" > $OUT/pmc.log 2>&1 || { echo "pmc failed"; tail -5 $OUT/pmc.log; exit 1; }
 python3 tools/pmc_traffic.py $OUT/pmc/summary.json $BPL tile_kernel profiles/pmc_summary.json > $OUT/pmc_traffic.json || exit 1
 cp profiles/pmc_summary.json $OUT/pmc_summary.json
