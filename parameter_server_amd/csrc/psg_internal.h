@@ -85,7 +85,7 @@ hipError_t launch_partition(const JobDev* d_jobs, const uint32_t* d_split_item_j
 // every round holds one push (long pieces); psg_tile_packed.hip: rounds may
 // hold several pushes (many short pieces)
 hipError_t launch_aggregate_tile(int dtype, int m, const TileDesc* d_tiles, uint32_t ntiles,
-                                 hipStream_t stream);
+                                 bool wide, hipStream_t stream);
 hipError_t launch_aggregate_tile_packed(int dtype, int m, const TileDesc* d_tiles,
                                         uint32_t ntiles, hipStream_t stream);
 // psg_tile_dense.hip: every push of every job a contiguous slice of D

@@ -161,14 +161,22 @@ int forced_pack() {
   return e && (e[0] == '0' || e[0] == '1') ? e[0] - '0' : -1;
 }
 
+// PSG_WIDE=0|1 forces the tile kernel's push-group size (32 | 64).
+int forced_wide() {
+  const char* e = getenv("PSG_WIDE");
+  return e && (e[0] == '0' || e[0] == '1') ? e[0] - '0' : -1;
+}
+
 struct JobTable {
   int device = -1;
-  int knob_part = -1, knob_pack = -1;  // forced modes (read_knobs), -1 = chosen per build
+  int knob_part = -1, knob_pack = -1, knob_wide = -1;  // forced (read_knobs), -1 = chosen
   void read_knobs() {
     knob_part = forced_part_mode();
     knob_pack = forced_pack();
+    knob_wide = forced_wide();
   }
   bool pack = false;  // rounds may hold several pushes
+  bool wide = false;  // push groups of 64 in the tile kernel (a job has > 32 pushes)
   bool dense = false;  // every job dense: psg_tile_dense.hip, no partition
   int dtype = 0, m = 1;
   std::vector<JobDev> h;
@@ -285,6 +293,9 @@ struct JobTable {
     {
       const int fp = knob_pack;
       pack = fp >= 0 ? fp == 1 : (pieces_all > 0 && kv_all / pieces_all < kPackBelow);
+      uint32_t maxnp = 0;
+      for (const JobInfo& I : info) maxnp = std::max(maxnp, I.np);
+      wide = knob_wide >= 0 ? knob_wide == 1 : maxnp > 32;
     }
     size_t off = align_up(sizeof(JobDev) * jobs.size(), 256);
     const size_t tiles_off = off;
@@ -433,7 +444,7 @@ struct JobTable {
     else if (pack)
       HIP_TRY(psg::launch_aggregate_tile_packed(dtype, m, d_tiles, ntiles, s));
     else
-      HIP_TRY(psg::launch_aggregate_tile(dtype, m, d_tiles, ntiles, s));
+      HIP_TRY(psg::launch_aggregate_tile(dtype, m, d_tiles, ntiles, wide, s));
     return PSG_OK;
   }
 

@@ -41,6 +41,9 @@
 #include "psg_internal.h"
 
 #define AS1 __attribute__((address_space(1)))
+#ifndef KCAP64
+#define KCAP64 8
+#endif
 
 namespace psg {
 
@@ -61,8 +64,9 @@ constexpr int kNW = kNT / 64;    // waves
 constexpr int kSPT = kTS / kNT;  // slots per thread (contiguous)
 constexpr int kNB = 2 * kTS;     // buckets
 constexpr int kBPT = kNB / kNT;  // bucket-table entries per thread in the scan
-constexpr int kCap = 6;          // rounds a wave holds per pass
-constexpr int kGroup = 32;       // pushes per group (one lane of wave 0 each)
+// pushes per group (one lane of wave 0 each): 32, or 64 for jobs of more
+// than 32 pushes (one table phase and fewer, fuller passes per 64 pushes, at
+// 7 instead of 8 workgroups per CU)
 static_assert(kSPT == 4 && kBPT == 8, "layout");
 static_assert(kTS <= 0x7ffe, "u16 positions");
 
@@ -95,14 +99,15 @@ __device__ __forceinline__ uint32_t wave_scan_incl(uint32_t x) {
 
 // workgroups per CU the LDS allows (8 for the f32, m = 1 headline case):
 // the register budget follows it through __launch_bounds__
-template <typename V, int M>
+template <typename V, int M, int kGroup>
 constexpr int occupancy() {
-  constexpr int lds = 19328 + (int)(M * sizeof(V) - 4) * kTS + (M - 1) * 8 * kGroup;
+  constexpr int lds = 19328 + (int)(M * sizeof(V) - 4) * kTS + (M - 1) * 8 * kGroup +
+                      (kGroup - 32) * (4 + 2 * (kTS / 64) + 4 + 8 + 8);
   return 163840 / lds >= 8 ? 8 : 163840 / lds;
 }
 
-template <typename V, int M>
-__global__ __launch_bounds__(kNT, (occupancy<V, M>())) void tile_kernel(
+template <typename V, int M, int kGroup>
+__global__ __launch_bounds__(kNT, (occupancy<V, M, kGroup>())) void tile_kernel(
     const TileDesc* __restrict__ tiles, uint32_t ntiles) {
   __shared__ __attribute__((aligned(16))) uint64_t dk[kTS + 8];
   // bucket starts (u16); the histogram counts in it as packed pairs by 32-bit atomics
@@ -120,6 +125,10 @@ __global__ __launch_bounds__(kNT, (occupancy<V, M>())) void tile_kernel(
   __shared__ int pcarry;
   __shared__ uint32_t wsum[kNW];
 
+  // rounds a wave holds per pass: 6 at 8 workgroups per CU (64 VGPRs); the
+  // 64-push form runs 7 per CU and affords 8 (4 waves x 8 = 32 rounds: a
+  // group of 64 one-round pieces in 2 passes)
+  constexpr int kCap = kGroup == 64 ? KCAP64 : 6;
   const uint32_t w = uni((uint32_t)threadIdx.x >> 6);
   const int tid = threadIdx.x;
   const int lane = tid & 63;
@@ -451,18 +460,21 @@ __global__ __launch_bounds__(kNT, (occupancy<V, M>())) void tile_kernel(
 }
 
 template <typename V, int M>
-hipError_t go(const TileDesc* t, uint32_t n, hipStream_t s) {
-  hipLaunchKernelGGL((tile_kernel<V, M>), dim3(n), dim3(kNT), 0, s, t, n);
+hipError_t go(const TileDesc* t, uint32_t n, bool wide, hipStream_t s) {
+  if (wide)
+    hipLaunchKernelGGL((tile_kernel<V, M, 64>), dim3(n), dim3(kNT), 0, s, t, n);
+  else
+    hipLaunchKernelGGL((tile_kernel<V, M, 32>), dim3(n), dim3(kNT), 0, s, t, n);
   return hipGetLastError();
 }
 
 template <typename V>
-hipError_t launch_m(int m, const TileDesc* t, uint32_t n, hipStream_t s) {
+hipError_t launch_m(int m, const TileDesc* t, uint32_t n, bool wide, hipStream_t s) {
   switch (m) {
-    case 1: return go<V, 1>(t, n, s);
-    case 2: return go<V, 2>(t, n, s);
-    case 3: return go<V, 3>(t, n, s);
-    case 4: return go<V, 4>(t, n, s);
+    case 1: return go<V, 1>(t, n, wide, s);
+    case 2: return go<V, 2>(t, n, wide, s);
+    case 3: return go<V, 3>(t, n, wide, s);
+    case 4: return go<V, 4>(t, n, wide, s);
     default: return hipErrorInvalidValue;
   }
 }
@@ -470,10 +482,10 @@ hipError_t launch_m(int m, const TileDesc* t, uint32_t n, hipStream_t s) {
 }  // namespace
 
 hipError_t launch_aggregate_tile(int dtype, int m, const TileDesc* d_tiles, uint32_t ntiles,
-                                 hipStream_t stream) {
+                                 bool wide, hipStream_t stream) {
   if (ntiles == 0) return hipSuccess;
-  return dtype == 0 ? launch_m<float>(m, d_tiles, ntiles, stream)
-                    : launch_m<double>(m, d_tiles, ntiles, stream);
+  return dtype == 0 ? launch_m<float>(m, d_tiles, ntiles, wide, stream)
+                    : launch_m<double>(m, d_tiles, ntiles, wide, stream);
 }
 
 }  // namespace psg
