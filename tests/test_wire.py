@@ -412,6 +412,27 @@ def test_gpu_snappy_batched_parts_vs_oracle():
     for d in extra:
         datas.append(d)
         parts.append(O.snappy_compress(d))
+    # hand-built: a 70,000-byte literal (3-byte length), then 4-byte-offset
+    # copies reaching past the 64 KB ring (69,000 back) and inside it, and a
+    # run-length copy (offset 1): the decoder's far path reads its own
+    # earlier output from global memory
+    lit = rng.integers(0, 256, 70000, dtype=np.uint8).tobytes()
+    want = bytearray(lit)
+    for off, ln in ((69000, 64), (65537, 33), (100, 64), (1, 40)):
+        for _ in range(ln):
+            want.append(want[len(want) - off])
+    ulen, pre = len(want), bytearray()
+    while True:
+        pre.append((ulen & 0x7F) | (0x80 if ulen > 0x7F else 0))
+        ulen >>= 7
+        if not ulen:
+            break
+    s = pre + bytes([62 << 2]) + (len(lit) - 1).to_bytes(3, "little") + lit
+    for off, ln in ((69000, 64), (65537, 33), (100, 64), (1, 40)):
+        s += bytes([(ln - 1) << 2 | 3]) + off.to_bytes(4, "little")
+    assert O.snappy_uncompress(bytes(s)) == bytes(want)
+    datas.append(bytes(want))
+    parts.append(bytes(s))
     got, st = _gpu_snappy(parts, [len(d) for d in datas])
     assert st == [0] * len(parts)
     for g, d in zip(got, datas):
