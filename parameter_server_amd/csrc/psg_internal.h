@@ -99,6 +99,9 @@ hipError_t launch_gather(int dtype, const uint64_t* dkeys, uint64_t nd,
                          void* out, unsigned long long* matched,
                          hipStream_t stream);
 // keys strictly increasing?  *bad (device) += number of violations.
+// pinned host -> device copy read by the GPU (src: a device-visible host
+// address, 16-B aligned, as is dst)
+hipError_t launch_host_copy(void* dst, const void* src, size_t len, hipStream_t stream);
 hipError_t launch_check_sorted(const uint64_t* keys, uint64_t n,
                                unsigned long long* bad, hipStream_t stream,
                                bool strict = true);

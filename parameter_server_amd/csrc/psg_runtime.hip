@@ -551,13 +551,28 @@ struct CacheEntry {
   KeyRef keys;
 };
 
-bool host_pinned(const void* p) {
+// pinned host memory, and the address the device reads it at
+bool host_pinned(const void* p, const void** dev = nullptr) {
   hipPointerAttribute_t a;
   if (hipPointerGetAttributes(&a, p) != hipSuccess) {
     (void)hipGetLastError();  // pageable memory: not an error for us
     return false;
   }
-  return a.type == hipMemoryTypeHost;
+  if (a.type != hipMemoryTypeHost) return false;
+  if (dev) {
+    // the attribute's device pointer is the allocation's base: offset it
+    const char* hb = (const char*)a.hostPointer;
+    const char* db = (const char*)a.devicePointer;
+    *dev = (hb && db) ? (const void*)(db + ((const char*)p - hb)) : nullptr;
+  }
+  return true;
+}
+
+// PSG_ZERO_COPY=0 stages pinned buffers with DMA copies instead of the
+// zero-copy kernel (A/B and fallback knob; read at context creation)
+bool zero_copy_enabled() {
+  const char* e = getenv("PSG_ZERO_COPY");
+  return !(e && e[0] == '0');
 }
 
 // FreqencyFilter<uint64> of one channel (CountMin n_, k_, table)
@@ -702,10 +717,17 @@ struct psg_ctx {
   }
 
   bool pinned_wait = false;  // a pinned copy of this call is still in flight
+  bool zero_copy = true;     // pinned buffers read by a kernel, not a DMA copy
   int h2d(void* dst, const void* src, size_t len) {
     if (!len) return PSG_OK;
-    if (host_pinned(src)) {
-      HIP_TRY(hipMemcpyAsync(dst, src, len, hipMemcpyHostToDevice, copy));
+    const void* sdev = nullptr;
+    if (host_pinned(src, &sdev)) {
+      // the GPU reads the caller's pinned buffer itself when both ends are
+      // 16-B aligned (a DMA copy's fixed cost dominates at push sizes)
+      if (zero_copy && sdev && (((uintptr_t)sdev | (uintptr_t)dst) & 15u) == 0)
+        HIP_TRY(psg::launch_host_copy(dst, sdev, len, copy));
+      else
+        HIP_TRY(hipMemcpyAsync(dst, src, len, hipMemcpyHostToDevice, copy));
       pinned_wait = !(flags & PSG_HOLD_BUFFERS);
       return PSG_OK;
     }
@@ -721,6 +743,19 @@ struct psg_ctx {
       fly.push_back(Flight{off, piece, e});
       done += piece;
     }
+    return PSG_OK;
+  }
+
+  // device -> host on `stream`: into pinned memory the GPU writes itself
+  // (zero-copy kernel, no DMA fixed cost), else a DMA copy
+  int d2h(void* dst, const void* src, size_t len) {
+    if (!len) return PSG_OK;
+    const void* ddev = nullptr;
+    if (zero_copy && host_pinned(dst, &ddev) && ddev &&
+        (((uintptr_t)ddev | (uintptr_t)src) & 15u) == 0)
+      HIP_TRY(psg::launch_host_copy((void*)ddev, src, len, stream));
+    else
+      HIP_TRY(hipMemcpyAsync(dst, src, len, hipMemcpyDeviceToHost, stream));
     return PSG_OK;
   }
 
@@ -1024,6 +1059,7 @@ int psg_create(int device, int dtype, unsigned flags, psg_ctx** out) {
     if (v >= 1 && v <= psg::kMaxPush) c->flush_pushes = (size_t)v;
   }
   c->table.read_knobs();
+  c->zero_copy = zero_copy_enabled();
   hipError_t e = hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking);
   if (e == hipSuccess) e = hipStreamCreateWithFlags(&c->copy, hipStreamNonBlocking);
   if (e == hipSuccess) e = hipEventCreateWithFlags(&c->copy_ev, hipEventDisableTiming);
@@ -1524,14 +1560,11 @@ int psg_received(psg_ctx* c, int time, int m, void* const* out) {
   if (m != A.m || !out) return fail(PSG_ERR_ARG, "expected %d output arrays", A.m);
   int rc = c->flush(A);
   const size_t len = A.hi - A.lo, sv = vsize(c->dtype);
-  for (int i = 0; rc == PSG_OK && i < A.m && len; ++i) {
-    hipError_t e = hipMemcpyAsync(out[i], A.d_out[i], len * sv, hipMemcpyDeviceToHost, c->stream);
-    if (e != hipSuccess) rc = fail(PSG_ERR_DEVICE, "D2H: %s", hipGetErrorString(e));
-  }
+  for (int i = 0; rc == PSG_OK && i < A.m && len; ++i) rc = c->d2h(out[i], A.d_out[i], len * sv);
   unsigned long long bad = 0;
+  if (rc == PSG_OK) rc = c->d2h(c->h_small, A.d_bad, 8);
   if (rc == PSG_OK) {
-    hipError_t e = hipMemcpyAsync(c->h_small, A.d_bad, 8, hipMemcpyDeviceToHost, c->stream);
-    if (e == hipSuccess) e = hipStreamSynchronize(c->stream);
+    hipError_t e = hipStreamSynchronize(c->stream);
     if (e != hipSuccess) rc = fail(PSG_ERR_DEVICE, "received: %s", hipGetErrorString(e));
     bad = c->h_small[0];
   }

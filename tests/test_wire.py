@@ -314,6 +314,65 @@ def test_pinned_and_pageable_pushes_agree():
 
 
 @pytest.mark.gpu
+def test_pinned_offsets_zero_copy():
+    """Pinned pushes are read by the GPU itself (zero-copy kernel) when both
+    ends are 16-B aligned, by a DMA copy otherwise: buffers that start inside
+    a pinned allocation (aligned and unaligned offsets, odd lengths) give the
+    oracle's bits."""
+    import torch
+    assert torch.cuda.is_available()
+    from parameter_server_amd import synth
+    D, pushes = synth.overlap_pushes(seed=19, npush=6, n=30001)
+    tot = sum(k.size for k, _ in pushes) + 64 * len(pushes)
+    kall = torch.zeros(tot, dtype=torch.int64, pin_memory=True).numpy().view(np.uint64)
+    vall = torch.zeros(tot, dtype=torch.float32, pin_memory=True).numpy()
+    v = _kvv()
+    v.setValue(_msg(D))
+    at = 0
+    for p, (k, vals) in enumerate(pushes):
+        ko = at + (2 if p % 2 == 0 else 1)  # 16-B aligned / 8-B aligned keys
+        vo = at + (4 if p % 3 else 1)       # 16-B aligned / 4-B aligned values
+        kb, vb = kall[ko: ko + k.size], vall[vo: vo + k.size]
+        kb[:] = k
+        vb[:] = vals[0]
+        v.setValue(_msg(kb, [vb], t=3))
+        at += k.size + 64
+    (_, got), = v.received(3)
+    v.close()
+    _, _, _, want, _ = O.aggregate(D, 0, (1 << 64) - 1, pushes)
+    assert np.array_equal(_bits(got), _bits(want[0]))
+
+
+@pytest.mark.gpu
+def test_received_into_pinned_output():
+    """received(t) into pinned host arrays is written by the GPU itself
+    (zero-copy readback), at aligned and unaligned starts, m = 2, f64."""
+    import torch
+    assert torch.cuda.is_available()
+    from parameter_server_amd import synth
+    from parameter_server_amd.kv_vector import KVVector, Message
+    from parameter_server_amd._lib import PSG_F64
+    D, pushes = synth.overlap_pushes(seed=23, npush=4, n=20000)
+    rng = np.random.default_rng(23)
+    vals = [[rng.standard_normal(k.size), rng.standard_normal(k.size)] for k, _ in pushes]
+    _, _, _, want, _ = O.aggregate(D, 0, (1 << 64) - 1,
+                                   [(k, v) for (k, _), v in zip(pushes, vals)], False, 1,
+                                   np.float64)
+    for off in (0, 1):  # 16-B aligned start / 8-B aligned start (DMA fallback)
+        v = KVVector(0, PSG_F64)
+        v.setValue(Message(key=D))
+        for (k, _), x in zip(pushes, vals):
+            v.setValue(Message(time=5, key=k, value=x))
+        buf = [torch.full((D.size + 2,), np.nan, dtype=torch.float64, pin_memory=True).numpy()
+               for _ in range(2)]
+        out = v.received(5, out=[b[off:] for b in buf])
+        v.close()
+        for i in range(2):
+            assert out[i][1].ctypes.data == buf[i][off:].ctypes.data  # written in place
+            assert np.array_equal(_bits(out[i][1]), _bits(want[i]))
+
+
+@pytest.mark.gpu
 def test_hold_buffers_option():
     """PSG_HOLD_BUFFERS: pinned push buffers are DMA'd without a wait per
     push and must stay valid until received(t); the result is unchanged."""
