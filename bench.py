@@ -385,8 +385,9 @@ def end_to_end(inst, device, reps=7):
     Python in the loop).  Caller setups:
       pageable       keys+values and output in pageable memory (CPU copy into
                      the pinned staging ring, DMA overlapped with the next push);
-      pinned         pinned host memory, each push waits for its own DMA (the
-                     caller's buffers are free on return);
+      pinned         pinned host memory, read by the GPU itself (zero-copy
+                     kernel); each push waits for it (the caller's buffers
+                     are free on return);
       pinned_hold    pinned, PSG_HOLD_BUFFERS (buffers held until received,
                      as a MessagePtr holds its SArrays): no wait per push;
       pinned_cached  pinned_hold, and each worker's keys come from the key
