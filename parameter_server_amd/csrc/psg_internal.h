@@ -99,9 +99,20 @@ hipError_t launch_gather(int dtype, const uint64_t* dkeys, uint64_t nd,
                          void* out, unsigned long long* matched,
                          hipStream_t stream);
 // keys strictly increasing?  *bad (device) += number of violations.
-// pinned host -> device copy read by the GPU (src: a device-visible host
-// address, 16-B aligned, as is dst)
+// copies between pinned host memory and the device made by the GPU itself
+// (zero-copy; src/dst are device-visible addresses, 16-B aligned)
+struct HostCopyDesc {
+  const void* src;
+  void* dst;
+  uint64_t len;
+};
+constexpr int kHostCopyBatch = 32;  // buffers per launch (kernel arguments)
+struct HostCopyBatch {
+  HostCopyDesc d[kHostCopyBatch];
+  uint32_t n = 0;
+};
 hipError_t launch_host_copy(void* dst, const void* src, size_t len, hipStream_t stream);
+hipError_t launch_host_copy_batch(const HostCopyBatch& b, hipStream_t stream);
 hipError_t launch_check_sorted(const uint64_t* keys, uint64_t n,
                                unsigned long long* bad, hipStream_t stream,
                                bool strict = true);

@@ -100,26 +100,32 @@ __global__ __launch_bounds__(256) void gather_kernel(
   if (lane == 0 && found) atomicAdd(matched, (unsigned long long)found);
 }
 
-// pinned host -> device copy by the GPU itself (zero-copy reads over PCIe):
-// 16-B loads, 4 in flight per thread.  For the 0.5-4 MB buffers of a push it
-// beats a DMA copy's fixed cost (tools/calib/hostbw.py: 1 MB 47 vs 38 GB/s,
-// 512 KB 40 vs 28 GB/s).  Both ends 16-B aligned (the launcher checks).
+// pinned host <-> device copies by the GPU itself (zero-copy access over
+// PCIe): 16-B loads, 4 in flight per thread, every block walking each
+// buffer of the batch in turn.  For the 0.5-4 MB buffers of a push it beats
+// a DMA copy's fixed cost (tools/calib/hostbw.py: 1 MB 47 vs 38 GB/s,
+// 512 KB 40 vs 28 GB/s), and one launch carries a flush's worth of them.
+// Both ends 16-B aligned (the runtime checks).
 typedef uint32_t u32x4_t __attribute__((ext_vector_type(4)));
-__global__ __launch_bounds__(256) void host_copy_kernel(const u32x4_t* __restrict__ s,
-                                                        u32x4_t* __restrict__ d, uint64_t n16,
-                                                        uint32_t tail) {
+__global__ __launch_bounds__(256) void host_copy_kernel(HostCopyBatch b) {
   const uint64_t stride = (uint64_t)gridDim.x * 256u;
-  for (uint64_t u = (uint64_t)blockIdx.x * 256u + threadIdx.x; u < n16; u += 4 * stride) {
-    u32x4_t v[4];
+  for (uint32_t c = 0; c < b.n; ++c) {
+    const u32x4_t* __restrict__ s = (const u32x4_t*)b.d[c].src;
+    u32x4_t* __restrict__ d = (u32x4_t*)b.d[c].dst;
+    const uint64_t n16 = b.d[c].len / 16;
+    for (uint64_t u = (uint64_t)blockIdx.x * 256u + threadIdx.x; u < n16; u += 4 * stride) {
+      u32x4_t v[4];
 #pragma unroll
-    for (int j = 0; j < 4; ++j)
-      if (u + j * stride < n16) v[j] = __builtin_nontemporal_load(s + u + j * stride);
+      for (int j = 0; j < 4; ++j)
+        if (u + j * stride < n16) v[j] = __builtin_nontemporal_load(s + u + j * stride);
 #pragma unroll
-    for (int j = 0; j < 4; ++j)
-      if (u + j * stride < n16) d[u + j * stride] = v[j];
+      for (int j = 0; j < 4; ++j)
+        if (u + j * stride < n16) d[u + j * stride] = v[j];
+    }
+    const uint32_t tail = (uint32_t)(b.d[c].len % 16);
+    if (blockIdx.x == 0 && threadIdx.x < tail)
+      ((uint8_t*)(d + n16))[threadIdx.x] = ((const uint8_t*)(s + n16))[threadIdx.x];
   }
-  if (blockIdx.x == 0 && threadIdx.x < tail)
-    ((uint8_t*)(d + n16))[threadIdx.x] = ((const uint8_t*)(s + n16))[threadIdx.x];
 }
 
 __global__ __launch_bounds__(256) void check_sorted_kernel(
@@ -310,15 +316,22 @@ hipError_t launch_gather(int dtype, const uint64_t* dkeys, uint64_t nd,
   return hipGetLastError();
 }
 
+hipError_t launch_host_copy_batch(const HostCopyBatch& b, hipStream_t stream) {
+  uint64_t units = 0;
+  for (uint32_t c = 0; c < b.n; ++c) units += b.d[c].len / 16;
+  if (b.n == 0) return hipSuccess;
+  uint64_t blocks = (units + 1023) / 1024;  // 4 units per thread per pass
+  blocks = blocks < 1 ? 1 : (blocks > 128 ? 128 : blocks);
+  hipLaunchKernelGGL(host_copy_kernel, dim3((uint32_t)blocks), dim3(256), 0, stream, b);
+  return hipGetLastError();
+}
+
 hipError_t launch_host_copy(void* dst, const void* src, size_t len, hipStream_t stream) {
   if (len == 0) return hipSuccess;
-  const uint64_t n16 = len / 16;
-  const uint64_t per = 256u * 4u;  // units per block per pass
-  uint64_t blocks = (n16 + per - 1) / per;
-  blocks = blocks < 1 ? 1 : (blocks > 128 ? 128 : blocks);
-  hipLaunchKernelGGL(host_copy_kernel, dim3((uint32_t)blocks), dim3(256), 0, stream,
-                     (const u32x4_t*)src, (u32x4_t*)dst, n16, (uint32_t)(len % 16));
-  return hipGetLastError();
+  HostCopyBatch b;
+  b.n = 1;
+  b.d[0] = HostCopyDesc{src, dst, (uint64_t)len};
+  return launch_host_copy_batch(b, stream);
 }
 
 hipError_t launch_check_sorted(const uint64_t* keys, uint64_t n,

@@ -161,6 +161,13 @@ int forced_pack() {
   return e && (e[0] == '0' || e[0] == '1') ? e[0] - '0' : -1;
 }
 
+// PSG_ZERO_COPY=0 stages pinned buffers (and job-table images) with DMA
+// copies instead of the zero-copy kernel (A/B and fallback knob)
+bool zero_copy_enabled() {
+  const char* e = getenv("PSG_ZERO_COPY");
+  return !(e && e[0] == '0');
+}
+
 // PSG_WIDE=0|1 forces the tile kernel's push-group size (32 | 64).
 int forced_wide() {
   const char* e = getenv("PSG_WIDE");
@@ -174,6 +181,7 @@ struct JobTable {
     knob_part = forced_part_mode();
     knob_pack = forced_pack();
     knob_wide = forced_wide();
+    zero_copy = zero_copy_enabled();
   }
   bool pack = false;  // rounds may hold several pushes
   bool wide = false;  // push groups of 64 in the tile kernel (a job has > 32 pushes)
@@ -201,6 +209,8 @@ struct JobTable {
   // pinned host images of the blob, used alternately: a build fills one
   // while the previous build's copy may still be in flight
   char* himg[2] = {nullptr, nullptr};
+  const void* himg_dev[2] = {nullptr, nullptr};  // their device-visible addresses
+  bool zero_copy = true;  // the image moves by the zero-copy kernel, not a DMA copy
   size_t himg_cap[2] = {0, 0};
   hipEvent_t himg_ev[2] = {nullptr, nullptr};
   int himg_cur = 0;
@@ -217,6 +227,7 @@ struct JobTable {
       if (himg_ev[i]) (void)hipEventDestroy(himg_ev[i]);
       if (himg[i]) (void)hipHostFree(himg[i]);
       himg[i] = nullptr;
+      himg_dev[i] = nullptr;
       himg_ev[i] = nullptr;
       himg_cap[i] = 0;
     }
@@ -335,6 +346,10 @@ struct JobTable {
       himg_cap[ib] = 0;
       HIP_TRY(hipHostMalloc((void**)&himg[ib], off));
       himg_cap[ib] = off;
+      himg_dev[ib] = nullptr;
+      void* dp = nullptr;
+      if (hipHostGetDevicePointer(&dp, himg[ib], 0) == hipSuccess) himg_dev[ib] = dp;
+      else (void)hipGetLastError();
     }
     char* img = himg[ib];
     memset(img, 0, off);
@@ -429,7 +444,11 @@ struct JobTable {
     d_tiles = (psg::TileDesc*)(base + tiles_off);
     d_split_items = (uint32_t*)(base + sitems_off);
     d_items = (uint64_t*)(base + items_off);
-    HIP_TRY(hipMemcpyAsync(blob, img, off, hipMemcpyHostToDevice, strm));
+    // the image is small: a DMA copy's fixed cost exceeds its transfer time
+    if (zero_copy && himg_dev[ib] && (((uintptr_t)himg_dev[ib] | (uintptr_t)blob) & 15u) == 0)
+      HIP_TRY(psg::launch_host_copy(blob, himg_dev[ib], off, strm));
+    else
+      HIP_TRY(hipMemcpyAsync(blob, img, off, hipMemcpyHostToDevice, strm));
     HIP_TRY(hipEventRecord(himg_ev[ib], strm));
     if (!async) HIP_TRY(hipStreamSynchronize(strm));
     return PSG_OK;
@@ -568,12 +587,6 @@ bool host_pinned(const void* p, const void** dev = nullptr) {
   return true;
 }
 
-// PSG_ZERO_COPY=0 stages pinned buffers with DMA copies instead of the
-// zero-copy kernel (A/B and fallback knob; read at context creation)
-bool zero_copy_enabled() {
-  const char* e = getenv("PSG_ZERO_COPY");
-  return !(e && e[0] == '0');
-}
 
 // FreqencyFilter<uint64> of one channel (CountMin n_, k_, table)
 struct Filter {
@@ -643,6 +656,9 @@ struct psg_ctx {
   }
   void dev_put(void* p, size_t b) {
     if (!p) return;
+    // a deferred copy may target the block: issue it and order it before
+    // the block's release event on `stream`
+    if (zc.n) (void)join_copy();
     b = align_up(b ? b : 1, 4096);
     hipEvent_t e = nullptr;
     if (pool_bytes + b > kPoolCap || event(&e) != PSG_OK ||
@@ -718,13 +734,31 @@ struct psg_ctx {
 
   bool pinned_wait = false;  // a pinned copy of this call is still in flight
   bool zero_copy = true;     // pinned buffers read by a kernel, not a DMA copy
-  int h2d(void* dst, const void* src, size_t len) {
+  // held pushes' pinned buffers (PSG_HOLD_BUFFERS: valid until received):
+  // copied by one zero-copy launch when the merge needs them (join_copy)
+  psg::HostCopyBatch zc;
+  int zc_flush() {
+    if (zc.n == 0) return PSG_OK;
+    const hipError_t e = psg::launch_host_copy_batch(zc, copy);
+    zc.n = 0;
+    HIP_TRY(e);
+    return PSG_OK;
+  }
+  // `defer`: a push's keys or values, read by nothing before the merge
+  int h2d(void* dst, const void* src, size_t len, bool defer = false) {
     if (!len) return PSG_OK;
     const void* sdev = nullptr;
     if (host_pinned(src, &sdev)) {
       // the GPU reads the caller's pinned buffer itself when both ends are
       // 16-B aligned (a DMA copy's fixed cost dominates at push sizes)
-      if (zero_copy && sdev && (((uintptr_t)sdev | (uintptr_t)dst) & 15u) == 0)
+      const bool zok = zero_copy && sdev && (((uintptr_t)sdev | (uintptr_t)dst) & 15u) == 0;
+      if (zok && defer && (flags & PSG_HOLD_BUFFERS)) {
+        if (zc.n == (uint32_t)psg::kHostCopyBatch)
+          if (int rc = zc_flush()) return rc;
+        zc.d[zc.n++] = psg::HostCopyDesc{sdev, dst, (uint64_t)len};
+        return PSG_OK;
+      }
+      if (zok)
         HIP_TRY(psg::launch_host_copy(dst, sdev, len, copy));
       else
         HIP_TRY(hipMemcpyAsync(dst, src, len, hipMemcpyHostToDevice, copy));
@@ -771,6 +805,7 @@ struct psg_ctx {
 
   // work enqueued on `stream` from now on sees every H2D issued so far
   int join_copy() {
+    if (int rc = zc_flush()) return rc;
     HIP_TRY(hipEventRecord(copy_ev, copy));
     HIP_TRY(hipStreamWaitEvent(stream, copy_ev, 0));
     return PSG_OK;
@@ -1076,6 +1111,7 @@ int psg_create(int device, int dtype, unsigned flags, psg_ctx** out) {
 int psg_destroy(psg_ctx* c) {
   if (!c) return PSG_OK;
   (void)hipSetDevice(c->device);
+  c->zc.n = 0;  // held buffers of pushes never merged: not read any more
   if (c->copy) (void)hipStreamSynchronize(c->copy);
   if (c->stream) (void)hipStreamSynchronize(c->stream);
   for (auto& kv : c->agg) c->drop(kv.second);
@@ -1219,7 +1255,7 @@ int psg_ctx::push_values(int chl, int time, uint64_t kb, uint64_t ke, const KeyR
     if (int rc = dev_get(pp.vbytes, &pp.vblock, copy)) return rc;
     for (int i = 0; i < m; ++i) {
       pp.d_vals[i] = (char*)pp.vblock + i * vb;
-      if (int rc = h2d(pp.d_vals[i], vals[i], sv * n)) {
+      if (int rc = h2d(pp.d_vals[i], vals[i], sv * n, true)) {
         release_push(pp);
         return rc;
       }
@@ -1347,7 +1383,7 @@ int psg_push(psg_ctx* c, int chl, int time, uint64_t kb, uint64_t ke,
   if (int rc = check_push(c, chl, time, kb, ke, n, m, &lo, &hi)) return rc;
   KeyRef k;
   int rc = c->new_keys(n, &k);
-  if (rc == PSG_OK) rc = c->h2d(k->d, keys, 8 * n);
+  if (rc == PSG_OK) rc = c->h2d(k->d, keys, 8 * n, true);
   if (rc == PSG_OK) rc = c->push_values(chl, time, kb, ke, k, m, vals);
   const int rf = c->h2d_finish();
   return rc ? rc : rf;

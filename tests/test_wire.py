@@ -324,23 +324,28 @@ def test_pinned_offsets_zero_copy():
     from parameter_server_amd import synth
     D, pushes = synth.overlap_pushes(seed=19, npush=6, n=30001)
     tot = sum(k.size for k, _ in pushes) + 64 * len(pushes)
-    kall = torch.zeros(tot, dtype=torch.int64, pin_memory=True).numpy().view(np.uint64)
-    vall = torch.zeros(tot, dtype=torch.float32, pin_memory=True).numpy()
-    v = _kvv()
-    v.setValue(_msg(D))
-    at = 0
-    for p, (k, vals) in enumerate(pushes):
-        ko = at + (2 if p % 2 == 0 else 1)  # 16-B aligned / 8-B aligned keys
-        vo = at + (4 if p % 3 else 1)       # 16-B aligned / 4-B aligned values
-        kb, vb = kall[ko: ko + k.size], vall[vo: vo + k.size]
-        kb[:] = k
-        vb[:] = vals[0]
-        v.setValue(_msg(kb, [vb], t=3))
-        at += k.size + 64
-    (_, got), = v.received(3)
-    v.close()
+    from parameter_server_amd import _lib
     _, _, _, want, _ = O.aggregate(D, 0, (1 << 64) - 1, pushes)
-    assert np.array_equal(_bits(got), _bits(want[0]))
+    for hold in (False, True):  # hold: the aligned ones go in one batched launch
+        kall = torch.zeros(tot, dtype=torch.int64, pin_memory=True).numpy().view(np.uint64)
+        vall = torch.zeros(tot, dtype=torch.float32, pin_memory=True).numpy()
+        v = _kvv()
+        if hold:
+            _lib.check(v._L.psg_set_match_flags(v._h, _lib.PSG_SERIAL_MATCH |
+                                                _lib.PSG_HOLD_BUFFERS))
+        v.setValue(_msg(D))
+        at = 0
+        for p, (k, vals) in enumerate(pushes):
+            ko = at + (2 if p % 2 == 0 else 1)  # 16-B aligned / 8-B aligned keys
+            vo = at + (4 if p % 3 else 1)       # 16-B aligned / 4-B aligned values
+            kb, vb = kall[ko: ko + k.size], vall[vo: vo + k.size]
+            kb[:] = k
+            vb[:] = vals[0]
+            v.setValue(_msg(kb, [vb], t=3))
+            at += k.size + 64
+        (_, got), = v.received(3)
+        v.close()
+        assert np.array_equal(_bits(got), _bits(want[0])), hold
 
 
 @pytest.mark.gpu
