@@ -830,7 +830,11 @@ struct psg_ctx {
 
   // Enqueue the merge of every pending push of `a` into its device output;
   // unmatched keys accumulate in a.d_bad.  No host wait.
-  int flush(Aggregate& a) {
+  // `outs`: write the sums there instead of a.d_out (device-visible caller
+  // arrays; only for a single launch that starts the aggregate).
+  // `bad_host`: read a.d_bad back there right after the last launch, ahead
+  // of the host-side release work (psg_received waits for it)
+  int flush(Aggregate& a, void* const* outs = nullptr, void* bad_host = nullptr) {
     if (a.pending.empty()) return PSG_OK;
     if (int rc = join_copy()) return rc;
     while (!a.pending.empty()) {
@@ -846,10 +850,12 @@ struct psg_ctx {
         for (int i = 0; i < a.m; ++i) js.pvals.push_back(pp.d_vals[i]);
         js.pn.push_back(pp.n);
       }
-      for (int i = 0; i < a.m; ++i) js.out.push_back(a.d_out[i]);
+      for (int i = 0; i < a.m; ++i) js.out.push_back(outs ? outs[i] : a.d_out[i]);
       if (int rc = table.build(device, dtype, a.m, {js}, stream, true)) return rc;
       if (int rc = table.run(stream)) return rc;
       HIP_TRY(psg::launch_unmatched(table.d_jobs, 0, table.info[0].np, a.d_bad, stream));
+      if (bad_host && take == a.pending.size())
+        if (int rc = d2h(bad_host, a.d_bad, 8)) return rc;
       for (size_t p = 0; p < take; ++p) release_push(a.pending[p]);
       a.pending.erase(a.pending.begin(), a.pending.begin() + take);
       a.folded += take;
@@ -1594,11 +1600,23 @@ int psg_received(psg_ctx* c, int time, int m, void* const* out) {
   if (int rc = set_dev(c->device)) return rc;
   Aggregate& A = it->second;
   if (m != A.m || !out) return fail(PSG_ERR_ARG, "expected %d output arrays", A.m);
-  int rc = c->flush(A);
   const size_t len = A.hi - A.lo, sv = vsize(c->dtype);
-  for (int i = 0; rc == PSG_OK && i < A.m && len; ++i) rc = c->d2h(out[i], A.d_out[i], len * sv);
+  // the whole aggregate in one launch into pinned caller arrays: the merge
+  // kernel writes the sums there itself (no separate readback)
+  bool direct = c->zero_copy && A.folded == 0 && !A.pending.empty() &&
+                A.pending.size() <= c->flush_pushes && len > 0;
+  void* dev_out[psg::kMaxM] = {};
+  for (int i = 0; direct && i < A.m; ++i) {
+    const void* d = nullptr;
+    direct = host_pinned(out[i], &d) && d && ((uintptr_t)d & 15u) == 0;
+    dev_out[i] = (void*)d;
+  }
+  const bool pend = !A.pending.empty();
+  int rc = c->flush(A, direct ? dev_out : nullptr, direct ? c->h_small : nullptr);
+  for (int i = 0; !direct && rc == PSG_OK && i < A.m && len; ++i)
+    rc = c->d2h(out[i], A.d_out[i], len * sv);
   unsigned long long bad = 0;
-  if (rc == PSG_OK) rc = c->d2h(c->h_small, A.d_bad, 8);
+  if (rc == PSG_OK && !(direct && pend)) rc = c->d2h(c->h_small, A.d_bad, 8);
   if (rc == PSG_OK) {
     hipError_t e = hipStreamSynchronize(c->stream);
     if (e != hipSuccess) rc = fail(PSG_ERR_DEVICE, "received: %s", hipGetErrorString(e));

@@ -350,31 +350,33 @@ def test_pinned_offsets_zero_copy():
 
 @pytest.mark.gpu
 def test_received_into_pinned_output():
-    """received(t) into pinned host arrays is written by the GPU itself
-    (zero-copy readback), at aligned and unaligned starts, m = 2, f64."""
+    """received(t) into pinned host arrays: when one launch covers the
+    aggregate the merge kernel writes the sums there itself; at an unaligned
+    start it falls back to a readback.  f64 with m = 2 and f32 with m = 1."""
     import torch
     assert torch.cuda.is_available()
     from parameter_server_amd import synth
     from parameter_server_amd.kv_vector import KVVector, Message
-    from parameter_server_amd._lib import PSG_F64
+    from parameter_server_amd._lib import PSG_F32, PSG_F64
     D, pushes = synth.overlap_pushes(seed=23, npush=4, n=20000)
     rng = np.random.default_rng(23)
-    vals = [[rng.standard_normal(k.size), rng.standard_normal(k.size)] for k, _ in pushes]
-    _, _, _, want, _ = O.aggregate(D, 0, (1 << 64) - 1,
-                                   [(k, v) for (k, _), v in zip(pushes, vals)], False, 1,
-                                   np.float64)
-    for off in (0, 1):  # 16-B aligned start / 8-B aligned start (DMA fallback)
-        v = KVVector(0, PSG_F64)
-        v.setValue(Message(key=D))
-        for (k, _), x in zip(pushes, vals):
-            v.setValue(Message(time=5, key=k, value=x))
-        buf = [torch.full((D.size + 2,), np.nan, dtype=torch.float64, pin_memory=True).numpy()
-               for _ in range(2)]
-        out = v.received(5, out=[b[off:] for b in buf])
-        v.close()
-        for i in range(2):
-            assert out[i][1].ctypes.data == buf[i][off:].ctypes.data  # written in place
-            assert np.array_equal(_bits(out[i][1]), _bits(want[i]))
+    for dt, code, m in ((np.float64, PSG_F64, 2), (np.float32, PSG_F32, 1)):
+        vals = [[rng.standard_normal(k.size).astype(dt) for _ in range(m)] for k, _ in pushes]
+        _, _, _, want, _ = O.aggregate(D, 0, (1 << 64) - 1,
+                                       [(k, v) for (k, _), v in zip(pushes, vals)], False, 1, dt)
+        tdt = torch.float64 if dt == np.float64 else torch.float32
+        for off in (0, 1):  # 16-B aligned start / unaligned start (readback)
+            v = KVVector(0, code)
+            v.setValue(Message(key=D))
+            for (k, _), x in zip(pushes, vals):
+                v.setValue(Message(time=5, key=k, value=x))
+            buf = [torch.full((D.size + 2,), np.nan, dtype=tdt, pin_memory=True).numpy()
+                   for _ in range(m)]
+            out = v.received(5, out=[b[off:] for b in buf])
+            v.close()
+            for i in range(m):
+                assert out[i][1].ctypes.data == buf[i][off:].ctypes.data  # written in place
+                assert np.array_equal(_bits(out[i][1]), _bits(want[i])), (dt, off, i)
 
 
 @pytest.mark.gpu
