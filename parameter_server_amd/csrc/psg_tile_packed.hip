@@ -13,14 +13,16 @@
 // Shape:
 //   * the partition (psg_partition.hip) has cut every push at every tile:
 //     push q's keys of this tile are S_q[seg(q, t), seg(q, t+1));
-//   * pushes are taken in groups of <= kG (one lane of wave 0 each); the
-//     group's pieces are concatenated push-major and cut into ROUNDS of 64
-//     consecutive elements, so a round may hold the tail of one piece and
-//     the heads of the next (short pieces of many sparse pushes fill a
-//     round instead of leaving it mostly idle);
+//   * pushes are taken in groups of <= kG = 128 (wave 0, two per lane) whose
+//     elements fit one pass; the group's pieces are concatenated push-major
+//     and cut into ROUNDS of 64 consecutive elements, so a round may hold the
+//     tail of one piece and the heads of the next (short pieces of many
+//     sparse pushes fill a round instead of leaving it mostly idle); each
+//     push's lane writes its elements' push index into an LDS map, so a lane
+//     finds its element's push with one LDS read;
 //   * each wave takes a contiguous run of rounds per pass and issues all
 //     its element loads before the tile's bucket table is built;
-//   * D goes to LDS; a bucket table (2 buckets per slot over the tile's key
+//   * D goes to LDS; a bucket table (1 bucket per slot over the tile's key
 //     range, one high multiply) turns a search into one table read and one
 //     paired key read;
 //   * the fold runs wave by wave (4 barrier steps): rounds are push-major
@@ -59,17 +61,18 @@ constexpr int kTS = kTileSlots;  // slots per tile
 constexpr int kNT = 256;         // threads
 constexpr int kNW = kNT / 64;    // waves
 constexpr int kSPT = kTS / kNT;  // slots per thread (contiguous)
-constexpr int kNB = 2 * kTS;     // buckets
+constexpr int kNB = kTS;         // buckets (one per slot: the LDS budget of 8 workgroups per CU)
 constexpr int kBPT = kNB / kNT;  // bucket-table entries per thread in the scan
 constexpr int kCap = 6;          // rounds a wave holds per pass
-constexpr int kG = 64;           // pushes per group (one lane of wave 0 each)
-constexpr int kRMax = 160;       // rounds per group
-static_assert(kSPT == 4 && kBPT == 8, "layout");
+constexpr int kG = 128;          // pushes per group (two lanes' worth per lane of wave 0)
+constexpr int kECap = kNW * kCap * 64;  // elements per group: one pass
+static_assert(kSPT == 4 && kBPT == 4, "layout");
 static_assert(kTS <= 0x7ffe, "u16 positions");
-static_assert(kG + 2 <= 255, "u8 lastl");
+static_assert(kG + 2 <= 255 && kG <= 256, "u8 lastl, u8 element -> push map");
+static_assert(kECap >= kTS, "a piece (<= kTS keys) always fits a group");
 
 typedef unsigned long long u64x2 __attribute__((ext_vector_type(2)));
-typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
+typedef uint32_t u32x2 __attribute__((ext_vector_type(2)));
 
 __device__ __forceinline__ uint32_t uni(uint32_t v) { return __builtin_amdgcn_readfirstlane(v); }
 
@@ -96,7 +99,7 @@ __device__ __forceinline__ uint32_t wave_scan_incl(uint32_t x) {
 // the register budget follows it through __launch_bounds__
 template <typename V, int M>
 constexpr int occupancy() {
-  constexpr int lds = 19504 + (int)(M * sizeof(V) - 4) * kTS + (M - 1) * 8 * kG;
+  constexpr int lds = 20116 + (int)(M * sizeof(V) - 4) * kTS + (M - 1) * 8 * kG;
   return 163840 / lds >= 8 ? 8 : 163840 / lds;
 }
 
@@ -113,10 +116,11 @@ __global__ __launch_bounds__(kNT, (occupancy<V, M>())) void tile_packed_kernel(
   // last push holding the slot, relative to the group base g0: last + 2 - g0,
   // 0 when it precedes g0 - 1 (so the value fits a byte for any push count)
   __shared__ __attribute__((aligned(16))) uint8_t lastl[kTS];
-  // pre[q] = elements of the group before push q, rq[R] = push of round R's
-  // first element (+ a sentinel)
+  // pre[q] = elements of the group before push q; ep[e] = push of the
+  // group's element e (written by the push's lane: one LDS read per element
+  // instead of a search over pre)
   __shared__ uint32_t pre[kG + 1];
-  __shared__ uint16_t rq[kRMax + 4];
+  __shared__ uint8_t ep[kECap];
   __shared__ uint64_t pkp[kG], pvp[kG * M];  // piece starts (keys, values)
   __shared__ uint32_t cbits[kNW][kTS / 32];  // per-wave slot bitmap: collision test
   __shared__ int lastpos[kNW];
@@ -136,7 +140,8 @@ __global__ __launch_bounds__(kNT, (occupancy<V, M>())) void tile_packed_kernel(
   const bool cont = (T.flags & kFlagCont) != 0;
   const uint64_t* Dg = T.dk;
 
-  // ---- push tables of a group (wave 0, one lane per push), rounds
+  // ---- push tables of a group (wave 0, pushes lane and 64 + lane), the
+  // element -> push map
   auto load_tables = [&](uint32_t g0) {
     if (w == 0) {
       // a fresh copy of the lane id per call: otherwise the compiler hoists
@@ -145,51 +150,58 @@ __global__ __launch_bounds__(kNT, (occupancy<V, M>())) void tile_packed_kernel(
       int lane = tid & 63;
       asm volatile("" : "+v"(lane));
       const uint32_t gq = np - g0 < (uint32_t)kG ? np - g0 : (uint32_t)kG;
-      uint32_t len = 0, over = 0;
-      uint64_t kp = 0, vp[M];
+      uint32_t len[2] = {0, 0}, over[2] = {0, 0};
+      uint64_t kp[2] = {0, 0}, vp[2][M];
 #pragma unroll
-      for (int mi = 0; mi < M; ++mi) vp[mi] = 0;
-      if ((uint32_t)lane < gq) {
-        const uint32_t q = g0 + (uint32_t)lane;
-        const uint32_t* sg = T.seg + (size_t)q * T.stride;
-        const uint32_t n = (uint32_t)G(T.pn)[q];
-        uint32_t a = G(sg)[0], b = G(sg)[T.segb];
-        // bounds from a failed partition (an unsorted push) stay inside the push
-        a = a < n ? a : n;
-        b = b < n ? b : n;
-        // pieces out of order or longer than the tile (duplicates): those
-        // keys cannot all match
-        over = b < a ? 1u : (b - a > (uint32_t)kTS ? b - a - (uint32_t)kTS : 0u);
-        len = b > a ? (b - a < (uint32_t)kTS ? b - a : (uint32_t)kTS) : 0u;
-        kp = (uint64_t)(G(T.pkeys)[q] + a);
+      for (int h = 0; h < 2; ++h) {
 #pragma unroll
-        for (int mi = 0; mi < M; ++mi)
-          vp[mi] = (uint64_t)((const V*)G(T.pvals)[(size_t)q * M + mi] + a);
+        for (int mi = 0; mi < M; ++mi) vp[h][mi] = 0;
+        const uint32_t ql = (uint32_t)lane + 64u * h;
+        if (ql < gq) {
+          const uint32_t q = g0 + ql;
+          const uint32_t* sg = T.seg + (size_t)q * T.stride;
+          const uint32_t n = (uint32_t)G(T.pn)[q];
+          uint32_t a = G(sg)[0], b = G(sg)[T.segb];
+          // bounds from a failed partition (an unsorted push) stay inside the push
+          a = a < n ? a : n;
+          b = b < n ? b : n;
+          // pieces out of order or longer than the tile (duplicates): those
+          // keys cannot all match
+          over[h] = b < a ? 1u : (b - a > (uint32_t)kTS ? b - a - (uint32_t)kTS : 0u);
+          len[h] = b > a ? (b - a < (uint32_t)kTS ? b - a : (uint32_t)kTS) : 0u;
+          kp[h] = (uint64_t)(G(T.pkeys)[q] + a);
+#pragma unroll
+          for (int mi = 0; mi < M; ++mi)
+            vp[h][mi] = (uint64_t)((const V*)G(T.pvals)[(size_t)q * M + mi] + a);
+        }
       }
-      // elements through this push
-      const uint32_t x = wave_scan_incl(len);
-      // the group: the pushes whose rounds fit kRMax (>= 1: a piece is <= 16 rounds)
+      // elements through each push
+      const uint32_t x0 = wave_scan_incl(len[0]);
+      const uint32_t x1 = wave_scan_incl(len[1]) + uni(__builtin_amdgcn_readlane((int)x0, 63));
+      // the group: the pushes whose elements fit one pass (>= 1: a piece is <= kTS)
       const uint32_t gp =
-          (uint32_t)__popcll(__ballot((uint32_t)lane < gq && x <= (uint32_t)(kRMax * 64)));
-      if ((uint32_t)lane < gp) {
-        pkp[lane] = kp;
+          (uint32_t)__popcll(__ballot((uint32_t)lane < gq && x0 <= (uint32_t)kECap)) +
+          (uint32_t)__popcll(__ballot((uint32_t)lane + 64u < gq && x1 <= (uint32_t)kECap));
 #pragma unroll
-        for (int mi = 0; mi < M; ++mi) pvp[lane * M + mi] = vp[mi];
-        if (over)
-          __hip_atomic_fetch_add(GW(T.fail) + g0 + lane, (unsigned long long)over,
-                                 __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        pre[lane + 1] = x;
-        // the rounds whose first element lies in this piece
+      for (int h = 0; h < 2; ++h) {
+        const uint32_t ql = (uint32_t)lane + 64u * h;
+        const uint32_t x = h ? x1 : x0;
+        if (ql < gp) {
+          pkp[ql] = kp[h];
+#pragma unroll
+          for (int mi = 0; mi < M; ++mi) pvp[ql * M + mi] = vp[h][mi];
+          if (over[h])
+            __hip_atomic_fetch_add(GW(T.fail) + g0 + ql, (unsigned long long)over[h],
+                                   __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+          pre[ql + 1] = x;
 #pragma nounroll
-        for (uint32_t r = (x - len + 63u) >> 6; r * 64u < x; ++r) rq[r] = (uint16_t)lane;
+          for (uint32_t e = x - len[h]; e < x; ++e) ep[e] = (uint8_t)ql;
+        }
+        if (ql + 1u == gp) gsh[1] = (x + 63u) >> 6;  // rounds of the group
       }
       if (lane == 0) {
         pre[0] = 0;
         gsh[0] = gp;
-      }
-      if ((uint32_t)lane + 1u == gp) {
-        gsh[1] = (x + 63u) >> 6;
-        rq[(x + 63u) >> 6] = (uint16_t)lane;  // sentinel: the last round's search bound
       }
     }
   };
@@ -241,7 +253,7 @@ __global__ __launch_bounds__(kNT, (occupancy<V, M>())) void tile_packed_kernel(
   {
     uint32_t z = 0;  // opaque zero: not a hoisted (and spilled) constant vector
     asm volatile("" : "+v"(z));
-    *(u32x4*)&bt[tid * kBPT] = u32x4{z, z, z, z};
+    *(u32x2*)&bt[tid * kBPT] = u32x2{z, z};
     if (lane < kTS / 32) cbits[w][lane] = z;
   }
   if (tid == 0) pcarry = -1;
@@ -253,9 +265,9 @@ __global__ __launch_bounds__(kNT, (occupancy<V, M>())) void tile_packed_kernel(
   uint32_t Et = np ? uni(pre[gp]) : 0u;  // elements of the group
   uint32_t done = 0, g0 = 0;
   uint32_t nrw = 0, ua = 0, Rw = 0;
-  // per lane and held round r, 8 bits: q | first-of-piece << 6 | exists << 7
-  // (packed 4 rounds per register: a 64-VGPR budget holds 6 rounds unspilled)
-  uint32_t rp[(kCap + 3) / 4];
+  // per lane and held round r, 10 bits: q | first-of-piece << 7 | exists << 8
+  // (packed 3 rounds per register: a 64-VGPR budget holds 6 rounds unspilled)
+  uint32_t rp[(kCap + 2) / 3];
   uint64_t ek[kCap];
   V ev[kCap][M];
   uint32_t mmask = 0;  // wave-uniform: bit r = round r holds more than one push
@@ -268,24 +280,20 @@ __global__ __launch_bounds__(kNT, (occupancy<V, M>())) void tile_packed_kernel(
     nrw = ub > ua ? ub - ua : 0u;
     mmask = 0;
 #pragma unroll
-    for (int r = 0; r < (kCap + 3) / 4; ++r) rp[r] = 0;
+    for (int r = 0; r < (kCap + 2) / 3; ++r) rp[r] = 0;
 #pragma unroll
     for (int r = 0; r < kCap; ++r) {
       if ((uint32_t)r < nrw) {
         const uint32_t R = ua + (uint32_t)r;
         const uint32_t e = R * 64u + (uint32_t)lane;
-        // push of element e: the largest q in [rq[R], rq[R+1]] with pre[q] <= e
-        const uint32_t qlo = uni(rq[R]);
-        const uint32_t qhi = uni(rq[R + 1]);
-        uint32_t q = qlo;
-        const uint32_t span = qhi - qlo;  // wave-uniform trip count
-        for (uint32_t st = span ? 1u << (31 - __builtin_clz(span)) : 0u; st; st >>= 1)
-          if (q + st <= qhi && pre[q + st] <= e) q += st;
         const bool have = e < Et;
-        if (!have) q = qlo;  // a piece that exists: its first element is a safe address
+        // push of element e; lane 0 holds the round's first element, which
+        // exists, so its push is a safe address for the lanes past the end
+        uint32_t q = ep[have ? e : R * 64u];
+        const uint32_t qlo = uni(q);
         const uint32_t i = have ? e - pre[q] : 0u;
         mmask |= (__ballot(have && q != qlo) != 0 ? 1u : 0u) << r;
-        rp[r >> 2] |= (q | (uint32_t)(have && i == 0u) << 6 | (uint32_t)have << 7) << (8 * (r & 3));
+        rp[r / 3] |= (q | (uint32_t)(have && i == 0u) << 7 | (uint32_t)have << 8) << (10 * (r % 3));
         ek[r] = G((const uint64_t*)pkp[q])[i];
 #pragma unroll
         for (int mi = 0; mi < M; ++mi) ev[r][mi] = G((const V*)pvp[q * M + mi])[i];
@@ -310,9 +318,8 @@ __global__ __launch_bounds__(kNT, (occupancy<V, M>())) void tile_packed_kernel(
     }
   __syncthreads();  // (2)
   {
-    const u32x4 h = *(const u32x4*)&bt[tid * kBPT];
-    uint32_t e[kBPT] = {h.x & 0xffffu, h.x >> 16, h.y & 0xffffu, h.y >> 16,
-                        h.z & 0xffffu, h.z >> 16, h.w & 0xffffu, h.w >> 16};
+    const u32x2 h = *(const u32x2*)&bt[tid * kBPT];
+    uint32_t e[kBPT] = {h.x & 0xffffu, h.x >> 16, h.y & 0xffffu, h.y >> 16};
     uint32_t tot = 0;
 #pragma unroll
     for (int j = 0; j < kBPT; ++j) {
@@ -326,9 +333,8 @@ __global__ __launch_bounds__(kNT, (occupancy<V, M>())) void tile_packed_kernel(
     uint32_t off = x - tot;
 #pragma unroll
     for (uint32_t v = 0; v < (uint32_t)kNW - 1u; ++v) off += v < w ? wsum[v] : 0u;
-    const u32x4 o = {(e[0] + off) | (e[1] + off) << 16, (e[2] + off) | (e[3] + off) << 16,
-                     (e[4] + off) | (e[5] + off) << 16, (e[6] + off) | (e[7] + off) << 16};
-    *(u32x4*)&bt[tid * kBPT] = o;
+    const u32x2 o = {(e[0] + off) | (e[1] + off) << 16, (e[2] + off) | (e[3] + off) << 16};
+    *(u32x2*)&bt[tid * kBPT] = o;
     if (tid == 0) bt[kNB] = (uint16_t)nt;
   }
   __syncthreads();  // (4)
@@ -349,7 +355,7 @@ __global__ __launch_bounds__(kNT, (occupancy<V, M>())) void tile_packed_kernel(
       if (U) load_pass();
       continue;
     }
-    auto re = [&](int r) -> uint32_t { return (rp[r >> 2] >> (8 * (r & 3))) & 0xffu; };
+    auto re = [&](int r) -> uint32_t { return (rp[r / 3] >> (10 * (r % 3))) & 0x3ffu; };
     // ---- search every held round
     uint32_t pos[kCap];
     uint32_t okm = 0;  // per lane: bit r = found; bit 8 + r = found and in order
@@ -390,8 +396,8 @@ __global__ __launch_bounds__(kNT, (occupancy<V, M>())) void tile_packed_kernel(
         if (r > 0) prev0 = __builtin_amdgcn_readlane((int)pos[r - 1], 63);
         else prev0 = w > 0 ? lastpos[w - 1] : pcarry;
         int prev = __builtin_amdgcn_update_dpp(prev0, (int)pos[r], 0x138, 0xf, 0xf, false);
-        if ((re(r) >> 6) & 1u) prev = -1;  // first element of its piece
-        const bool ok = ((re(r) >> 7) & 1u) && ((okm >> r) & 1u) && (int)pos[r] > prev;
+        if ((re(r) >> 7) & 1u) prev = -1;  // first element of its piece
+        const bool ok = ((re(r) >> 8) & 1u) && ((okm >> r) & 1u) && (int)pos[r] > prev;
         okm |= (uint32_t)ok << (8 + r);
       }
     }
@@ -400,13 +406,13 @@ __global__ __launch_bounds__(kNT, (occupancy<V, M>())) void tile_packed_kernel(
     {
       uint32_t exist = 0;
 #pragma unroll
-      for (int r = 0; r < kCap; ++r) exist |= ((re(r) >> 7) & 1u) << r;
+      for (int r = 0; r < kCap; ++r) exist |= ((re(r) >> 8) & 1u) << r;
       const uint32_t badm = exist & ~(okm >> 8);
       if (__ballot(badm != 0u)) {
 #pragma unroll
         for (int r = 0; r < kCap; ++r)
           if ((badm >> r) & 1u)
-            __hip_atomic_fetch_add(GW(T.fail) + g0 + (re(r) & 63u), 1ull, __ATOMIC_RELAXED,
+            __hip_atomic_fetch_add(GW(T.fail) + g0 + (re(r) & 127u), 1ull, __ATOMIC_RELAXED,
                                    __HIP_MEMORY_SCOPE_AGENT);
       }
     }
@@ -440,7 +446,7 @@ __global__ __launch_bounds__(kNT, (occupancy<V, M>())) void tile_packed_kernel(
         for (int r = 0; r < kCap; ++r) {
           if ((uint32_t)r < nrw) {
             bool pend = (okm >> (8 + r)) & 1u;
-            const uint32_t q = re(r) & 63u;
+            const uint32_t q = re(r) & 127u;
             const uint32_t s = pos[r];
             const bool first = g0 + q == 0u && !cont;
             auto apply = [&]() {
