@@ -100,6 +100,18 @@ __device__ __forceinline__ uint32_t block_excl_scan(uint32_t v, uint32_t* wsum,
   return (w > 0 ? wsum[w - 1] : 0u) + x - v;
 }
 
+// Scale of the tile kernels' bucket map bucket(x) = umulhi(x, mul): every
+// x <= r32 (< 2^32) lands below nb.  An f32 reciprocal with a 2^-20 margin
+// (reciprocal ~2^-23, conversions and products 2^-24 each) replaces the
+// 64-bit integer division floor(nb * 2^32 / (r32 + 1)), which compiles to a
+// ~100-instruction scalar routine in every wave; only the spread of keys over
+// buckets depends on the exact value, not what a search finds.
+__device__ __forceinline__ uint32_t bucket_scale(uint64_t r32, uint32_t nb) {
+  const float f = (float)nb * 4294967296.0f * (1.0f - 0x1p-20f) *
+                  __builtin_amdgcn_rcpf((float)(r32 + 1ull));
+  return f >= 4294967295.0f ? 0xffffffffu : (uint32_t)f;
+}
+
 // One step of the per-key fold in push-arrival order.  p = push index in
 // this launch, lp = last push index in this launch that held the key (-1:
 // none yet).  Serial (the reference default) adds +0.0 for every absent

@@ -72,6 +72,7 @@ static_assert(kTS <= 0x7ffe, "u16 positions");
 
 typedef unsigned long long u64x2 __attribute__((ext_vector_type(2)));
 typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
+typedef uint32_t u32x2 __attribute__((ext_vector_type(2)));
 
 __device__ __forceinline__ uint32_t uni(uint32_t v) { return __builtin_amdgcn_readfirstlane(v); }
 
@@ -101,7 +102,7 @@ __device__ __forceinline__ uint32_t wave_scan_incl(uint32_t x) {
 // the register budget follows it through __launch_bounds__
 template <typename V, int M, int kGroup>
 constexpr int occupancy() {
-  constexpr int lds = 19328 + (int)(M * sizeof(V) - 4) * kTS + (M - 1) * 8 * kGroup +
+  constexpr int lds = 20352 + (int)(M * sizeof(V) - 4) * kTS + (M - 1) * 8 * kGroup +
                       (kGroup - 32) * (4 + 2 * (kTS / 64) + 4 + 8 + 8);
   return 163840 / lds >= 8 ? 8 : 163840 / lds;
 }
@@ -114,9 +115,11 @@ __global__ __launch_bounds__(kNT, (occupancy<V, M, kGroup>())) void tile_kernel(
   __shared__ __attribute__((aligned(16))) uint32_t bt32[(kNB + 8) / 2];
   uint16_t* const bt = (uint16_t*)bt32;
   __shared__ __attribute__((aligned(16))) V acc[M][kTS];
-  // last push holding the slot, relative to the group base g0: last + 2 - g0,
-  // 0 when it precedes g0 - 1 (so the value fits a byte for any push count)
-  __shared__ __attribute__((aligned(16))) uint8_t lastl[kTS];
+  // serial mode: pushes holding the slot (u16 pairs, counted by non-returning
+  // LDS adds during the search, off the fold's dependency chain): the fold
+  // adds the "+0.0" of absent pushes as ONE trailing +0.0 when the count is
+  // below np (see the stores)
+  __shared__ __attribute__((aligned(16))) uint32_t cnt32[kTS / 2];
   __shared__ uint32_t rpre[kGroup + 1];             // rounds before push q of the group
   __shared__ uint16_t rtab[kGroup * (kTS / 64)];    // round -> q << 4 | chunk
   __shared__ uint32_t pln[kGroup];                  // piece length
@@ -216,21 +219,21 @@ __global__ __launch_bounds__(kNT, (occupancy<V, M, kGroup>())) void tile_kernel(
   const int bits = range ? 64 - __builtin_clzll(range) : 0;
   const int s2 = bits > 32 ? bits - 32 : 0;
   const uint64_t r32 = range >> s2;  // < 2^32
-  const uint64_t mq = ((uint64_t)kNB << 32) / (r32 + 1);
-  const uint32_t mul = mq > 0xffffffffull ? 0xffffffffu : (uint32_t)mq;
+  const uint32_t mul = dev::bucket_scale(r32, kNB);
   auto bucket = [&](uint64_t k) -> uint32_t {
     const uint64_t x = (k - klo) >> s2;
     return x > r32 ? (uint32_t)(kNB - 1) : __umulhi((uint32_t)x, mul);
   };
 
-  // ---- install D, sums, lastl; clear the histogram
+  // ---- install D, sums, counts; clear the histogram
 #pragma unroll
   for (int j = 0; j < 4; ++j) {
     dk[s0 + j] = d[j];
 #pragma unroll
     for (int mi = 0; mi < M; ++mi) acc[mi][s0 + j] = a0[mi][j];
-    lastl[s0 + j] = 1;  // last = -1 = g0 - 1
   }
+  cnt32[2 * tid] = 0u;
+  cnt32[2 * tid + 1] = 0u;
   if (tid < 8) dk[kTS + tid] = ~0ull;
   {
     uint32_t z = 0;  // zero
@@ -319,9 +322,6 @@ __global__ __launch_bounds__(kNT, (occupancy<V, M, kGroup>())) void tile_kernel(
     if (!U) {  // this group of pushes has no keys in the tile, or is done
       g0 += kGroup;
       if (g0 >= np) break;
-      // rebase lastl on the new group: last == g0 - 1 -> 1, older -> 0
-#pragma unroll
-      for (int j = 0; j < 4; ++j) lastl[s0 + j] = lastl[s0 + j] == kGroup + 1 ? 1 : 0;
       load_tables(g0);
       __syncthreads();
       U = uni(rpre[np - g0 < (uint32_t)kGroup ? np - g0 : kGroup]);
@@ -372,6 +372,9 @@ __global__ __launch_bounds__(kNT, (occupancy<V, M, kGroup>())) void tile_kernel(
         const int prev = __builtin_amdgcn_update_dpp(prev0, (int)pos[r], 0x138, 0xf, 0xf, false);
         const bool ok = ((fl >> r) & 1u) && ((fl >> (8 + r)) & 1u) && (int)pos[r] > prev;
         fl |= (uint32_t)ok << (16 + r);
+        if (!parallel && ok)
+          __hip_atomic_fetch_add(&cnt32[pos[r] >> 1], 1u << (16u * (pos[r] & 1u)),
+                                 __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
       }
     }
     // elements that exist but did not match: one ballot per pass, counts per
@@ -397,16 +400,9 @@ __global__ __launch_bounds__(kNT, (occupancy<V, M, kGroup>())) void tile_kernel(
           if ((uint32_t)r < nrw && ((fl >> (16 + r)) & 1u)) {
             const uint32_t q = re[r] >> 4;
             const uint32_t s = pos[r];
-            const uint32_t l1 = lastl[s];
             const bool first = g0 + q == 0u && !cont;
-            const bool gap = !parallel && l1 <= q;  // last < g0 + q - 1
 #pragma unroll
-            for (int mi = 0; mi < M; ++mi) {
-              const V a = acc[mi][s];
-              const V ag = gap ? a + V(0) : a;
-              acc[mi][s] = first ? ev[r][mi] : ag + ev[r][mi];
-            }
-            lastl[s] = (uint8_t)(q + 2u);
+            for (int mi = 0; mi < M; ++mi) acc[mi][s] = first ? ev[r][mi] : acc[mi][s] + ev[r][mi];
           }
         }
         if (w == wl && lane == 63) pcarry = mylast;
@@ -424,12 +420,16 @@ __global__ __launch_bounds__(kNT, (occupancy<V, M, kGroup>())) void tile_kernel(
     if (tid == 0) pcarry = -1;
   }
 
-  // ---- trailing "+0.0" of absent last pushes (serial), stores
+  // ---- the "+0.0" of absent pushes (serial), stores.  The reference adds
+  // +0.0 for every push lacking the key (kv_vector.h:200); adding +0.0 is
+  // the identity except on -0.0 (-> +0.0) and a signalling NaN (quieted),
+  // and once either happened later adds keep the result, so the fold over
+  // the present values followed by ONE +0.0 iff some push lacked the key is
+  // bit-identical to the reference's dense fold
   V res[M][4];
 #pragma unroll
   for (int j = 0; j < 4; ++j) {
-    // the last group's base is g0 - kGroup: gap iff last < np - 1
-    const bool gap = !parallel && (uint32_t)lastl[s0 + j] < np - (g0 - kGroup) + 1u;
+    const bool gap = !parallel && (uint32_t)((const uint16_t*)cnt32)[s0 + j] != np;
 #pragma unroll
     for (int mi = 0; mi < M; ++mi) {
       const V a = acc[mi][s0 + j];

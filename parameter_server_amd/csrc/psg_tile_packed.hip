@@ -40,6 +40,7 @@
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
+#include "psg_device.h"
 #include "psg_internal.h"
 
 #define AS1 __attribute__((address_space(1)))
@@ -234,8 +235,7 @@ __global__ __launch_bounds__(kNT, (occupancy<V, M>())) void tile_packed_kernel(
   const int bits = range ? 64 - __builtin_clzll(range) : 0;
   const int s2 = bits > 32 ? bits - 32 : 0;
   const uint64_t r32 = range >> s2;  // < 2^32
-  const uint64_t mq = ((uint64_t)kNB << 32) / (r32 + 1);
-  const uint32_t mul = mq > 0xffffffffull ? 0xffffffffu : (uint32_t)mq;
+  const uint32_t mul = dev::bucket_scale(r32, kNB);
   auto bucket = [&](uint64_t k) -> uint32_t {
     const uint64_t x = (k - klo) >> s2;
     return x > r32 ? (uint32_t)(kNB - 1) : __umulhi((uint32_t)x, mul);
