@@ -131,7 +131,14 @@ __device__ __forceinline__ void stream_item(const JobDev& J, uint32_t p, uint32_
   // T0 = (splitters <= S[i0-1]) - 1: an interpolated guess checked against a
   // window of 64 splitters around it (murmur-hashed keys and D are near-
   // uniform, so the guess is a few tiles off), else a 64-ary search
+  // The guess's window is 128 splitters (two per lane) starting a little
+  // below the guess, so the splitters the chunk's first window pass needs
+  // (T0 + 1 onwards) are usually already in registers: one dependent round
+  // trip fewer per chunk.  win = index of splitter T0 + 1 in that window.
   int64_t T0 = -1;
+  int64_t g = 0;
+  uint64_t w0 = ~0ull, w1 = ~0ull;
+  int32_t win = -1;
   if (i0 > 0) {
     const uint64_t kp = uni64(S[i0 - 1]);
     const uint64_t s0 = uni64(sp[0]), sn = uni64(sp[nt]);
@@ -139,17 +146,21 @@ __device__ __forceinline__ void stream_item(const JobDev& J, uint32_t p, uint32_
       T0 = nt;
     } else if (kp >= s0) {
       const double f = (double)(kp - s0) / (double)(sn - s0);
-      int64_t g = (int64_t)(f * (double)nt) - 32;
+      g = (int64_t)(f * (double)nt) - 24;
       g = g < 0 ? 0 : (g + 64 > (int64_t)nt + 1 ? (int64_t)nt + 1 - 64 : g);
       g = g < 0 ? 0 : g;
       const int64_t t = g + lane;
-      const bool le = t <= (int64_t)nt && sp[t] <= kp;
+      w0 = t <= (int64_t)nt ? sp[t] : ~0ull;
+      w1 = t + 64 <= (int64_t)nt ? sp[t + 64] : ~0ull;
+      const bool le = t <= (int64_t)nt && w0 <= kp;
       const uint32_t cnt = (uint32_t)__popcll(__ballot(le));
       const bool inside = (cnt > 0 || g == 0) && (cnt < 64 || g + 64 > (int64_t)nt);
-      if (inside)
+      if (inside) {
         T0 = g + (int64_t)cnt - 1;
-      else
+        win = (int32_t)cnt;
+      } else {
         T0 = (int64_t)dev::wave_search(sp, (uint64_t)nt + 1u, kp, true, lane) - 1;
+      }
     }
   }
   // stores before the wave's reads of them: LDS accesses of one wave are
@@ -162,7 +173,16 @@ __device__ __forceinline__ void stream_item(const JobDev& J, uint32_t p, uint32_
   const uint64_t klast = uni64(ck[cl - 1]);
   for (int64_t t0 = T0 + 1; t0 <= (int64_t)nt; t0 += 64) {
     const int64_t t = t0 + lane;
-    const uint64_t sv = t <= (int64_t)nt ? sp[t] : ~0ull;
+    uint64_t sv;
+    if (win >= 0) {  // first pass after an interpolated T0: from the window
+      const int32_t x = win + lane;  // window index of splitter t (< 128)
+      const uint64_t a0 = (uint64_t)__shfl((long long)w0, x & 63, 64);
+      const uint64_t a1 = (uint64_t)__shfl((long long)w1, x & 63, 64);
+      sv = t <= (int64_t)nt ? (x < 64 ? a0 : a1) : ~0ull;
+      win = -1;
+    } else {
+      sv = t <= (int64_t)nt ? sp[t] : ~0ull;
+    }
     // keys of the chunk below sv: lower_bound over ck[0, cl)
     uint32_t pos = 0;
 #pragma unroll

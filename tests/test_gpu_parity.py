@@ -169,6 +169,44 @@ def test_dense_and_crowded_tiles(torch_cuda):
     assert_bitexact(out[0][1], want[0])
 
 
+def extreme_range_keys():
+    """5 tiles of 1024 server keys whose key ranges hit the bucket map's
+    edges: 1023 wide; just under 2^32; exactly 2^32 (33 bits); one crowded
+    bucket (1000 consecutive keys + 24 far ones); up to 2^64 - 2."""
+    u = np.uint64
+    seg0 = np.arange(1024, dtype=u)
+    seg1 = u(1 << 20) + np.arange(1024, dtype=u) * u((2 ** 32 - 1) // 1023)
+    seg2 = np.concatenate([u(1 << 40) + np.arange(1023, dtype=u),
+                           np.array([(1 << 40) + (1 << 32)], u)])
+    seg3 = np.concatenate([u(1 << 50) + np.arange(1000, dtype=u),
+                           u(1 << 50) + u(1 << 30) + np.arange(24, dtype=u) * u(1 << 40)])
+    step = (2 ** 64 - 2 - 2 ** 62) // 1023
+    seg4 = np.array([2 ** 62 + i * step for i in range(1024)], u)
+    D = np.concatenate([seg0, seg1, seg2, seg3, seg4])
+    assert np.all(D[1:] > D[:-1]) and int(D[-1]) <= 2 ** 64 - 2
+    return D
+
+
+@pytest.mark.parametrize("pack", ["0", "1"])
+def test_extreme_key_ranges(torch_cuda, pack, monkeypatch):
+    """Bucket scale (f32 reciprocal with a margin) at the key-range edges,
+    crowded buckets, both round forms and both match modes, bit-exact."""
+    monkeypatch.setenv("PSG_PACK", pack)
+    D = extreme_range_keys()
+    rng = np.random.default_rng(77)
+    pushes = []
+    for p in range(6):
+        k = np.sort(rng.choice(D, D.size // 2, replace=False))
+        v = rng.standard_normal(k.size).astype(np.float32)
+        v[rng.random(k.size) < 0.05] = -0.0
+        pushes.append((k, [v]))
+    for parallel in (False, True):
+        out = run_ctx(D, pushes, parallel=parallel)
+        rc, lo, hi, want, _ = O.aggregate(D, *ALL, pushes, parallel, 1, np.float32)
+        assert rc == 0
+        assert_bitexact(out[0][1], want[0])
+
+
 # ------------------------------------------------------------------- errors
 def test_defined_errors(torch_cuda):
     from parameter_server_amd._lib import (PSGError, PSG_ERR_UNMATCHED, PSG_ERR_RANGE,
