@@ -10,6 +10,10 @@ namespace psg {
 constexpr int kMaxPush = 4096;  // pushes per job per launch
 constexpr int kMaxM = 4;        // value arrays per push
 constexpr int kTileSlots = 1024;  // server slots per aggregate-kernel tile
+// sparse (packed-round) plans use tiles twice as large: each push's piece
+// per tile doubles, so a round's element loads touch half as many pushes
+// (pages) per element
+constexpr int kPackTileSlots = 2048;
 
 constexpr uint32_t kFlagParallel = 1u;  // PSG_PARALLEL_MATCH
 constexpr uint32_t kFlagCont = 2u;      // continue an aggregate of an earlier launch

@@ -243,16 +243,31 @@ struct JobTable {
     device = dev;
     dtype = dt;
     m = mm;
-    const uint32_t tile = psg::kTileSlots;
     const int forced = knob_part;
     h.assign(jobs.size(), JobDev{});
     info.assign(jobs.size(), JobInfo{});
     struct Offs { size_t pk, pv, pn, out, fail, seg, split, dpos; };
     std::vector<Offs> offs(jobs.size());
     uint64_t tiles = 0, items = 0, sitems = 0;
-    double kv_all = 0, pieces_all = 0;
     dense = !jobs.empty();
     for (const JobSpec& s : jobs) dense = dense && s.dense;
+    // the round form first (mean keys per push per 1024-slot tile): it fixes
+    // the tile size, 2048 slots for the packed kernel
+    {
+      const uint64_t t1 = psg::kTileSlots;
+      double kv_all = 0, pieces_all = 0;
+      for (const JobSpec& s : jobs) {
+        uint64_t np = 0;
+        for (uint64_t n : s.pn) {
+          kv_all += (double)n;
+          np += n != 0;
+        }
+        pieces_all += (double)np * (double)((s.nslots + t1 - 1) / t1);
+      }
+      const int fp = knob_pack;
+      pack = fp >= 0 ? fp == 1 : (pieces_all > 0 && kv_all / pieces_all < kPackBelow);
+    }
+    const uint32_t tile = pack && !dense ? psg::kPackTileSlots : psg::kTileSlots;
     for (size_t j = 0; j < jobs.size(); ++j) {
       const JobSpec& s = jobs[j];
       JobInfo& I = info[j];
@@ -278,9 +293,9 @@ struct JobTable {
       d.npush = I.np;
       d.ntiles = I.ntiles;
       d.tile = tile;
-      const double piece = I.np && I.ntiles ? (double)kv / ((double)I.np * I.ntiles) : 1e9;
-      kv_all += (double)kv;
-      pieces_all += (double)I.np * I.ntiles;
+      // keys per push per 1024 slots (the partition modes' calibration unit)
+      const uint64_t nt1 = (s.nslots + psg::kTileSlots - 1) / psg::kTileSlots;
+      const double piece = I.np && nt1 ? (double)kv / ((double)I.np * nt1) : 1e9;
       d.mode = s.dense ? psg::kSearch
                        : forced >= 0 ? (uint32_t)forced
                                      : (piece < kStreamBelow ? psg::kStream : psg::kSearch);
@@ -302,8 +317,6 @@ struct JobTable {
       if (j >= (1ull << 27)) return fail(PSG_ERR_ARG, "too many jobs");
     }
     {
-      const int fp = knob_pack;
-      pack = fp >= 0 ? fp == 1 : (pieces_all > 0 && kv_all / pieces_all < kPackBelow);
       uint32_t maxnp = 0;
       for (const JobInfo& I : info) maxnp = std::max(maxnp, I.np);
       wide = knob_wide >= 0 ? knob_wide == 1 : maxnp > 32;

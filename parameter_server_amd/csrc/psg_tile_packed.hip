@@ -1,6 +1,8 @@
 // psg_tile_packed.hip -- the aggregate kernel for sparse jobs (many short
-// pieces per tile): one 256-thread workgroup per tile of kTS = 1024 server
-// slots.  Jobs whose pieces are long go to psg_tile.hip's push-uniform
+// pieces per tile): one 512-thread workgroup (8 waves) per tile of
+// kTS = 2048 server slots (twice the tile kernel's: a push's piece per tile
+// doubles, so each round's loads touch half as many pushes' pages per
+// element; 4 workgroups, 32 waves per CU).  Jobs whose pieces are long go to psg_tile.hip's push-uniform
 // rounds instead (the runtime picks by mean piece length, kPackBelow).
 //
 // Reference semantics: KVVector::serialSetValue / parallelSetValue
@@ -25,7 +27,7 @@
 //   * D goes to LDS; a bucket table (1 bucket per slot over the tile's key
 //     range, one high multiply) turns a search into one table read and one
 //     paired key read;
-//   * the fold runs wave by wave (4 barrier steps): rounds are push-major
+//   * the fold runs wave by wave (8 barrier steps): rounds are push-major
 //     and waves hold contiguous runs of them, so every slot sees its
 //     contributions in arrival order with no atomics.  Inside one round two
 //     pushes can hit one slot: a per-wave slot bitmap detects that, and such
@@ -58,11 +60,11 @@ __device__ __forceinline__ AS1 T* GW(T* p) {
   return (AS1 T*)p;
 }
 
-constexpr int kTS = kTileSlots;  // slots per tile
-constexpr int kNT = 256;         // threads
+constexpr int kTS = kPackTileSlots;  // slots per tile
+constexpr int kNT = 512;             // threads
 constexpr int kNW = kNT / 64;    // waves
 constexpr int kSPT = kTS / kNT;  // slots per thread (contiguous)
-constexpr int kNB = kTS;         // buckets (one per slot: the LDS budget of 8 workgroups per CU)
+constexpr int kNB = kTS;         // buckets (one per slot: the LDS budget of 4 workgroups per CU)
 constexpr int kBPT = kNB / kNT;  // bucket-table entries per thread in the scan
 constexpr int kCap = 6;          // rounds a wave holds per pass
 constexpr int kG = 128;          // pushes per group (two lanes' worth per lane of wave 0)
@@ -96,12 +98,14 @@ __device__ __forceinline__ uint32_t wave_scan_incl(uint32_t x) {
   return x;
 }
 
-// workgroups per CU the LDS allows (8 for the f32, m = 1 headline case):
+// waves per SIMD the LDS allows (8 for the f32, m = 1 case: 4 workgroups per CU):
 // the register budget follows it through __launch_bounds__
 template <typename V, int M>
 constexpr int occupancy() {
-  constexpr int lds = 20116 + (int)(M * sizeof(V) - 4) * kTS + (M - 1) * 8 * kG;
-  return 163840 / lds >= 8 ? 8 : 163840 / lds;
+  constexpr int lds = 38560 + (int)(M * sizeof(V) - 4) * kTS + (M - 1) * 8 * kG;
+  // waves per SIMD (the launch bound's unit): workgroups per CU x waves / 4
+  constexpr int w = (163840 / lds) * kNW / 4;
+  return w >= 8 ? 8 : (w < 1 ? 1 : w);
 }
 
 // rounds of 64 consecutive elements of the concatenated pieces: a round

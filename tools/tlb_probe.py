@@ -27,10 +27,10 @@ def run(name, insts):
     plan, keep, jobs = bench.make_plan(insts, dev, 0)
     stream = torch.cuda.current_stream()
     _, part, agg = bench.timed_steps(plan, 10, 2, stream, None)
-    tiles = sum((int(j["nslots"]) + 1023) // 1024 for j in jobs)
+    slots = sum(int(j["nslots"]) for j in jobs)
     kv = int(plan.kv_pairs)
-    print(f"{name}: {len(jobs)} jobs, {tiles} tiles, {kv} kv: aggregate {agg:.3f} ms "
-          f"({agg * 1e3 / tiles * 2048:.1f} us per 2048 tiles), partition {part:.3f} ms", flush=True)
+    print(f"{name}: {len(jobs)} jobs, {slots} slots, {kv} kv: aggregate {agg:.3f} ms "
+          f"({agg * 1e6 / kv:.2f} ns per 1000 kv), partition {part:.3f} ms", flush=True)
     del plan, keep
     torch.cuda.empty_cache()
 
