@@ -60,6 +60,12 @@ WORKLOADS = {
 }
 
 
+# the aggregate kernel each workload's plan runs (the runtime picks the form:
+# dense slices, short pieces -> packed rounds, > 32 pushes -> 64-push groups)
+KERNEL = {"cfg2": "tile_kernel<float,1,32>", "cfg3": "tile_kernel<float,1,64>",
+          "cfg4": "dense_kernel<float,1>", "cfg5": "tile_packed_kernel<float,1>"}
+
+
 def parse():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -252,7 +258,7 @@ def main():
             "unit": "GB/s",
             "frac": achieved / HBM_PEAK_GBPS,
             "traffic": traffic.get("tile") if traffic else None,
-            "kernel": "tile_kernel<float,1>",
+            "kernel": KERNEL[wl],
             "bytes_per_launch": nbytes,
             "bytes_formula": formula,
             "kernel_ms": agg_ms,
