@@ -53,10 +53,48 @@ __global__ __launch_bounds__(256) void splitter_kernel(const JobDev* __restrict_
 }
 
 // ---- kSearch: one lane per (push, tile boundary) ----
+// lower_bound(S, xl) inside a bracket with S[a] < xl <= S[c]: interpolation
+// probes (pushes of murmur-hashed keys are near-uniform), bisection, then
+// the last <= 15 candidates in one round trip
+__device__ __forceinline__ uint64_t bracket_search(const uint64_t* S, uint64_t xl, uint64_t a,
+                                                   uint64_t c, uint64_t ka, uint64_t kc) {
+  for (int it = 0; it < 6 && c - a > 16u; ++it) {
+    const double f = (double)(xl - ka) / (double)(kc - ka);
+    uint64_t mid = a + 1 + (uint64_t)(f * (double)(c - a - 1));
+    mid = mid < c ? mid : c - 1;
+    const uint64_t km = S[mid];
+    if (km < xl) {
+      a = mid;
+      ka = km;
+    } else {
+      c = mid;
+      kc = km;
+    }
+  }
+  while (c - a > 16u) {
+    const uint64_t mid = a + ((c - a) >> 1);
+    if (S[mid] < xl) a = mid; else c = mid;
+  }
+  // independent loads of S[a+1 .. c-1] (indices clamped to c, where
+  // S[c] >= xl counts 0)
+  uint32_t below = 0;
+#pragma unroll
+  for (uint32_t i = 1; i < 16u; ++i) {
+    const uint64_t idx = a + i < c ? a + i : c;
+    below += S[idx] < xl ? 1u : 0u;
+  }
+  return a + 1u + below;
+}
+
+// A wave holds 64 consecutive boundaries of one push.  Its first and last
+// lanes search the whole push; the lanes between start from the bracket
+// their answers give (about 63 tiles' worth of the push instead of all of
+// it), which saves about one probe line per boundary (the partition is
+// bound by the random lines it reads).  A bracket that does
+// not hold (an unsorted push) falls back to the whole push.
 __device__ __forceinline__ void search_item(const JobDev& J, uint32_t p, uint32_t g, int lane) {
   const uint32_t b = (g << 6) + (uint32_t)lane;
   const bool valid = b <= J.ntiles;
-  uint64_t res = 0;
   const uint64_t* S = J.pkeys[p];
   const uint64_t n = J.pn[p];
   const uint32_t bc = valid ? b : J.ntiles;
@@ -65,39 +103,31 @@ __device__ __forceinline__ void search_item(const JobDev& J, uint32_t p, uint32_
   // upper_bound(x) == lower_bound(x + 1): D never holds 2^64-1
   const uint64_t xl = up ? x + 1ull : x;
   const uint64_t k0 = S[0], kn = S[n - 1];
-  if (xl <= k0) {
-    res = 0;
-  } else if (xl > kn) {
-    res = n;
-  } else {
-    // invariant S[a] < xl <= S[c]; interpolation probes, then bisection
-    uint64_t a = 0, c = n - 1, ka = k0, kc = kn;
-    for (int it = 0; it < 6 && c - a > 16u; ++it) {
-      const double f = (double)(xl - ka) / (double)(kc - ka);
-      uint64_t mid = a + 1 + (uint64_t)(f * (double)(c - a - 1));
-      mid = mid < c ? mid : c - 1;
-      const uint64_t km = S[mid];
-      if (km < xl) {
-        a = mid;
-        ka = km;
-      } else {
-        c = mid;
-        kc = km;
+  // the wave's last valid lane (invalid lanes repeat boundary ntiles)
+  const int last = (int)((J.ntiles - (g << 6)) < 63u ? (J.ntiles - (g << 6)) : 63u);
+  const bool edge = lane == 0 || lane == last;
+  uint64_t res = 0;
+  if (edge) {
+    res = xl <= k0 ? 0 : (xl > kn ? n : bracket_search(S, xl, 0, n - 1, k0, kn));
+  }
+  const uint64_t r0 = (uint64_t)__shfl((long long)res, 0, 64);
+  const uint64_t r1 = (uint64_t)__shfl((long long)res, last, 64);
+  if (!edge) {
+    if (xl <= k0) {
+      res = 0;
+    } else if (xl > kn) {
+      res = n;
+    } else {
+      uint64_t a = r0 > 0 ? r0 - 1 : 0, c = r1 < n ? r1 : n - 1;
+      uint64_t ka = 0, kc = 0;
+      bool ok = a < c;
+      if (ok) {
+        ka = S[a];
+        kc = S[c];
+        ok = ka < xl && xl <= kc;
       }
+      res = ok ? bracket_search(S, xl, a, c, ka, kc) : bracket_search(S, xl, 0, n - 1, k0, kn);
     }
-    while (c - a > 16u) {
-      const uint64_t mid = a + ((c - a) >> 1);
-      if (S[mid] < xl) a = mid; else c = mid;
-    }
-    // the last <= 15 candidates in one round trip: independent loads of
-    // S[a+1 .. c-1] (indices clamped to c, where S[c] >= xl counts 0)
-    uint32_t below = 0;
-#pragma unroll
-    for (uint32_t i = 1; i < 16u; ++i) {
-      const uint64_t idx = a + i < c ? a + i : c;
-      below += S[idx] < xl ? 1u : 0u;
-    }
-    res = a + 1u + below;
   }
   if (valid) {
     J.seg[(size_t)p * J.segq + (size_t)b * J.segb] = (uint32_t)res;
