@@ -23,7 +23,7 @@ constexpr uint32_t kFlagCont = 2u;      // continue an aggregate of an earlier l
 //          per boundary, right when pieces are long (cfg2: ~140 keys);
 // kStream: every push key read once and mapped to its tile through the
 //          job's splitter array -- cost per key, right when pieces are
-//          short (many sparse pushes: cfg3 ~29 keys, cfg5 ~4).
+//          short (many sparse pushes: cfg5 ~4 keys).
 enum PartMode : uint32_t { kSearch = 0, kStream = 1 };
 constexpr uint32_t kStreamChunk = 256;  // push keys per streaming-partition wave
 
