@@ -25,7 +25,7 @@ constexpr uint32_t kFlagCont = 2u;      // continue an aggregate of an earlier l
 //          job's splitter array -- cost per key, right when pieces are
 //          short (many sparse pushes: cfg5 ~4 keys).
 enum PartMode : uint32_t { kSearch = 0, kStream = 1 };
-constexpr uint32_t kStreamChunk = 256;  // push keys per streaming-partition wave
+constexpr uint32_t kStreamChunk = 512;  // push keys per streaming-partition wave
 
 // One (channel, time) aggregate as the partition kernels see it.  All
 // pointers are device pointers.  seg[p*segq + b*segb] = first index of push

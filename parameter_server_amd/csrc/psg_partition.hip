@@ -15,7 +15,7 @@
 //            murmur-hashed keys are near-uniform over their range), then a
 //            bisection, then one batch of 15 independent loads.  Costs a few
 //            random lines per boundary: the right choice for long pieces.
-//   kStream: one wave per 256 consecutive keys of one push; every key is
+//   kStream: one wave per 512 consecutive keys of one push; every key is
 //            mapped to its tile through the job's splitter array
 //            split[t] = D[t*tile] (split[ntiles] = D[nslots-1] + 1), and the
 //            tile transitions between consecutive keys write seg.  Costs
@@ -136,6 +136,7 @@ __device__ __forceinline__ void search_item(const JobDev& J, uint32_t p, uint32_
 }
 
 // ---- kStream: one wave per kStreamChunk consecutive keys of one push ----
+constexpr uint32_t kKPL = kStreamChunk / 64;  // keys per lane
 // seg[p][t] = lower_bound(S_p, split[t]).  A chunk [i0, i0 + cl) owns the
 // splitters whose lower bound falls inside it (the push's last chunk also
 // those past its last key): split[t] > S[i0-1] and split[t] <= S[i0+cl-1].
@@ -152,10 +153,10 @@ __device__ __forceinline__ void stream_item(const JobDev& J, uint32_t p, uint32_
   const uint32_t cl = (uint32_t)(n - i0 < kStreamChunk ? n - i0 : kStreamChunk);
   const bool last = i0 + cl == n;
   // the chunk's keys into LDS (4 per lane); +inf past the push's end
-  uint64_t k[4];
+  uint64_t k[kKPL];
 #pragma unroll
-  for (int j = 0; j < 4; ++j) {
-    const uint32_t x = 4u * (uint32_t)lane + j;
+  for (int j = 0; j < kKPL; ++j) {
+    const uint32_t x = kKPL * (uint32_t)lane + j;
     k[j] = x < cl ? S[i0 + x] : ~0ull;
   }
   // T0 = (splitters <= S[i0-1]) - 1: an interpolated guess checked against a
@@ -196,7 +197,7 @@ __device__ __forceinline__ void stream_item(const JobDev& J, uint32_t p, uint32_
   // stores before the wave's reads of them: LDS accesses of one wave are
   // ordered; the fences keep the compiler from moving the reads up
 #pragma unroll
-  for (int j = 0; j < 4; ++j) ck[4 * lane + j] = k[j];
+  for (int j = 0; j < kKPL; ++j) ck[kKPL * lane + j] = k[j];
   __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
   __builtin_amdgcn_wave_barrier();
   __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
@@ -227,12 +228,12 @@ __device__ __forceinline__ void stream_item(const JobDev& J, uint32_t p, uint32_
   // order check: a key not above its predecessor cannot match
   uint32_t bad = 0;
   {
-    const uint64_t kprev_l = (uint64_t)__shfl_up((long long)k[3], 1, 64);
+    const uint64_t kprev_l = (uint64_t)__shfl_up((long long)k[kKPL - 1], 1, 64);
     uint64_t prev = lane == 0 ? (i0 > 0 ? S[i0 - 1] : 0ull) : kprev_l;
     bool has = lane > 0 || i0 > 0;
 #pragma unroll
-    for (int j = 0; j < 4; ++j) {
-      if (4u * (uint32_t)lane + j < cl) {
+    for (int j = 0; j < kKPL; ++j) {
+      if (kKPL * (uint32_t)lane + j < cl) {
         if (has && !(prev < k[j])) ++bad;
         prev = k[j];
         has = true;

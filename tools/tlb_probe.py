@@ -30,7 +30,7 @@ def run(name, insts):
     slots = sum(int(j["nslots"]) for j in jobs)
     kv = int(plan.kv_pairs)
     print(f"{name}: {len(jobs)} jobs, {slots} slots, {kv} kv: aggregate {agg:.3f} ms "
-          f"({agg * 1e6 / kv:.2f} ns per 1000 kv), partition {part:.3f} ms", flush=True)
+          f"({agg * 1e9 / kv:.2f} ps per kv), partition {part:.3f} ms", flush=True)
     del plan, keep
     torch.cuda.empty_cache()
 
