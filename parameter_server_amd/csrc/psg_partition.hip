@@ -86,10 +86,10 @@ __device__ __forceinline__ uint64_t bracket_search(const uint64_t* S, uint64_t x
   return a + 1u + below;
 }
 
-// A wave holds 64 consecutive boundaries of one push.  Its first and last
-// lanes search the whole push; the lanes between start from the bracket
-// their answers give (about 63 tiles' worth of the push instead of all of
-// it), which saves about one probe line per boundary (the partition is
+// A wave holds 64 consecutive boundaries of one push.  Every 16th lane and
+// the last search the whole push; the lanes between start from the bracket
+// their neighbours' answers give (about 16 tiles' worth of the push instead
+// of all of it), which saves probe lines per boundary (the partition is
 // bound by the random lines it reads).  A bracket that does
 // not hold (an unsorted push) falls back to the whole push.
 __device__ __forceinline__ void search_item(const JobDev& J, uint32_t p, uint32_t g, int lane) {
@@ -105,13 +105,16 @@ __device__ __forceinline__ void search_item(const JobDev& J, uint32_t p, uint32_
   const uint64_t k0 = S[0], kn = S[n - 1];
   // the wave's last valid lane (invalid lanes repeat boundary ntiles)
   const int last = (int)((J.ntiles - (g << 6)) < 63u ? (J.ntiles - (g << 6)) : 63u);
-  const bool edge = lane == 0 || lane == last;
+  // bracketing lanes: every 16th and the last valid one
+  const bool edge = (lane & 15) == 0 || lane == last;
+  const int lo_l = lane & ~15;
+  const int hi_l = lo_l + 16 < last ? lo_l + 16 : last;
   uint64_t res = 0;
   if (edge) {
     res = xl <= k0 ? 0 : (xl > kn ? n : bracket_search(S, xl, 0, n - 1, k0, kn));
   }
-  const uint64_t r0 = (uint64_t)__shfl((long long)res, 0, 64);
-  const uint64_t r1 = (uint64_t)__shfl((long long)res, last, 64);
+  const uint64_t r0 = (uint64_t)__shfl((long long)res, lo_l, 64);
+  const uint64_t r1 = (uint64_t)__shfl((long long)res, hi_l, 64);
   if (!edge) {
     if (xl <= k0) {
       res = 0;
