@@ -7,8 +7,9 @@
 // (src/parameter/kv_vector.h:84-204) over oldMatch / match
 // (src/system/message.h:134-267): out[j] = fold over pushes p in arrival
 // order of V_p[k] where S_p[k] == D[lo+j]; the first push assigns, later
-// pushes add, and the serial path adds +0.0 for absent pushes (one "+0.0"
-// per run of absent pushes is exact, see dev::fold_step).
+// pushes add, and the serial path adds +0.0 for absent pushes: one "+0.0"
+// after the fold, iff a push lacked the key, is bit-identical (see the
+// stores).
 //
 // Shape:
 //   * the partition (psg_partition.hip) has cut every push at every tile's
@@ -25,8 +26,8 @@
 //     one table read and one paired key read;
 //   * the fold runs wave by wave (4 barrier steps): rounds are push-major
 //     and waves hold contiguous runs of them, so every slot sees its
-//     contributions in arrival order with no atomics; sums and "last push
-//     holding the slot" live in LDS;
+//     contributions in arrival order with no atomics; sums and per-slot
+//     contributor counts (serial mode) live in LDS;
 //   * thread t owns slots 4t..4t+3: 16-B loads of D and 16-B stores;
 //   * consecutive tiles run on one XCD (blocks b and b+8 share one), so the
 //     cache lines two neighbouring tiles' pieces share are read once.
