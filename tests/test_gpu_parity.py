@@ -169,6 +169,23 @@ def test_dense_and_crowded_tiles(torch_cuda):
     assert_bitexact(out[0][1], want[0])
 
 
+@pytest.mark.parametrize("dtype,m", [(np.float64, 1), (np.float64, 2), (np.float32, 3),
+                                     (np.float32, 4), (np.float64, 4)])
+def test_packed_rounds_value_types(torch_cuda, dtype, m, monkeypatch):
+    """The packed kernel (2048-slot tiles) for every value type and array
+    count it instantiates, sparse pushes spanning several tiles and push
+    groups, serial and parallel, bit-exact against the oracle."""
+    monkeypatch.setenv("PSG_PACK", "1")
+    D, pushes = random_case(31 + m, dtype, m, 150, 0.004, 30000)
+    pushes = [p for p in pushes if p[0].size]
+    for parallel in (False, True):
+        out = run_ctx(D, pushes, dtype=dtype, parallel=parallel)
+        rc, lo, hi, want, _ = O.aggregate(D, *ALL, pushes, parallel, 1, dtype)
+        assert rc == 0 and len(out) == m
+        for i in range(m):
+            assert_bitexact(out[i][1], want[i])
+
+
 def extreme_range_keys():
     """5 tiles of 1024 server keys whose key ranges hit the bucket map's
     edges: 1023 wide; just under 2^32; exactly 2^32 (33 bits); one crowded
