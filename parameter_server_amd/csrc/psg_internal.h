@@ -14,6 +14,8 @@ constexpr int kTileSlots = 1024;  // server slots per aggregate-kernel tile
 // per tile doubles, so a round's element loads touch half as many pushes
 // (pages) per element
 constexpr int kPackTileSlots = 2048;
+// and so do tile-kernel plans with more than 32 pushes (psg_tile.hip)
+constexpr int kWideSlots = 2048;
 
 constexpr uint32_t kFlagParallel = 1u;  // PSG_PARALLEL_MATCH
 constexpr uint32_t kFlagCont = 2u;      // continue an aggregate of an earlier launch

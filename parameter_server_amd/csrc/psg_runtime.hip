@@ -253,23 +253,29 @@ struct JobTable {
     uint64_t tiles = 0, items = 0, sitems = 0;
     dense = !jobs.empty();
     for (const JobSpec& s : jobs) dense = dense && s.dense;
-    // the round form first (mean keys per push per 1024-slot tile): it fixes
-    // the tile size, 2048 slots for the packed kernel
+    // the round form first (mean keys per push per 1024-slot tile) and the
+    // push-group size: they fix the tile size, 2048 slots for the packed
+    // kernel and for the tile kernel's 64-push form
     {
       const uint64_t t1 = psg::kTileSlots;
       double kv_all = 0, pieces_all = 0;
+      uint32_t maxnp = 0;
       for (const JobSpec& s : jobs) {
-        uint64_t np = 0;
+        uint32_t np = 0;
         for (uint64_t n : s.pn) {
           kv_all += (double)n;
           np += n != 0;
         }
+        maxnp = std::max(maxnp, np);
         pieces_all += (double)np * (double)((s.nslots + t1 - 1) / t1);
       }
       const int fp = knob_pack;
       pack = fp >= 0 ? fp == 1 : (pieces_all > 0 && kv_all / pieces_all < kPackBelow);
+      wide = knob_wide >= 0 ? knob_wide == 1 : maxnp > 32;
     }
-    const uint32_t tile = pack && !dense ? psg::kPackTileSlots : psg::kTileSlots;
+    const uint32_t tile = dense ? psg::kTileSlots
+                          : pack ? psg::kPackTileSlots
+                                 : wide ? psg::kWideSlots : psg::kTileSlots;
     for (size_t j = 0; j < jobs.size(); ++j) {
       const JobSpec& s = jobs[j];
       JobInfo& I = info[j];
@@ -317,11 +323,6 @@ struct JobTable {
       if (tiles >= (1ull << 31) || items >= (1ull << 31) || sitems >= (1ull << 31))
         return fail(PSG_ERR_ARG, "batch too large (%llu tiles)", (unsigned long long)tiles);
       if (j >= (1ull << 27)) return fail(PSG_ERR_ARG, "too many jobs");
-    }
-    {
-      uint32_t maxnp = 0;
-      for (const JobInfo& I : info) maxnp = std::max(maxnp, I.np);
-      wide = knob_wide >= 0 ? knob_wide == 1 : maxnp > 32;
     }
     size_t off = align_up(sizeof(JobDev) * jobs.size(), 256);
     const size_t tiles_off = off;

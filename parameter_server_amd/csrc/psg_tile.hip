@@ -1,5 +1,6 @@
 // psg_tile.hip -- the aggregate kernel for long pieces (push-uniform rounds):
-// one 256-thread workgroup per tile of kTS server slots, built for
+// one workgroup per tile of kTS server slots (1024 slots and 256 threads, or
+// 2048 and 512 for jobs of more than 32 pushes), built for
 // instruction efficiency.  psg_tile_packed.hip is its form for many short
 // pieces (rounds that pack several pushes).
 //
@@ -59,17 +60,16 @@ __device__ __forceinline__ AS1 T* GW(T* p) {
   return (AS1 T*)p;
 }
 
-constexpr int kTS = kTileSlots;  // slots per tile
-constexpr int kNT = 256;         // threads
-constexpr int kNW = kNT / 64;    // waves
-constexpr int kSPT = kTS / kNT;  // slots per thread (contiguous)
-constexpr int kNB = 2 * kTS;     // buckets
-constexpr int kBPT = kNB / kNT;  // bucket-table entries per thread in the scan
-// pushes per group (one lane of wave 0 each): 32, or 64 for jobs of more
-// than 32 pushes (one table phase and fewer, fuller passes per 64 pushes, at
-// 7 instead of 8 workgroups per CU)
-static_assert(kSPT == 4 && kBPT == 8, "layout");
-static_assert(kTS <= 0x7ffe, "u16 positions");
+// Two forms, by pushes per group (one lane of wave 0 each):
+//   32 pushes: 1024-slot tiles, 256 threads, 2 buckets per slot;
+//   64 pushes (jobs of more than 32 pushes): 2048-slot tiles (kWideSlots),
+//      512 threads, 1 bucket per slot -- each push's piece per tile doubles,
+//      so its push-uniform rounds are fuller (cfg3: ~30 -> ~60 of 64 lanes).
+constexpr int ts_of(int g) { return g == 64 ? kWideSlots : kTileSlots; }
+constexpr int nt_of(int g) { return ts_of(g) / 4; }
+constexpr int nb_of(int g) { return g == 64 ? ts_of(g) : 2 * ts_of(g); }
+constexpr int cb_of(int g) { return ts_of(g) / 64 > 16 ? 5 : 4; }  // round-chunk bits
+static_assert(ts_of(64) <= 0x7ffe, "u16 positions");
 
 typedef unsigned long long u64x2 __attribute__((ext_vector_type(2)));
 typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
@@ -103,14 +103,25 @@ __device__ __forceinline__ uint32_t wave_scan_incl(uint32_t x) {
 // the register budget follows it through __launch_bounds__
 template <typename V, int M, int kGroup>
 constexpr int occupancy() {
-  constexpr int lds = 20352 + (int)(M * sizeof(V) - 4) * kTS + (M - 1) * 8 * kGroup +
-                      (kGroup - 32) * (4 + 2 * (kTS / 64) + 4 + 8 + 8);
-  return 163840 / lds >= 8 ? 8 : 163840 / lds;
+  constexpr int ts = ts_of(kGroup), nw = nt_of(kGroup) / 64;
+  constexpr int lds = (ts + 8) * 8 + (nb_of(kGroup) + 8) * 2 + M * (int)sizeof(V) * ts + ts * 2 +
+                      (kGroup + 1) * 4 + kGroup * (ts / 64) * 2 + kGroup * 12 + kGroup * M * 8 +
+                      nw * 8 + 8;
+  // waves per SIMD (the launch bound's unit): workgroups per CU x waves / 4
+  constexpr int w = (163840 / lds) * nw / 4;
+  return w >= 8 ? 8 : (w < 1 ? 1 : w);
 }
 
 template <typename V, int M, int kGroup>
-__global__ __launch_bounds__(kNT, (occupancy<V, M, kGroup>())) void tile_kernel(
+__global__ __launch_bounds__(nt_of(kGroup), (occupancy<V, M, kGroup>())) void tile_kernel(
     const TileDesc* __restrict__ tiles, uint32_t ntiles) {
+  constexpr int kTS = ts_of(kGroup);   // slots per tile
+  constexpr int kNT = nt_of(kGroup);   // threads
+  constexpr int kNW = kNT / 64;        // waves
+  constexpr int kNB = nb_of(kGroup);   // buckets
+  constexpr int kBPT = kNB / kNT;      // bucket-table entries per thread in the scan
+  constexpr int kCB = cb_of(kGroup);   // bits of a round's chunk index
+  static_assert(kTS / kNT == 4 && (kBPT == 8 || kBPT == 4), "layout");
   __shared__ __attribute__((aligned(16))) uint64_t dk[kTS + 8];
   // bucket starts (u16); the histogram counts in it as packed pairs by 32-bit atomics
   __shared__ __attribute__((aligned(16))) uint32_t bt32[(kNB + 8) / 2];
@@ -122,7 +133,7 @@ __global__ __launch_bounds__(kNT, (occupancy<V, M, kGroup>())) void tile_kernel(
   // below np (see the stores)
   __shared__ __attribute__((aligned(16))) uint32_t cnt32[kTS / 2];
   __shared__ uint32_t rpre[kGroup + 1];             // rounds before push q of the group
-  __shared__ uint16_t rtab[kGroup * (kTS / 64)];    // round -> q << 4 | chunk
+  __shared__ uint16_t rtab[kGroup * (kTS / 64)];    // round -> q << kCB | chunk
   __shared__ uint32_t pln[kGroup];                  // piece length
   __shared__ uint64_t pkp[kGroup], pvp[kGroup * M];  // piece starts (keys, values)
   __shared__ int lastpos[kNW];
@@ -185,7 +196,7 @@ __global__ __launch_bounds__(kNT, (occupancy<V, M, kGroup>())) void tile_kernel(
       if (lane < kGroup) rpre[lane + 1] = x;
       if (lane == 0) rpre[0] = 0;
 #pragma nounroll
-      for (uint32_t c = 0; c < nr; ++c) rtab[x - nr + c] = (uint16_t)((uint32_t)lane << 4 | c);
+      for (uint32_t c = 0; c < nr; ++c) rtab[x - nr + c] = (uint16_t)((uint32_t)lane << kCB | c);
     }
   };
   if (np) load_tables(0);
@@ -238,7 +249,8 @@ __global__ __launch_bounds__(kNT, (occupancy<V, M, kGroup>())) void tile_kernel(
   if (tid < 8) dk[kTS + tid] = ~0ull;
   {
     uint32_t z = 0;  // zero
-    *(u32x4*)&bt[tid * kBPT] = u32x4{z, z, z, z};
+#pragma unroll
+    for (int i = 0; i < kBPT / 2; ++i) bt32[tid * (kBPT / 2) + i] = z;
   }
   if (tid == 0) pcarry = -1;
   __syncthreads();  // (1) tables, D, cleared histogram
@@ -247,7 +259,7 @@ __global__ __launch_bounds__(kNT, (occupancy<V, M, kGroup>())) void tile_kernel(
   uint32_t done = 0, U = np ? uni(rpre[np < (uint32_t)kGroup ? np : kGroup]) : 0u;
   uint32_t g0 = 0;
   uint32_t nrw = 0, ua = 0, Rw = 0;
-  uint32_t re[kCap];  // round: q << 4 | chunk (the same in every lane)
+  uint32_t re[kCap];  // round: q << kCB | chunk (the same in every lane)
   uint64_t ek[kCap];
   V ev[kCap][M];
   uint32_t fl = 0;  // per lane: bit r = element of round r exists, bit 8+r = found,
@@ -265,8 +277,8 @@ __global__ __launch_bounds__(kNT, (occupancy<V, M, kGroup>())) void tile_kernel(
       re[r] = 0;
       if ((uint32_t)r < nrw) {
         const uint32_t e = rtab[ua + (uint32_t)r];
-        const uint32_t q = e >> 4;
-        const uint32_t i = (e & 15u) * 64u + (uint32_t)lane;
+        const uint32_t q = e >> kCB;
+        const uint32_t i = (e & ((1u << kCB) - 1u)) * 64u + (uint32_t)lane;
         re[r] = e;
         const bool have = i < pln[q];
         fl |= (uint32_t)have << r;  // shift of a 0/1: no literal masks held in VGPRs
@@ -296,9 +308,13 @@ __global__ __launch_bounds__(kNT, (occupancy<V, M, kGroup>())) void tile_kernel(
     }
   __syncthreads();  // (2)
   {
-    const u32x4 h = *(const u32x4*)&bt[tid * kBPT];
-    uint32_t e[kBPT] = {h.x & 0xffffu, h.x >> 16, h.y & 0xffffu, h.y >> 16,
-                        h.z & 0xffffu, h.z >> 16, h.w & 0xffffu, h.w >> 16};
+    uint32_t e[kBPT];
+#pragma unroll
+    for (int i = 0; i < kBPT / 2; ++i) {
+      const uint32_t h = bt32[tid * (kBPT / 2) + i];
+      e[2 * i] = h & 0xffffu;
+      e[2 * i + 1] = h >> 16;
+    }
     uint32_t tot = 0;
 #pragma unroll
     for (int j = 0; j < kBPT; ++j) {
@@ -312,9 +328,9 @@ __global__ __launch_bounds__(kNT, (occupancy<V, M, kGroup>())) void tile_kernel(
     uint32_t off = x - tot;
 #pragma unroll
     for (uint32_t v = 0; v < (uint32_t)kNW - 1u; ++v) off += v < w ? wsum[v] : 0u;
-    const u32x4 o = {(e[0] + off) | (e[1] + off) << 16, (e[2] + off) | (e[3] + off) << 16,
-                     (e[4] + off) | (e[5] + off) << 16, (e[6] + off) | (e[7] + off) << 16};
-    *(u32x4*)&bt[tid * kBPT] = o;
+#pragma unroll
+    for (int i = 0; i < kBPT / 2; ++i)
+      bt32[tid * (kBPT / 2) + i] = (e[2 * i] + off) | (e[2 * i + 1] + off) << 16;
     if (tid == 0) bt[kNB] = (uint16_t)nt;
   }
   __syncthreads();  // (4)
@@ -367,7 +383,7 @@ __global__ __launch_bounds__(kNT, (occupancy<V, M, kGroup>())) void tile_kernel(
     for (int r = 0; r < kCap; ++r) {
       if ((uint32_t)r < nrw) {
         int prev0;
-        if ((re[r] & 15u) == 0u) prev0 = -1;  // first round of the piece
+        if ((re[r] & ((1u << kCB) - 1u)) == 0u) prev0 = -1;  // first round of the piece
         else if (r > 0) prev0 = __builtin_amdgcn_readlane((int)pos[r - 1], 63);
         else prev0 = w > 0 ? lastpos[w - 1] : pcarry;
         const int prev = __builtin_amdgcn_update_dpp(prev0, (int)pos[r], 0x138, 0xf, 0xf, false);
@@ -385,7 +401,7 @@ __global__ __launch_bounds__(kNT, (occupancy<V, M, kGroup>())) void tile_kernel(
       for (int r = 0; r < kCap; ++r) {
         const uint64_t bad = __ballot(((fl >> r) & ~(fl >> (16 + r)) & 1u) != 0u);
         if ((uint32_t)r < nrw && bad && lane == 0)
-          __hip_atomic_fetch_add(GW(T.fail) + g0 + (re[r] >> 4),
+          __hip_atomic_fetch_add(GW(T.fail) + g0 + (re[r] >> kCB),
                                  (unsigned long long)__popcll(bad), __ATOMIC_RELAXED,
                                  __HIP_MEMORY_SCOPE_AGENT);
       }
@@ -399,7 +415,7 @@ __global__ __launch_bounds__(kNT, (occupancy<V, M, kGroup>())) void tile_kernel(
 #pragma unroll
         for (int r = 0; r < kCap; ++r) {
           if ((uint32_t)r < nrw && ((fl >> (16 + r)) & 1u)) {
-            const uint32_t q = re[r] >> 4;
+            const uint32_t q = re[r] >> kCB;
             const uint32_t s = pos[r];
             const bool first = g0 + q == 0u && !cont;
 #pragma unroll
@@ -463,9 +479,9 @@ __global__ __launch_bounds__(kNT, (occupancy<V, M, kGroup>())) void tile_kernel(
 template <typename V, int M>
 hipError_t go(const TileDesc* t, uint32_t n, bool wide, hipStream_t s) {
   if (wide)
-    hipLaunchKernelGGL((tile_kernel<V, M, 64>), dim3(n), dim3(kNT), 0, s, t, n);
+    hipLaunchKernelGGL((tile_kernel<V, M, 64>), dim3(n), dim3(nt_of(64)), 0, s, t, n);
   else
-    hipLaunchKernelGGL((tile_kernel<V, M, 32>), dim3(n), dim3(kNT), 0, s, t, n);
+    hipLaunchKernelGGL((tile_kernel<V, M, 32>), dim3(n), dim3(nt_of(32)), 0, s, t, n);
   return hipGetLastError();
 }
 
