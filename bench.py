@@ -82,6 +82,8 @@ def parse():
     ap.add_argument("--cfg5-steps", type=int, default=10)
     ap.add_argument("--cpu-seconds", type=float, default=10.0)
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--plan-flags", type=lambda x: int(x, 0), default=0,
+                    help="kernel-form overrides of include/psg.h (A/B measurements only)")
     ap.add_argument("--no-check", action="store_true",
                     help="skip the matched-count guard (ablation builds via PSG_LIB_PATH only)")
     ap.add_argument("--profile-steps", type=int, default=0,
@@ -102,6 +104,9 @@ def to_dev(a, dev):
     return torch.from_numpy(a.view(np.int64) if a.dtype == np.uint64 else a).to(dev)
 
 
+PLAN_FLAGS = 0  # --plan-flags
+
+
 def make_plan(insts, dev, local):
     """MergePlan over [(D, pushes)] resident on `dev`; returns (plan, keep, jobs)."""
     import torch
@@ -119,7 +124,7 @@ def make_plan(insts, dev, local):
                      "push_vals": [[t.data_ptr() for t in vs] for vs in pv],
                      "push_n": [int(k.size) for k, _ in pushes],
                      "out": [out.data_ptr()]})
-    plan = MergePlan(local, PSG_F32, 1, jobs)
+    plan = MergePlan(local, PSG_F32, 1, jobs, flags=PLAN_FLAGS)
     return plan, keep, jobs
 
 
@@ -155,7 +160,9 @@ def timed_steps(plan, K, W, stream, dist):
 
 
 def main():
+    global PLAN_FLAGS
     args = parse()
+    PLAN_FLAGS = args.plan_flags
     import torch
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
@@ -285,44 +292,103 @@ def main():
         dist.destroy_process_group()
 
 
+def timed_stages(stages, K, W, stream, dist):
+    """Like timed_steps for a step made of `stages` (callables enqueuing on
+    `stream`): W warm-up steps, then K timed steps between barrier +
+    synchronize pairs.  Returns (wall s, [mean ms per stage]) (HIP events on
+    `stream` between the stages)."""
+    import torch
+    for _ in range(W):
+        for f in stages:
+            f()
+    torch.cuda.synchronize()
+    if dist:
+        dist.barrier()
+    torch.cuda.synchronize()
+    ev = [[torch.cuda.Event(enable_timing=True) for _ in range(len(stages) + 1)] for _ in range(K)]
+    t0 = time.perf_counter()
+    for s in range(K):
+        ev[s][0].record(stream)
+        for i, f in enumerate(stages):
+            f()
+            ev[s][i + 1].record(stream)
+    torch.cuda.synchronize()
+    if dist:
+        dist.barrier()
+    torch.cuda.synchronize()
+    wall = time.perf_counter() - t0
+    ms = [float(np.mean([ev[s][i].elapsed_time(ev[s][i + 1]) for s in range(K)]))
+          for i in range(len(stages))]
+    return wall, ms
+
+
 def cfg5_block(args, rank, world, bounds, dist, dev, local, stream):
     """BASELINE.json configs[4]: one fixed global workload (256 pushes x
-    262,144 keys over a 1 B-key space), range-partitioned over the N ranks
-    with worker-sliced ingress (each rank merges its shard's pieces of all
-    256 pushes; no data-path collective), and the same whole workload on
-    rank 0's GPU alone in the same job."""
+    262,144 keys over a 1 B-key space) range-partitioned over the N ranks
+    by evenDivide(N), two ingress modes:
+      sliced    workers slice their pushes by the server ranges (the
+                reference's RNode::submit -> sliceKeyOrderedMsg), so each
+                rank receives only its shard's pieces of all 256 pushes: the
+                step is the merge, no data-path collective;
+      unsliced  rank r receives whole pushes (256/N of them); the step is
+                psg_exchange_run (device re-cut + pack + one grouped RCCL
+                send/recv per peer over xGMI) followed by the merge of the
+                pieces this rank received (same arrival order: sources hold
+                consecutive push blocks, so the sums are bit-identical to
+                the sliced leg's, checked);
+    plus the whole workload on rank 0's GPU alone in the same job
+    (speedup_vs_1gpu)."""
     import torch
-    from parameter_server_amd import synth
+    from parameter_server_amd import shard, synth
+    from parameter_server_amd._lib import PSG_F32
+    from parameter_server_amd.kv_vector import MergePlan
     t0 = time.time()
     _, pushes = synth.uniform_pushes(seed=5, union=False)
     kv_total = sum(int(k.size) for k, _ in pushes)
     pieces = synth.shard_pieces(pushes, bounds, rank)
     D = np.unique(np.concatenate([k for k, _ in pieces]))
     log(f"rank {rank}: cfg5 shard {D.size:,} keys generated in {time.time() - t0:.1f}s")
+    sh = stream.cuda_stream
+    K = args.cfg5_steps
+    # ---- sliced ingress (the reference's mode)
     plan, keep, jobs = make_plan([(D, pieces)], dev, local)
-    plan.run(stream.cuda_stream)
+    plan.run(sh)
     assert args.no_check or np.array_equal(plan.matched(),
                                             np.array([k.size for k, _ in pieces], np.uint64))
-    K = args.cfg5_steps
-    wall, part_ms, agg_ms = timed_steps(plan, K, 2, stream, dist)
+    wall, (part_ms, agg_ms) = timed_stages([lambda: plan.run_stage(0, sh),
+                                            lambda: plan.run_stage(1, sh)], K, 2, stream, dist)
     wall_max, kv_all = reduce_over_ranks(wall, plan.kv_pairs, dist, dev)
     assert int(kv_all) == kv_total
     nbytes = int(plan.bytes)
-    out = {
-        "workload": ("256 pushes x 262144 murmur-shuffled uniform keys (1e9-rank space), "
-                     f"f32; fixed global workload split by evenDivide({world})"),
-        "scaling": "strong",
-        "n_gpus": world,
+    sliced = {
         "value": kv_total * K / wall_max,
-        "unit": "kv-pairs/s",
         "ms_per_step": wall_max / K * 1e3,
         "rank0": {"slots": int(D.size), "kernel_ms": agg_ms, "partition_ms": part_ms,
                   "bytes_per_launch": nbytes,
                   "frac": nbytes / (agg_ms * 1e-3) / 1e9 / HBM_PEAK_GBPS,
                   "step_frac": nbytes / (wall / K) / 1e9 / HBM_PEAK_GBPS},
     }
+    out_sliced = keep[0][3].clone()
     del plan, keep
     torch.cuda.empty_cache()
+    out = {
+        "workload": ("256 pushes x 262144 murmur-shuffled uniform keys (1e9-rank space), "
+                     f"f32; fixed global workload split by evenDivide({world})"),
+        "scaling": "strong",
+        "n_gpus": world,
+        "value": sliced["value"],
+        "unit": "kv-pairs/s",
+        "ms_per_step": sliced["ms_per_step"],
+        "rank0": sliced["rank0"],
+        "modes": {"sliced": sliced},
+    }
+    # ---- unsliced ingress: whole pushes per rank, RCCL exchange in the step
+    try:
+        out["modes"]["unsliced"] = cfg5_unsliced(args, rank, world, bounds, dist, dev, local,
+                                                 stream, pushes, D, out_sliced, kv_total)
+    finally:
+        del out_sliced
+        torch.cuda.empty_cache()
     if world > 1:
         # the same whole workload on ONE GPU (rank 0), the others waiting
         t1 = None
@@ -341,6 +407,71 @@ def cfg5_block(args, rank, world, bounds, dist, dev, local, stream):
         out["one_gpu_ms_per_step"] = out["ms_per_step"]
         out["speedup_vs_1gpu"] = 1.0
     return out
+
+
+def cfg5_unsliced(args, rank, world, bounds, dist, dev, local, stream, pushes, D, out_sliced,
+                  kv_total):
+    """The cfg5 step with unsliced ingress (mode B): rank r holds pushes
+    [r*P/N, (r+1)*P/N) whole; psg_exchange_run re-homes their pieces over
+    RCCL, then the plan merges the pieces this rank received."""
+    import torch
+    from parameter_server_amd import shard
+    from parameter_server_amd._lib import PSG_F32
+    from parameter_server_amd.kv_vector import MergePlan
+    P = len(pushes)
+    a, b = rank * P // world, (rank + 1) * P // world
+    sh = stream.cuda_stream
+    dp = [(to_dev(k, dev), [to_dev(v, dev) for v in vs]) for k, vs in pushes[a:b]]
+    comm = shard.make_comm(local, rank, world, dist)
+    x = shard.RcclExchange(comm, dp, world, PSG_F32)
+    try:
+        pcs = x.pieces()  # (offset, count) per (source, push), arrival order
+        dD = to_dev(D, dev)
+        res = torch.empty(max(1, D.size), dtype=torch.float32, device=dev)
+        job = {"keys": dD.data_ptr(), "nslots": int(D.size),
+               "push_keys": [x.recv_keys_ptr + 8 * o for o, _ in pcs],
+               "push_vals": [[x.recv_vals_ptr[0] + 4 * o] for o, _ in pcs],
+               "push_n": [c for _, c in pcs], "out": [res.data_ptr()]}
+        plan = MergePlan(local, PSG_F32, 1, [job])
+        x.run(sh)
+        plan.run(sh)
+        if not args.no_check:
+            assert np.array_equal(plan.matched(), np.array([c for _, c in pcs], np.uint64))
+            assert x.status() == 0
+            # same pushes, same arrival order as the sliced leg: same bits
+            assert torch.equal(res.view(torch.int32), out_sliced.view(torch.int32)), \
+                "unsliced cfg5 merge differs from the sliced one"
+        K = args.cfg5_steps
+        wall, (x_ms, part_ms, agg_ms) = timed_stages(
+            [lambda: x.run(sh), lambda: plan.run_stage(0, sh), lambda: plan.run_stage(1, sh)],
+            K, 2, stream, dist)
+        wall_max, kv_all = reduce_over_ranks(wall, plan.kv_pairs, dist, dev)
+        assert int(kv_all) == kv_total
+        assert args.no_check or x.status() == 0
+        _, _, send_cnt = x.send_layout()
+        per_dest = send_cnt.sum(axis=1) * 12  # keys + f32 values
+        peers = [s for s in range(world) if s != rank]
+        to_peers = int(sum(per_dest[s] for s in peers))
+        peer_max = int(max((per_dest[s] for s in peers), default=0))
+        xs = x_ms * 1e-3
+        res_out = {
+            "value": kv_total * K / wall_max,
+            "ms_per_step": wall_max / K * 1e3,
+            "rank0": {"exchange_ms": x_ms, "partition_ms": part_ms, "kernel_ms": agg_ms,
+                      "pushes_held": b - a, "bytes_sent_to_peers": to_peers,
+                      "bytes_kept_local": int(per_dest[rank]),
+                      "max_bytes_to_one_peer": peer_max,
+                      "GBps_to_peers": to_peers / xs / 1e9 if peers else None,
+                      "GBps_per_peer_max": peer_max / xs / 1e9 if peers else None},
+            "step": "psg_exchange_run (device re-cut + pack + grouped RCCL send/recv) + "
+                    "partition + aggregate of the received pieces",
+        }
+        del plan, dD, res
+        return res_out
+    finally:
+        x.close()
+        shard.destroy_comm(comm)
+        del dp
 
 
 def reduce_over_ranks(wall, kv_rank, dist, dev):

@@ -69,6 +69,19 @@ typedef enum psg_dtype { PSG_F32 = 0, PSG_F64 = 1 } psg_dtype;
  * without a wait per push.  Without it every push returns with the caller's
  * buffers free. */
 #define PSG_HOLD_BUFFERS 0x100u
+/* Kernel-form overrides, for tests and A/B measurements (flags of
+ * psg_plan_create, psg_create and psg_set_match_flags).  By default the
+ * runtime picks each form from the shape of the pushes; the results are
+ * bit-identical whichever form runs.  No environment variable changes the
+ * path. */
+#define PSG_FORM_PACKED 0x1000u   /* rounds that pack several pushes (short pieces) */
+#define PSG_FORM_UNIFORM 0x2000u  /* rounds of one push each (long pieces) */
+#define PSG_PART_SEARCH 0x4000u   /* partition: one search per (push, tile boundary) */
+#define PSG_PART_STREAM 0x8000u   /* partition: every push key read once */
+#define PSG_GROUP32 0x10000u      /* uniform rounds: groups of 32 pushes, 1024-slot tiles */
+#define PSG_GROUP64 0x20000u      /* uniform rounds: groups of 64 pushes, 2048-slot tiles */
+#define PSG_NO_DENSE 0x40000u     /* never the dense (contiguous-slice) kernel */
+#define PSG_NO_ZERO_COPY 0x80000u /* context: DMA copies instead of GPU reads of pinned memory */
 
 int psg_abi_version(void);
 const char* psg_status_string(int status);
@@ -85,6 +98,10 @@ typedef struct psg_ctx psg_ctx;
 int psg_create(int device, int dtype, unsigned flags, psg_ctx** out);
 int psg_destroy(psg_ctx* ctx);
 int psg_set_match_flags(psg_ctx* ctx, unsigned flags);
+/* Pushes of one time merged per launch (default and maximum
+ * psg_plan_max_push()); an aggregate of more pushes continues across
+ * launches with the same bits.  Lower values force launch seams (tests). */
+int psg_set_flush_pushes(psg_ctx* ctx, int n);
 
 /* Key-only push: key_[chl] = key_[chl].setUnion(keys); val_[chl].clear()
  * (kv_vector.h:177-182).  keys must be strictly increasing. */
@@ -242,6 +259,23 @@ int psg_exchange_run(psg_exchange* x, void* stream);
 int psg_exchange_recv(psg_exchange* x, const uint64_t** keys, void** vals,
                       uint64_t* nrecv, uint64_t* recv_cnt, uint64_t* nsent);
 int psg_exchange_destroy(psg_exchange* x);
+/* The layout is fixed at create (the pushes' device buffers are read again
+ * by every run, like a psg_plan's).  Each run also redoes the cut on the
+ * device and counts the positions that differ from the layout (pushes whose
+ * keys changed since create); psg_exchange_status synchronises the last
+ * run's stream and returns PSG_ERR_SIZE (*changed = that count) if any run
+ * saw one.  The run's pieces are then those of the create-time cut. */
+int psg_exchange_status(psg_exchange* x, uint64_t* changed);
+/* The same slice-and-pack for nshards virtual shards on one device with no
+ * communicator ("8 shards on 1 device"): a run re-cuts and packs
+ * only; psg_exchange_send_layout gives the packed buffers (device) and
+ * send_cnt[s * npush + p] (host, may be NULL): shard s's piece of push p
+ * starts after all earlier (s, p) pieces.  Works on either kind. */
+int psg_exchange_create_local(int device, int nshards, int dtype, int m, int npush,
+                              const uint64_t* const* push_keys, const uint64_t* push_n,
+                              const void* const* push_vals, psg_exchange** out);
+int psg_exchange_send_layout(psg_exchange* x, const uint64_t** keys, void** vals,
+                             uint64_t* send_cnt);
 
 /* Server shard boundaries: Range<uint64>::all().evenDivide(n, i)
  * (range.h:75-98, linear_method.cc:137-145); bounds[n+1]. */

@@ -41,6 +41,15 @@ PSG_F64 = 1
 PSG_SERIAL_MATCH = 0
 PSG_PARALLEL_MATCH = 1
 PSG_HOLD_BUFFERS = 0x100
+# kernel-form overrides (include/psg.h): tests and A/B measurements only
+PSG_FORM_PACKED = 0x1000
+PSG_FORM_UNIFORM = 0x2000
+PSG_PART_SEARCH = 0x4000
+PSG_PART_STREAM = 0x8000
+PSG_GROUP32 = 0x10000
+PSG_GROUP64 = 0x20000
+PSG_NO_DENSE = 0x40000
+PSG_NO_ZERO_COPY = 0x80000
 MAX_VALUE_ARRAYS = 4
 
 # Every symbol include/psg.h declares, with its ctypes signature.
@@ -72,6 +81,7 @@ SIGNATURES = {
     "psg_device_count": (C.c_int, [C.POINTER(C.c_int)]),
     "psg_create": (C.c_int, [C.c_int, C.c_int, C.c_uint, C.POINTER(_p)]),
     "psg_destroy": (C.c_int, [_p]),
+    "psg_set_flush_pushes": (C.c_int, [_p, C.c_int]),
     "psg_set_match_flags": (C.c_int, [_p, C.c_uint]),
     "psg_key_union": (C.c_int, [_p, C.c_int, _p, _sz]),
     "psg_key_size": (C.c_int, [_p, C.c_int, _psz]),
@@ -123,6 +133,10 @@ SIGNATURES = {
     "psg_exchange_run": (C.c_int, [_p, _p]),
     "psg_exchange_recv": (C.c_int, [_p, C.POINTER(_p), _p, _pu64, _p, _pu64]),
     "psg_exchange_destroy": (C.c_int, [_p]),
+    "psg_exchange_status": (C.c_int, [_p, _pu64]),
+    "psg_exchange_create_local": (C.c_int, [C.c_int, C.c_int, C.c_int, C.c_int, C.c_int, _p,
+                                            _p, _p, C.POINTER(_p)]),
+    "psg_exchange_send_layout": (C.c_int, [_p, C.POINTER(_p), _p, _p]),
     "psg_darling_init": (C.c_int, [_p, C.c_int, C.c_double]),
     "psg_darling_reset_active": (C.c_int, [_p, C.c_int]),
     "psg_darling_update": (C.c_int, [_p, C.c_int, C.c_int, _p, C.POINTER(C.c_double)]),

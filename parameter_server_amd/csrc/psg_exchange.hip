@@ -9,14 +9,22 @@
 // Set-up (psg_exchange_create, synchronous): one wave per (push, boundary)
 // finds the cut positions (a sorted push's piece for shard s is the
 // contiguous run [lower_bound(b_s), lower_bound(b_s+1))); the piece counts
-// go to their shards with one grouped ncclSend/ncclRecv round; the send and
-// receive buffers are sized from them.  A step (psg_exchange_run, on a
-// stream, no host wait): one gather kernel packs every piece into
-// destination-major send buffers, then per peer one ncclSend/ncclRecv of
-// the keys and one per value array in a single group.  After a step,
-// shard `rank` holds, for each source rank src and push p, the piece at
-// recv offset off[src][p] with cnt[src][p] keys (the layout a psg_plan
-// job points at directly).
+// go to their shards with one grouped ncclSend/ncclRecv round (plus an error
+// word, so a rank that cannot build its layout still takes part and every
+// rank fails together); the send and receive buffers are sized from them.
+// A step (psg_exchange_run, on a stream, no host wait): the cut is redone
+// on the device and compared with the layout (a push whose keys changed
+// since set-up is counted, psg_exchange_status), one gather kernel packs
+// every piece into destination-major send buffers (16-B lanes where the
+// piece allows), then per peer one ncclSend/ncclRecv of the keys and one per
+// value array in a single group.  After a step, shard `rank` holds, for
+// each source rank src and push p, the piece at recv offset off[src][p]
+// with cnt[src][p] keys (the layout a psg_plan job points at directly).
+//
+// psg_exchange_create_local builds the same layout for S virtual shards on
+// one device with no communicator: a step re-cuts and packs, and
+// psg_exchange_send_layout hands out the packed buffers (tests of the
+// multi-shard layout on one GPU, SURVEY 4 "8 shards on 1 device").
 #include <hip/hip_runtime.h>
 #include <rccl/rccl.h>
 
@@ -39,11 +47,15 @@ using psg::fail;
 
 namespace {
 
-// pos[p * (S+1) + s] = lower_bound(push p, bounds[s]); one wave each
+// pos[p * (S+1) + s] = lower_bound(push p, bounds[s]); one wave each.
+// Verify mode (expect != null): count the positions that differ from the
+// layout built at set-up instead of writing them.
 __global__ __launch_bounds__(256) void cut_kernel(const uint64_t* const* __restrict__ keys,
                                                   const uint64_t* __restrict__ n,
                                                   const uint64_t* __restrict__ bounds, int S1,
-                                                  int P, uint64_t* __restrict__ pos) {
+                                                  int P, uint64_t* __restrict__ pos,
+                                                  const uint64_t* __restrict__ expect,
+                                                  unsigned long long* __restrict__ bad) {
   const int w = (int)((blockIdx.x * 256u + threadIdx.x) >> 6);
   const int lane = threadIdx.x & 63;
   if (w >= P * S1) return;
@@ -51,7 +63,13 @@ __global__ __launch_bounds__(256) void cut_kernel(const uint64_t* const* __restr
   // every separator, the last (2^64-1, the end of Range::all()) included:
   // the reference's cut (message.h:96-99) leaves a key 2^64-1 in no shard
   const uint64_t r = psg::dev::wave_search(keys[p], n[p], bounds[s], false, lane);
-  if (lane == 0) pos[w] = r;
+  if (lane == 0) {
+    if (expect) {
+      if (r != expect[w]) atomicAdd(bad, 1ull);
+    } else {
+      pos[w] = r;
+    }
+  }
 }
 
 // one piece of the send layout
@@ -61,6 +79,31 @@ struct Piece {
   uint64_t len;
   uint32_t p, pad;
 };
+
+typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
+
+// bytes [0, len) from s to d, 256 threads: 16-B lanes when both ends share
+// their offset mod 16 (the head and tail bytes around them by 4-B or 1-B
+// lanes), else element lanes of `eb` bytes
+__device__ __forceinline__ void copy_run(char* __restrict__ d, const char* __restrict__ s,
+                                         uint64_t len, int eb) {
+  const uint64_t mis = ((uintptr_t)d ^ (uintptr_t)s) & 15u;
+  if (mis == 0 && len >= 64) {
+    const uint64_t head = (16u - ((uintptr_t)d & 15u)) & 15u;
+    for (uint64_t i = threadIdx.x; i < head; i += 256) d[i] = s[i];
+    const uint64_t n16 = (len - head) / 16;
+    const u32x4* s16 = (const u32x4*)(s + head);
+    u32x4* d16 = (u32x4*)(d + head);
+    for (uint64_t i = threadIdx.x; i < n16; i += 256) d16[i] = __builtin_nontemporal_load(s16 + i);
+    for (uint64_t i = head + 16 * n16 + threadIdx.x; i < len; i += 256) d[i] = s[i];
+  } else if (eb == 8) {
+    for (uint64_t i = threadIdx.x; i < len / 8; i += 256)
+      ((uint64_t*)d)[i] = ((const uint64_t*)s)[i];
+  } else {
+    for (uint64_t i = threadIdx.x; i < len / 4; i += 256)
+      ((uint32_t*)d)[i] = ((const uint32_t*)s)[i];
+  }
+}
 
 // every piece into the destination-major send buffers: keys (8 B) and m
 // value arrays of `vb` bytes per element; a workgroup per 2048-element chunk
@@ -77,18 +120,10 @@ __global__ __launch_bounds__(256) void pack_kernel(const Piece* __restrict__ pie
     const Piece pc = pieces[e >> 24];
     const uint64_t c0 = (e & 0xffffffull) * kChunk;
     const uint64_t len = pc.len - c0 < kChunk ? pc.len - c0 : kChunk;
-    const uint64_t* ks = keys[pc.p] + pc.src + c0;
-    uint64_t* kd = skeys + pc.dst + c0;
-    for (uint64_t i = threadIdx.x; i < len; i += 256) kd[i] = ks[i];
-    for (int a = 0; a < m; ++a) {
-      const char* vs = (const char*)vals[(size_t)pc.p * m + a] + (pc.src + c0) * vb;
-      char* vd = (char*)svals[a] + (pc.dst + c0) * vb;
-      if (vb == 4) {
-        for (uint64_t i = threadIdx.x; i < len; i += 256) ((uint32_t*)vd)[i] = ((const uint32_t*)vs)[i];
-      } else {
-        for (uint64_t i = threadIdx.x; i < len; i += 256) ((uint64_t*)vd)[i] = ((const uint64_t*)vs)[i];
-      }
-    }
+    copy_run((char*)(skeys + pc.dst + c0), (const char*)(keys[pc.p] + pc.src + c0), 8 * len, 8);
+    for (int a = 0; a < m; ++a)
+      copy_run((char*)svals[a] + (pc.dst + c0) * vb,
+               (const char*)vals[(size_t)pc.p * m + a] + (pc.src + c0) * vb, len * vb, vb);
   }
 }
 
@@ -100,7 +135,8 @@ struct psg_comm {
 };
 
 struct psg_exchange {
-  psg_comm* comm = nullptr;
+  psg_comm* comm = nullptr;  // null: a local exchange (S virtual shards, no transport)
+  int device = 0;
   int dtype = 0, m = 1, P = 0, S = 1;
   std::vector<uint64_t> send_cnt;   // [s][p]
   std::vector<uint64_t> recv_cnt;   // [src][p]
@@ -115,7 +151,12 @@ struct psg_exchange {
   void* const* d_svals = nullptr;
   Piece* d_pieces = nullptr;
   uint64_t* d_chunks = nullptr;
+  const uint64_t* d_n = nullptr;       // push lengths
+  const uint64_t* d_bounds = nullptr;  // the S + 1 shard boundaries
+  const uint64_t* d_pos = nullptr;     // the layout's cut positions [p][S + 1]
+  unsigned long long* d_bad = nullptr; // positions that differed in a run's re-cut
   uint64_t nchunks = 0, nsend = 0, nrecv = 0;
+  hipStream_t last = nullptr;          // stream of the last run
 };
 
 namespace {
@@ -158,24 +199,33 @@ int psg_comm_destroy(psg_comm* c) {
   return PSG_OK;
 }
 
-int psg_exchange_create(psg_comm* comm, int dtype, int m, int npush,
-                        const uint64_t* const* push_keys, const uint64_t* push_n,
-                        const void* const* push_vals, psg_exchange** out) {
-  if (!comm || !out || npush < 0 || (npush && (!push_keys || !push_n || !push_vals)))
-    return fail(PSG_ERR_ARG, "null argument");
-  if (dtype != PSG_F32 && dtype != PSG_F64) return fail(PSG_ERR_ARG, "dtype %d", dtype);
-  if (m < 1 || m > PSG_MAX_VALUE_ARRAYS) return fail(PSG_ERR_ARG, "m=%d", m);
-  HIP_TRY(hipSetDevice(comm->device));
-  const int S = comm->nranks, P = npush, S1 = S + 1;
+namespace {
+
+// psg_exchange_create / psg_exchange_create_local.  comm == null: S local
+// shards, no count exchange, no receive buffers.
+int exchange_create(psg_comm* comm, int device, int S, int dtype, int m, int npush,
+                    const uint64_t* const* push_keys, const uint64_t* push_n,
+                    const void* const* push_vals, psg_exchange** out) {
+  int err = PSG_OK;  // a local argument error; collective callers still exchange counts
+  if (!out || npush < 0 || (npush && (!push_keys || !push_n || !push_vals)))
+    err = fail(PSG_ERR_ARG, "null argument");
+  else if (dtype != PSG_F32 && dtype != PSG_F64)
+    err = fail(PSG_ERR_ARG, "dtype %d", dtype);
+  else if (m < 1 || m > PSG_MAX_VALUE_ARRAYS)
+    err = fail(PSG_ERR_ARG, "m=%d", m);
+  if (err && !comm) return err;
+  if (err) npush = 0;  // take part in the count round with an error word only
+  HIP_TRY(hipSetDevice(device));
+  const int P = npush, S1 = S + 1;
   const int vb = dtype == PSG_F32 ? 4 : 8;
   std::vector<uint64_t> bounds(S1);
   if (int rc = psg_shard_bounds((size_t)S, bounds.data())) return rc;
   hipStream_t st;
   HIP_TRY(hipStreamCreateWithFlags(&st, hipStreamNonBlocking));
-  // ---- set-up block: bounds, push tables, cut positions, counts
+  // ---- set-up block: bounds, push tables, cut positions, counts (+1 error word per peer)
   const size_t o_b = 0, o_k = al(8 * S1), o_n = o_k + al(8 * P), o_pos = o_n + al(8 * P),
-               o_sc = o_pos + al(8 * (size_t)P * S1), o_rc = o_sc + al(8 * (size_t)P * S),
-               tot = o_rc + al(8 * (size_t)P * S);
+               o_sc = o_pos + al(8 * (size_t)P * S1), o_rc = o_sc + al(8 * (size_t)(P + 1) * S),
+               tot = o_rc + al(8 * (size_t)(P + 1) * S);
   char* setup = nullptr;
   if (hipMalloc((void**)&setup, tot) != hipSuccess) {
     (void)hipStreamDestroy(st);
@@ -184,6 +234,7 @@ int psg_exchange_create(psg_comm* comm, int dtype, int m, int npush,
   std::vector<uint64_t> pos((size_t)P * S1);
   psg_exchange* x = new psg_exchange();
   x->comm = comm;
+  x->device = device;
   x->dtype = dtype;
   x->m = m;
   x->P = P;
@@ -208,12 +259,14 @@ int psg_exchange_create(psg_comm* comm, int dtype, int m, int npush,
     const uint64_t waves = (uint64_t)P * S1;
     hipLaunchKernelGGL(cut_kernel, dim3((uint32_t)((waves + 3) / 4)), dim3(256), 0, st,
                        (const uint64_t* const*)(setup + o_k), (const uint64_t*)(setup + o_n),
-                       (const uint64_t*)(setup + o_b), S1, P, (uint64_t*)(setup + o_pos));
+                       (const uint64_t*)(setup + o_b), S1, P, (uint64_t*)(setup + o_pos),
+                       nullptr, nullptr);
     X_TRY(hipGetLastError());
     X_TRY(hipMemcpyAsync(pos.data(), setup + o_pos, 8 * pos.size(), hipMemcpyDeviceToHost, st));
     X_TRY(hipStreamSynchronize(st));
   }
-  // send counts [s][p]; pieces in destination-major, push order
+  // send counts [s][p] (+ this rank's error word per peer); pieces in
+  // destination-major, push order
   x->send_cnt.assign((size_t)S * P, 0);
   x->send_tot.assign(S, 0);
   x->send_off.assign(S, 0);
@@ -226,8 +279,11 @@ int psg_exchange_create(psg_comm* comm, int dtype, int m, int npush,
       const uint64_t a = pos[(size_t)p * S1 + s], b = pos[(size_t)p * S1 + s + 1];
       const uint64_t c = b > a ? b - a : 0;
       x->send_cnt[(size_t)s * P + p] = c;
-      if (c) {
-        if (pieces.size() >= (1u << 24)) return done(fail(PSG_ERR_ARG, "too many pieces"));
+      if (c && !err) {
+        if (pieces.size() >= (1u << 24)) {
+          err = fail(PSG_ERR_ARG, "too many pieces (> 2^24)");
+          break;
+        }
         for (uint64_t q = 0; q * 2048 < c; ++q) chunks.push_back((uint64_t)pieces.size() << 24 | q);
         pieces.push_back(Piece{a, off, c, (uint32_t)p, 0});
       }
@@ -236,30 +292,41 @@ int psg_exchange_create(psg_comm* comm, int dtype, int m, int npush,
     x->send_tot[s] = off - x->send_off[s];
   }
   x->nsend = off;
-  // counts to their shards: P words to and from every peer
-  X_TRY(hipMemcpyAsync(setup + o_sc, x->send_cnt.data(), 8 * x->send_cnt.size(),
-                       hipMemcpyHostToDevice, st));
-  {
+  if (!comm) {
+    if (err) return done(err);
+  } else {
+    // counts to their shards: P words + the error word to and from every peer
+    std::vector<uint64_t> sc((size_t)(P + 1) * S);
+    for (int s = 0; s < S; ++s) {
+      for (int p = 0; p < P; ++p) sc[(size_t)s * (P + 1) + p] = x->send_cnt[(size_t)s * P + p];
+      sc[(size_t)s * (P + 1) + P] = err ? 1u : 0u;
+    }
+    X_TRY(hipMemcpyAsync(setup + o_sc, sc.data(), 8 * sc.size(), hipMemcpyHostToDevice, st));
     ncclResult_t r = ncclGroupStart();
-    for (int s = 0; r == ncclSuccess && s < S && P; ++s) {
-      r = ncclSend(setup + o_sc + 8 * (size_t)s * P, P, ncclUint64, s, comm->nccl, st);
+    for (int s = 0; r == ncclSuccess && s < S; ++s) {
+      r = ncclSend(setup + o_sc + 8 * (size_t)s * (P + 1), P + 1, ncclUint64, s, comm->nccl, st);
       if (r == ncclSuccess)
-        r = ncclRecv(setup + o_rc + 8 * (size_t)s * P, P, ncclUint64, s, comm->nccl, st);
+        r = ncclRecv(setup + o_rc + 8 * (size_t)s * (P + 1), P + 1, ncclUint64, s, comm->nccl, st);
     }
     const ncclResult_t r2 = ncclGroupEnd();
     if (r != ncclSuccess || r2 != ncclSuccess)
       return done(fail(PSG_ERR_DEVICE, "count exchange: %s",
                        ncclGetErrorString(r != ncclSuccess ? r : r2)));
+    std::vector<uint64_t> rc((size_t)(P + 1) * S);
+    X_TRY(hipMemcpyAsync(rc.data(), setup + o_rc, 8 * rc.size(), hipMemcpyDeviceToHost, st));
+    X_TRY(hipStreamSynchronize(st));
+    if (err) return done(err);
+    for (int s = 0; s < S; ++s)
+      if (rc[(size_t)s * (P + 1) + P])
+        return done(fail(PSG_ERR_ARG, "exchange set-up failed on rank %d", s));
+    x->recv_cnt.assign((size_t)S * P, 0);
+    for (int s = 0; s < S; ++s)
+      for (int p = 0; p < P; ++p) x->recv_cnt[(size_t)s * P + p] = rc[(size_t)s * (P + 1) + p];
   }
-  x->recv_cnt.assign((size_t)S * P, 0);
-  if (P)
-    X_TRY(hipMemcpyAsync(x->recv_cnt.data(), setup + o_rc, 8 * x->recv_cnt.size(),
-                         hipMemcpyDeviceToHost, st));
-  X_TRY(hipStreamSynchronize(st));
   x->recv_tot.assign(S, 0);
   x->recv_off.assign(S, 0);
   uint64_t roff = 0;
-  for (int s = 0; s < S; ++s) {
+  for (int s = 0; comm && s < S; ++s) {
     x->recv_off[s] = roff;
     for (int p = 0; p < P; ++p) roff += x->recv_cnt[(size_t)s * P + p];
     x->recv_tot[s] = roff - x->recv_off[s];
@@ -279,7 +346,11 @@ int psg_exchange_create(psg_comm* comm, int dtype, int m, int npush,
   const size_t b_svp = b; b += al(8 * (size_t)m);
   const size_t b_pc = b; b += al(sizeof(Piece) * pieces.size());
   const size_t b_ch = b; b += al(8 * chunks.size());
-  X_TRY(hipMalloc(&x->dev, b ? b : 256));
+  const size_t b_n = b; b += al(8 * (size_t)P);
+  const size_t b_bd = b; b += al(8 * (size_t)S1);
+  const size_t b_pos = b; b += al(8 * (size_t)P * S1);
+  const size_t b_bad = b; b += al(8);
+  X_TRY(hipMalloc(&x->dev, b));
   char* d = (char*)x->dev;
   x->skeys = (uint64_t*)(d + b_sk);
   x->rkeys = (uint64_t*)(d + b_rk);
@@ -294,10 +365,18 @@ int psg_exchange_create(psg_comm* comm, int dtype, int m, int npush,
   x->d_svals = (void* const*)(d + b_svp);
   x->d_pieces = (Piece*)(d + b_pc);
   x->d_chunks = (uint64_t*)(d + b_ch);
+  x->d_n = (const uint64_t*)(d + b_n);
+  x->d_bounds = (const uint64_t*)(d + b_bd);
+  x->d_pos = (const uint64_t*)(d + b_pos);
+  x->d_bad = (unsigned long long*)(d + b_bad);
   if (P) {
     X_TRY(hipMemcpyAsync(d + b_keys, push_keys, 8 * (size_t)P, hipMemcpyHostToDevice, st));
     X_TRY(hipMemcpyAsync(d + b_vals, push_vals, 8 * (size_t)P * m, hipMemcpyHostToDevice, st));
+    X_TRY(hipMemcpyAsync(d + b_n, push_n, 8 * (size_t)P, hipMemcpyHostToDevice, st));
+    X_TRY(hipMemcpyAsync(d + b_pos, pos.data(), 8 * pos.size(), hipMemcpyHostToDevice, st));
   }
+  X_TRY(hipMemcpyAsync(d + b_bd, bounds.data(), 8 * (size_t)S1, hipMemcpyHostToDevice, st));
+  X_TRY(hipMemsetAsync(d + b_bad, 0, 8, st));
   X_TRY(hipMemcpyAsync(d + b_svp, svp.data(), 8 * (size_t)m, hipMemcpyHostToDevice, st));
   if (!pieces.empty())
     X_TRY(hipMemcpyAsync(d + b_pc, pieces.data(), sizeof(Piece) * pieces.size(),
@@ -309,11 +388,38 @@ int psg_exchange_create(psg_comm* comm, int dtype, int m, int npush,
   return done(PSG_OK);
 }
 
+}  // namespace
+
+int psg_exchange_create(psg_comm* comm, int dtype, int m, int npush,
+                        const uint64_t* const* push_keys, const uint64_t* push_n,
+                        const void* const* push_vals, psg_exchange** out) {
+  if (!comm) return fail(PSG_ERR_ARG, "null communicator");
+  return exchange_create(comm, comm->device, comm->nranks, dtype, m, npush, push_keys, push_n,
+                         push_vals, out);
+}
+
+int psg_exchange_create_local(int device, int nshards, int dtype, int m, int npush,
+                              const uint64_t* const* push_keys, const uint64_t* push_n,
+                              const void* const* push_vals, psg_exchange** out) {
+  if (nshards < 1) return fail(PSG_ERR_ARG, "nshards=%d", nshards);
+  return exchange_create(nullptr, device, nshards, dtype, m, npush, push_keys, push_n, push_vals,
+                         out);
+}
+
 int psg_exchange_run(psg_exchange* x, void* stream) {
   if (!x) return fail(PSG_ERR_ARG, "null exchange");
-  HIP_TRY(hipSetDevice(x->comm->device));
+  HIP_TRY(hipSetDevice(x->device));
   hipStream_t st = (hipStream_t)stream;
+  x->last = st;
   const int vb = x->dtype == PSG_F32 ? 4 : 8;
+  if (x->P) {
+    // the cut of this step's pushes, checked against the layout (no host wait)
+    const int S1 = x->S + 1;
+    const uint64_t waves = (uint64_t)x->P * S1;
+    hipLaunchKernelGGL(cut_kernel, dim3((uint32_t)((waves + 3) / 4)), dim3(256), 0, st, x->d_keys,
+                       x->d_n, x->d_bounds, S1, x->P, nullptr, x->d_pos, x->d_bad);
+    HIP_TRY(hipGetLastError());
+  }
   if (x->nchunks) {
     const uint64_t blocks = x->nchunks < 4096 ? x->nchunks : 4096;
     hipLaunchKernelGGL(pack_kernel, dim3((uint32_t)blocks), dim3(256), 0, st, x->d_pieces,
@@ -321,6 +427,7 @@ int psg_exchange_run(psg_exchange* x, void* stream) {
                        x->d_svals);
     HIP_TRY(hipGetLastError());
   }
+  if (!x->comm) return PSG_OK;  // local shards: the packed buffers are the result
   ncclResult_t r = ncclGroupStart();
   for (int s = 0; r == ncclSuccess && s < x->S; ++s) {
     if (x->send_tot[s]) {
@@ -343,6 +450,28 @@ int psg_exchange_run(psg_exchange* x, void* stream) {
   return PSG_OK;
 }
 
+int psg_exchange_status(psg_exchange* x, uint64_t* changed) {
+  if (!x) return fail(PSG_ERR_ARG, "null exchange");
+  HIP_TRY(hipSetDevice(x->device));
+  if (x->last) HIP_TRY(hipStreamSynchronize(x->last));
+  unsigned long long bad = 0;
+  HIP_TRY(hipMemcpy(&bad, x->d_bad, 8, hipMemcpyDeviceToHost));
+  if (changed) *changed = bad;
+  if (bad)
+    return fail(PSG_ERR_SIZE, "exchange: %llu cut positions differ from the set-up layout", bad);
+  return PSG_OK;
+}
+
+int psg_exchange_send_layout(psg_exchange* x, const uint64_t** keys, void** vals,
+                             uint64_t* send_cnt) {
+  if (!x) return fail(PSG_ERR_ARG, "null exchange");
+  if (keys) *keys = x->skeys;
+  for (int a = 0; vals && a < x->m; ++a) vals[a] = x->svals[a];
+  if (send_cnt && !x->send_cnt.empty())
+    memcpy(send_cnt, x->send_cnt.data(), 8 * x->send_cnt.size());
+  return PSG_OK;
+}
+
 int psg_exchange_recv(psg_exchange* x, const uint64_t** keys, void** vals, uint64_t* nrecv,
                       uint64_t* recv_cnt, uint64_t* sent) {
   if (!x) return fail(PSG_ERR_ARG, "null exchange");
@@ -357,7 +486,7 @@ int psg_exchange_recv(psg_exchange* x, const uint64_t** keys, void** vals, uint6
 int psg_exchange_destroy(psg_exchange* x) {
   if (!x) return PSG_OK;
   if (x->dev) {
-    (void)hipSetDevice(x->comm->device);
+    (void)hipSetDevice(x->device);
     (void)hipDeviceSynchronize();
     (void)hipFree(x->dev);
   }

@@ -79,24 +79,13 @@ constexpr double kStreamBelow = 24.0;
 // pieces into one 64-lane round; above it rounds are
 // push-uniform, which is faster while most rounds are full anyway.
 constexpr double kPackBelow = 16.0;
+// psg_push tests pushes of at least this many keys for a contiguous slice
+constexpr size_t kDenseMinKeys = 1024;
 
-// A/B knobs (measurements and tests): read from the environment when a
-// context or a plan is created (JobTable::read_knobs), never per flush or
-// launch.
-// PSG_PART_MODE=search|stream forces the partition mode.
-int forced_part_mode() {
-  const char* e = getenv("PSG_PART_MODE");
-  if (!e) return -1;
-  if (!strcmp(e, "search")) return psg::kSearch;
-  if (!strcmp(e, "stream")) return psg::kStream;
-  return -1;
-}
-
-// PSG_DENSE=0 turns the dense check of psg_plan_create off.
-bool dense_enabled() {
-  const char* e = getenv("PSG_DENSE");
-  return !(e && e[0] == '0');
-}
+// Kernel-form overrides come from explicit flags (psg.h PSG_FORM_*,
+// PSG_PART_*, PSG_GROUP*, PSG_NO_DENSE, PSG_NO_ZERO_COPY), never from the
+// environment: tests and A/B measurements pass them to psg_plan_create /
+// psg_create; results are bit-identical either way.
 
 // Marks the jobs whose every non-empty push is a contiguous slice of the
 // job's server keys (psg_tile_dense.hip), with each push's start position.
@@ -157,33 +146,15 @@ int detect_dense(std::vector<JobSpec>& specs) {
   return PSG_OK;
 }
 
-// PSG_PACK=0|1 forces the round form.
-int forced_pack() {
-  const char* e = getenv("PSG_PACK");
-  return e && (e[0] == '0' || e[0] == '1') ? e[0] - '0' : -1;
-}
-
-// PSG_ZERO_COPY=0 stages pinned buffers (and job-table images) with DMA
-// copies instead of the zero-copy kernel (A/B and fallback knob)
-bool zero_copy_enabled() {
-  const char* e = getenv("PSG_ZERO_COPY");
-  return !(e && e[0] == '0');
-}
-
-// PSG_WIDE=0|1 forces the tile kernel's push-group size (32 | 64).
-int forced_wide() {
-  const char* e = getenv("PSG_WIDE");
-  return e && (e[0] == '0' || e[0] == '1') ? e[0] - '0' : -1;
-}
-
 struct JobTable {
   int device = -1;
   int knob_part = -1, knob_pack = -1, knob_wide = -1;  // forced (read_knobs), -1 = chosen
-  void read_knobs() {
-    knob_part = forced_part_mode();
-    knob_pack = forced_pack();
-    knob_wide = forced_wide();
-    zero_copy = zero_copy_enabled();
+  void read_knobs(unsigned f) {
+    knob_part = (f & PSG_PART_SEARCH) ? (int)psg::kSearch
+                : (f & PSG_PART_STREAM) ? (int)psg::kStream : -1;
+    knob_pack = (f & PSG_FORM_PACKED) ? 1 : (f & PSG_FORM_UNIFORM) ? 0 : -1;
+    knob_wide = (f & PSG_GROUP64) ? 1 : (f & PSG_GROUP32) ? 0 : -1;
+    zero_copy = !(f & PSG_NO_ZERO_COPY);
   }
   bool pack = false;  // rounds may hold several pushes
   bool wide = false;  // push groups of 64 in the tile kernel (a job has > 32 pushes)
@@ -559,6 +530,11 @@ struct PendingPush {
   size_t vbytes = 0;
   void* d_vals[psg::kMaxM] = {};
   uint64_t n = 0;
+  // a contiguous slice of the server keys (psg_push's dense test): the merge
+  // reads D[dpos, dpos + n) of the aggregate's range in place of the keys
+  bool dense = false;
+  uint64_t dpos = 0;           // position of the first key in [lo, hi)
+  const uint64_t* kd = nullptr;  // D + lo + dpos
 };
 
 struct Aggregate {
@@ -860,11 +836,18 @@ struct psg_ctx {
       js.nslots = a.hi - a.lo;
       js.flags = (flags & PSG_PARALLEL_MATCH ? psg::kFlagParallel : 0u) |
                  (a.folded > 0 ? psg::kFlagCont : 0u);
+      bool dense = true;
       for (size_t p = 0; p < take; ++p) {
         const PendingPush& pp = a.pending[p];
-        js.pkeys.push_back(pp.keys->d);
+        js.pkeys.push_back(pp.kd ? pp.kd : pp.keys->d);
         for (int i = 0; i < a.m; ++i) js.pvals.push_back(pp.d_vals[i]);
         js.pn.push_back(pp.n);
+        dense = dense && pp.dense;
+      }
+      // every push a contiguous slice: the dense kernel (no key reads)
+      if (dense) {
+        js.dense = true;
+        for (size_t p = 0; p < take; ++p) js.dpos.push_back(a.pending[p].dpos);
       }
       for (int i = 0; i < a.m; ++i) js.out.push_back(outs ? outs[i] : a.d_out[i]);
       if (int rc = table.build(device, dtype, a.m, {js}, stream, true)) return rc;
@@ -890,8 +873,13 @@ struct psg_ctx {
   // the value push behind psg_push / psg_push_cached / psg_push_compressed:
   // keys already resident; values staged from the host, or (vblock) already
   // resident in a pool block of m arrays of align_up(n * s_V, 256) bytes
+  // `slice`: the push is D[*slice, *slice + n) (absolute positions) by its
+  // end keys; its staged keys are checked strictly increasing on `copy`
+  // (the order check that completes the proof, psg_push) into the
+  // aggregate's unmatched counter
   int push_values(int chl, int time, uint64_t kb, uint64_t ke, const KeyRef& keys, int m,
-                  const void* const* vals, void* vblock = nullptr);
+                  const void* const* vals, void* vblock = nullptr,
+                  const size_t* slice = nullptr);
 };
 
 namespace {
@@ -964,10 +952,10 @@ int psg_plan_create(int device, int dtype, int m, unsigned flags,
     for (int i = 0; i < m; ++i) s.out.push_back(J.out[i]);
     bytes += J.nslots * (8 + m * sv);
   }
-  if (dense_enabled())
+  if (!(flags & PSG_NO_DENSE))
     if (int rc = detect_dense(specs)) return rc;
   psg_plan* p = new psg_plan();
-  p->table.read_knobs();
+  p->table.read_knobs(flags);
   int rc = p->table.build(device, dtype, m, specs);
   if (rc) {
     p->table.release();
@@ -1111,12 +1099,8 @@ int psg_create(int device, int dtype, unsigned flags, psg_ctx** out) {
   c->device = device;
   c->dtype = dtype;
   c->flags = flags;
-  if (const char* f = getenv("PSG_FLUSH_PUSHES")) {  // testing aid: force launch seams
-    const long v = atol(f);
-    if (v >= 1 && v <= psg::kMaxPush) c->flush_pushes = (size_t)v;
-  }
-  c->table.read_knobs();
-  c->zero_copy = zero_copy_enabled();
+  c->table.read_knobs(flags);
+  c->zero_copy = !(flags & PSG_NO_ZERO_COPY);
   hipError_t e = hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking);
   if (e == hipSuccess) e = hipStreamCreateWithFlags(&c->copy, hipStreamNonBlocking);
   if (e == hipSuccess) e = hipEventCreateWithFlags(&c->copy_ev, hipEventDisableTiming);
@@ -1167,7 +1151,18 @@ int psg_destroy(psg_ctx* c) {
 int psg_set_match_flags(psg_ctx* c, unsigned flags) {
   if (!c) return fail(PSG_ERR_ARG, "null ctx");
   std::lock_guard<std::mutex> l(c->mu);
+  if (c->zc.n) HIP_TRY(hipSetDevice(c->device));
+  if (int rc = c->zc_flush()) return rc;  // held copies were queued under the old mode
   c->flags = flags;
+  c->table.read_knobs(flags);
+  c->zero_copy = !(flags & PSG_NO_ZERO_COPY);
+  return PSG_OK;
+}
+
+int psg_set_flush_pushes(psg_ctx* c, int n) {
+  if (!c || n < 1 || n > psg::kMaxPush) return fail(PSG_ERR_ARG, "flush pushes %d", n);
+  std::lock_guard<std::mutex> l(c->mu);
+  c->flush_pushes = (size_t)n;
   return PSG_OK;
 }
 
@@ -1253,7 +1248,7 @@ int check_push(psg_ctx* c, int chl, int time, uint64_t kb, uint64_t ke, size_t n
 }  // namespace
 
 int psg_ctx::push_values(int chl, int time, uint64_t kb, uint64_t ke, const KeyRef& keys, int m,
-                         const void* const* vals, void* vblock) {
+                         const void* const* vals, void* vblock, const size_t* slice) {
   (void)kb;
   (void)ke;
   size_t lo = 0, hi = 0;
@@ -1291,11 +1286,19 @@ int psg_ctx::push_values(int chl, int time, uint64_t kb, uint64_t ke, const KeyR
     A.hi = hi;
     for (int i = 0; i < m; ++i)
       if (int rc = dev_get((hi - lo) * sv, &A.d_out[i], stream)) return rc;
-    if (int rc = dev_get(8, (void**)&A.d_bad, stream)) return rc;
-    HIP_TRY(hipMemsetAsync(A.d_bad, 0, 8, stream));
+    // zeroed on `copy`: the dense pushes' order checks add to it there;
+    // every reader on `stream` runs after a join_copy
+    if (int rc = dev_get(8, (void**)&A.d_bad, copy)) return rc;
+    HIP_TRY(hipMemsetAsync(A.d_bad, 0, 8, copy));
     ait = agg.emplace(time, A).first;
   }
   Aggregate& A = ait->second;
+  if (slice) {
+    pp.dense = true;
+    pp.dpos = *slice - lo;
+    pp.kd = ch[chl].d_keys + *slice;
+    HIP_TRY(psg::launch_check_sorted(keys->d, n, A.d_bad, copy, true));
+  }
   A.pending.push_back(pp);
   A.expected_total += n;
   if (A.pending.size() >= flush_pushes) return flush(A);
@@ -1403,10 +1406,27 @@ int psg_push(psg_ctx* c, int chl, int time, uint64_t kb, uint64_t ke,
   if (int rc = set_dev(c->device)) return rc;
   size_t lo, hi;
   if (int rc = check_push(c, chl, time, kb, ke, n, m, &lo, &hi)) return rc;
+  // Dense test ("back - front + 1 == n"): the push's first
+  // key is server key a, its last is server key a + n - 1, and those n
+  // server keys are n consecutive integers.  Then n strictly increasing
+  // keys between them can only be exactly D[a, a + n): the merge reads no
+  // keys (dense kernel, D's slice stands in for them) and the staged keys
+  // are only checked strictly increasing, on the copy stream, into the
+  // unmatched count psg_received reports -- the reference's
+  // CHECK_EQ(matched, n) (kv_vector.h:192) in full.
+  size_t a = 0;
+  bool dense = false;
+  if (n >= kDenseMinKeys) {
+    const std::vector<uint64_t>& h = c->ch[chl].h_keys;
+    a = std::lower_bound(h.begin() + lo, h.begin() + hi, keys[0]) - h.begin();
+    dense = a + n <= hi && h[a] == keys[0] && h[a + n - 1] == keys[n - 1] &&
+            h[a + n - 1] - h[a] == n - 1;
+  }
   KeyRef k;
   int rc = c->new_keys(n, &k);
-  if (rc == PSG_OK) rc = c->h2d(k->d, keys, 8 * n, true);
-  if (rc == PSG_OK) rc = c->push_values(chl, time, kb, ke, k, m, vals);
+  // a dense push's keys are read by its check right away: not deferred
+  if (rc == PSG_OK) rc = c->h2d(k->d, keys, 8 * n, !dense);
+  if (rc == PSG_OK) rc = c->push_values(chl, time, kb, ke, k, m, vals, nullptr, dense ? &a : nullptr);
   const int rf = c->h2d_finish();
   return rc ? rc : rf;
 }

@@ -49,6 +49,18 @@
 
 namespace psg {
 
+#ifdef PSG_PHASES
+// diagnostic build only (tools/phases.py): shader clocks between the phase
+// marks of thread 0 of every workgroup, one row per tile (plain stores, no
+// contention), rows of the last launch
+constexpr int kPhTiles = 1 << 17;
+__device__ uint32_t g_phase[kPhTiles][8];
+#define PH(i) do { if (tid == 0 && ti < (uint32_t)kPhTiles) { const unsigned long long _t = clock64(); \
+    g_phase[ti][i] += (uint32_t)(_t - ph_t); ph_t = _t; } } while (0)
+#else
+#define PH(i) do { } while (0)
+#endif
+
 namespace {
 
 template <typename T>
@@ -149,6 +161,11 @@ __global__ __launch_bounds__(nt_of(kGroup), (occupancy<V, M, kGroup>())) void ti
   const int lane = tid & 63;
   const uint32_t ti = xcd_tile(blockIdx.x, gridDim.x);
   if (ti >= ntiles) return;
+#ifdef PSG_PHASES
+  unsigned long long ph_t = clock64();
+  if (tid == 0 && ti < (uint32_t)kPhTiles)
+    for (int i = 0; i < 8; ++i) g_phase[ti][i] = 0;
+#endif
   const TileDesc& T = tiles[ti];
   const uint32_t np = T.np;
   const uint32_t nt = T.nt;
@@ -254,6 +271,7 @@ __global__ __launch_bounds__(nt_of(kGroup), (occupancy<V, M, kGroup>())) void ti
   }
   if (tid == 0) pcarry = -1;
   __syncthreads();  // (1) tables, D, cleared histogram
+  PH(0);
 
   // ---- a pass: this wave's run of rounds, loaded into registers
   uint32_t done = 0, U = np ? uni(rpre[np < (uint32_t)kGroup ? np : kGroup]) : 0u;
@@ -290,7 +308,7 @@ __global__ __launch_bounds__(nt_of(kGroup), (occupancy<V, M, kGroup>())) void ti
     }
   };
   if (U) load_pass();
-
+  PH(1);
 
   // ---- bucket table: histogram, exclusive scan -> bt[b] = first slot of bucket b
   // D keys back from LDS: the registers that held them are free during the
@@ -334,6 +352,7 @@ __global__ __launch_bounds__(nt_of(kGroup), (occupancy<V, M, kGroup>())) void ti
     if (tid == 0) bt[kNB] = (uint16_t)nt;
   }
   __syncthreads();  // (4)
+  PH(2);
 
   for (;;) {
     if (!U) {  // this group of pushes has no keys in the tile, or is done
@@ -377,6 +396,7 @@ __global__ __launch_bounds__(nt_of(kGroup), (occupancy<V, M, kGroup>())) void ti
       if ((uint32_t)r + 1u == nrw) mylast = (int)pos[r];
     if (nrw && lane == 63) lastpos[w] = mylast;
     __syncthreads();  // (5) lastpos of every wave
+    PH(3);
 
     // ---- order check
 #pragma unroll
@@ -426,6 +446,7 @@ __global__ __launch_bounds__(nt_of(kGroup), (occupancy<V, M, kGroup>())) void ti
       }
       __syncthreads();
     }
+    PH(4);
 
     // ---- next pass, or next group of pushes
     done += kNW * Rw;
@@ -437,6 +458,7 @@ __global__ __launch_bounds__(nt_of(kGroup), (occupancy<V, M, kGroup>())) void ti
     if (tid == 0) pcarry = -1;
   }
 
+  PH(5);
   // ---- the "+0.0" of absent pushes (serial), stores.  The reference adds
   // +0.0 for every push lacking the key (kv_vector.h:200); adding +0.0 is
   // the identity except on -0.0 (-> +0.0) and a signalling NaN (quieted),
@@ -474,6 +496,7 @@ __global__ __launch_bounds__(nt_of(kGroup), (occupancy<V, M, kGroup>())) void ti
         if (s0 + j < nt) GW(o)[j] = res[mi][j];
     }
   }
+  PH(6);
 }
 
 template <typename V, int M>
@@ -497,6 +520,14 @@ hipError_t launch_m(int m, const TileDesc* t, uint32_t n, bool wide, hipStream_t
 }
 
 }  // namespace
+
+#ifdef PSG_PHASES
+// out: ntiles x 8 u32 rows of the last launch
+extern "C" int psg_debug_phases(uint32_t* out, uint32_t ntiles) {
+  if (ntiles > (uint32_t)kPhTiles) ntiles = kPhTiles;
+  return hipMemcpyFromSymbol(out, HIP_SYMBOL(g_phase), (size_t)ntiles * 32) == hipSuccess ? 0 : -1;
+}
+#endif
 
 hipError_t launch_aggregate_tile(int dtype, int m, const TileDesc* d_tiles, uint32_t ntiles,
                                  bool wide, hipStream_t stream) {

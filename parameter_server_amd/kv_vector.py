@@ -56,14 +56,21 @@ class KVVector:
     """KVVector<uint64, V> with keys, values and aggregates resident in HBM."""
 
     def __init__(self, device: int = 0, dtype: int = PSG_F32,
-                 parallel_match: bool = False):
+                 parallel_match: bool = False, flags: int = 0):
+        """flags: context options of psg_create (PSG_HOLD_BUFFERS and the
+        kernel-form overrides of include/psg.h, tests only)."""
         self._L = _lib.lib()
         self.dtype = dtype
         self.np_dtype = _np_dtype(dtype)
         h = C.c_void_p()
-        flags = PSG_PARALLEL_MATCH if parallel_match else PSG_SERIAL_MATCH
+        self._opts = flags & ~PSG_PARALLEL_MATCH
+        flags = self._opts | (PSG_PARALLEL_MATCH if parallel_match else PSG_SERIAL_MATCH)
         _lib.check(self._L.psg_create(device, dtype, flags, C.byref(h)))
         self._h = h
+
+    def set_flush_pushes(self, n: int) -> None:
+        """Pushes merged per launch (launch seams; psg_set_flush_pushes)."""
+        _lib.check(self._L.psg_set_flush_pushes(self._h, n))
 
     def close(self):
         if getattr(self, "_h", None):
@@ -79,7 +86,7 @@ class KVVector:
     def set_parallel_match(self, on: bool):
         """FLAGS_parallel_match (system/postoffice.cc:24)."""
         _lib.check(self._L.psg_set_match_flags(
-            self._h, PSG_PARALLEL_MATCH if on else PSG_SERIAL_MATCH))
+            self._h, self._opts | (PSG_PARALLEL_MATCH if on else PSG_SERIAL_MATCH)))
 
     # -- key(ch) / value(ch) / find(ch, range): kv_vector.h:17-23 ---------
     def key(self, channel: int) -> np.ndarray:
@@ -200,7 +207,8 @@ class MergePlan:
     """
 
     def __init__(self, device: int, dtype: int, m: int, jobs: Sequence[dict],
-                 parallel_match: bool = False):
+                 parallel_match: bool = False, flags: int = 0):
+        """flags: kernel-form overrides of include/psg.h (tests, A/B only)."""
         self._L = _lib.lib()
         self._keep = []
         cj = (_lib.MergeJob * max(1, len(jobs)))()
@@ -219,7 +227,8 @@ class MergePlan:
             cj[j].push_n = C.cast(pn, C.POINTER(C.c_uint64))
             cj[j].out = C.cast(out, C.POINTER(C.c_void_p))
         h = C.c_void_p()
-        flags = PSG_PARALLEL_MATCH if parallel_match else PSG_SERIAL_MATCH
+        flags = (flags & ~PSG_PARALLEL_MATCH) | (PSG_PARALLEL_MATCH if parallel_match
+                                                 else PSG_SERIAL_MATCH)
         _lib.check(self._L.psg_plan_create(device, dtype, m, flags, cj, len(jobs),
                                            C.byref(h)))
         self._h = h

@@ -81,27 +81,9 @@ def exchange_pieces(pushes, bounds, dist, device=None):
     return result
 
 
-def exchange_unsliced(args, rank, world, bounds, dist):
-    """bench.py --ingress unsliced: each rank draws its pushes of `batch`
-    aggregates (keys over the full key space), re-homes their pieces, and
-    returns for each aggregate its shard's job (all sources' pieces)."""
-    import torch
-    from . import synth
-    dev = torch.device("cuda", torch.cuda.current_device())
-    jobs = []
-    for j in range(args.batch):
-        D, pushes = synth.overlap_pushes(1 + j + 1000 * rank, args.npush, args.n, args.overlap)
-        per_src = exchange_pieces(pushes, bounds, dist, dev)
-        # one aggregate per j: every source's pieces, in (source, push) order
-        pieces = [pc for src in per_src for pc in src if pc[0].size]
-        if pieces:
-            Dsh = np.unique(np.concatenate([k for k, _ in pieces]))
-            jobs.append((Dsh, pieces))
-    return jobs
-
-
 class UnslicedExchange:
-    """Mode B inside the timed step (bench.py --ingress unsliced).
+    """Mode B inside a timed step (bench.py's cfg5 "unsliced" leg uses the
+    RCCL form directly, :class:`RcclExchange`).
 
     The rank holds whole pushes of `len(aggs)` aggregates on its device
     (aggs[j] = [(keys, [vals])] per push).  A step re-homes them: one gather
@@ -111,9 +93,13 @@ class UnslicedExchange:
     xGMI on GPUs; gloo in the CPU tests; a plain copy at world size 1).
     The slice positions are computed once at set-up (a sorted push's cut
     is data-dependent but costs S binary searches, the partition kernel's
-    work class).  After a step, `recv_keys`/`recv_vals` hold, for source
-    rank src, aggregate j and push p, the piece at `recv_off[src, j, p]`
-    with `recv_cnt[src, j, p]` keys: the layout the merge plan points at.
+    work class).  After a step, source rank src's piece of aggregate j,
+    push p starts at `recv_off[src, j, p]` with `recv_cnt[src, j, p]` keys:
+    the layout the merge plan points at.  The received data is the tensors
+    `recv_keys` / `recv_vals` (torch.distributed form), or device memory at
+    `x.recv_keys_ptr` / `x.recv_vals_ptr` (the GPU form, `x` an
+    :class:`RcclExchange`).  `bounds` must be evenDivide(world), the
+    server ranges both forms cut at.
     """
 
     def __init__(self, aggs, bounds, dist, device):
@@ -124,6 +110,10 @@ class UnslicedExchange:
         m = len(aggs[0][0][1])
         vdt = aggs[0][0][1][0].dtype
         self.x = None
+        from .kv_vector import shard_bounds
+        if not np.array_equal(np.asarray(bounds, np.uint64), shard_bounds(world)):
+            raise ValueError("UnslicedExchange cuts at evenDivide(world) (linear_method.cc:"
+                             "137-145); other bounds are not supported")
         if torch.device(device).type == "cuda":
             # GPUs: the C ABI's RCCL exchange (cut + pack kernels, grouped
             # send/recv per peer); bounds are evenDivide(world) there too
@@ -280,10 +270,91 @@ class RcclExchange:
         from . import _lib
         _lib.check(self._L.psg_exchange_run(self._h, stream))
 
+    def status(self) -> int:
+        """Cut positions of any run that differed from the set-up layout
+        (pushes changed since create); raises PSGError if nonzero."""
+        import ctypes as C
+        from . import _lib
+        n = C.c_uint64()
+        _lib.check(self._L.psg_exchange_status(self._h, C.byref(n)))
+        return n.value
+
+    def send_layout(self):
+        """(keys_ptr, [vals_ptr], send_cnt[S, P]) of the packed send buffers."""
+        return _send_layout(self._L, self._h, self.world, self.P, self.m)
+
     def pieces(self):
         """[(offset, count)] per (source, push), arrival order, empties dropped."""
         return [(int(self.recv_off[s, p]), int(self.recv_cnt[s, p]))
                 for s in range(self.world) for p in range(self.P) if self.recv_cnt[s, p]]
+
+    def close(self) -> None:
+        if getattr(self, "_h", None):
+            self._L.psg_exchange_destroy(self._h)
+            self._h = None
+
+    def __del__(self):  # pragma: no cover
+        try:
+            self.close()
+        except Exception:
+            pass
+
+
+def _send_layout(L, h, S, P, m):
+    import ctypes as C
+    from . import _lib
+    keys = C.c_void_p()
+    vals = (C.c_void_p * m)()
+    cnt = np.zeros(max(1, S * P), np.uint64)
+    _lib.check(L.psg_exchange_send_layout(h, C.byref(keys), vals, cnt.ctypes.data))
+    return keys.value, [vals[i] for i in range(m)], cnt[: S * P].reshape(S, P).astype(np.int64)
+
+
+class LocalExchange:
+    """The exchange's slice-and-pack for `nshards` virtual shards on one
+    device, no communicator (psg_exchange_create_local): each run re-cuts
+    the pushes on the device (checked against the set-up layout) and packs
+    shard s's pieces of every push destination-major.  Tests the multi-shard
+    layout of the RCCL path on one GPU.
+
+    pushes: [(keys, [vals] * m)] torch CUDA tensors (keys int64 holding the
+    sorted uint64 keys)."""
+
+    def __init__(self, device: int, pushes, nshards: int, dtype: int):
+        import ctypes as C
+        from . import _lib
+        self._L = _lib.lib()
+        self.S, self.P = nshards, len(pushes)
+        self.m = len(pushes[0][1]) if pushes else 1
+        self._keep = pushes
+        kp = (C.c_void_p * max(1, self.P))(*[k.data_ptr() for k, _ in pushes])
+        ns = (C.c_uint64 * max(1, self.P))(*[k.numel() for k, _ in pushes])
+        vp = (C.c_void_p * max(1, self.P * self.m))(*[v.data_ptr() for _, vs in pushes
+                                                      for v in vs])
+        h = C.c_void_p()
+        _lib.check(self._L.psg_exchange_create_local(device, nshards, dtype, self.m, self.P, kp,
+                                                     ns, vp, C.byref(h)))
+        self._h = h
+        self.keys_ptr, self.vals_ptr, self.send_cnt = _send_layout(self._L, h, nshards, self.P,
+                                                                   self.m)
+        flat = self.send_cnt.reshape(-1)
+        self.send_off = (np.cumsum(flat) - flat).reshape(nshards, self.P)
+
+    def run(self, stream=None) -> None:
+        from . import _lib
+        _lib.check(self._L.psg_exchange_run(self._h, stream))
+
+    def status(self) -> int:
+        import ctypes as C
+        from . import _lib
+        n = C.c_uint64()
+        _lib.check(self._L.psg_exchange_status(self._h, C.byref(n)))
+        return n.value
+
+    def pieces(self, s: int):
+        """Shard s's [(offset, count)] per push, push order, empties dropped."""
+        return [(int(self.send_off[s, p]), int(self.send_cnt[s, p]))
+                for p in range(self.P) if self.send_cnt[s, p]]
 
     def close(self) -> None:
         if getattr(self, "_h", None):

@@ -73,3 +73,111 @@ def test_world1_rccl_exchange_then_hip_merge(dtype, m):
     plan.close()
     x.close()
     shard.destroy_comm(ex.comm)
+
+
+def _dev_pushes(pushes, dev):
+    import torch
+    return [(torch.from_numpy(k.view(np.int64)).to(dev),
+             [torch.from_numpy(np.ascontiguousarray(v)).to(dev) for v in vs]) for k, vs in pushes]
+
+
+@pytest.mark.parametrize("dtype,m", [(np.float32, 1), (np.float64, 2)])
+def test_local_exchange_8_shards_layout_and_merge(dtype, m):
+    """The exchange's cut + pack with 8 shards on one device (the RCCL path's
+    multi-shard layout, psg_exchange_create_local): every shard's packed
+    pieces equal the oracle's sliceKeyOrderedMsg cut (message.h:89-123) at
+    evenDivide(8) (range.h:85-98), in push order; merging each shard's
+    pieces with the HIP plan equals the oracle's aggregate of that shard's
+    key range, bit for bit; a second run lands in the same buffers."""
+    import torch
+    from parameter_server_amd import shard, synth
+    from parameter_server_amd._lib import PSG_F32, PSG_F64
+    from parameter_server_amd.kv_vector import MergePlan, shard_bounds
+    S = 8
+    _, pushes = synth.uniform_pushes(seed=41, npush=12, n=20000, dtype=dtype, m=m, union=False)
+    pushes.append((np.zeros(0, np.uint64), [np.zeros(0, dtype)] * m))  # empty push
+    # a push confined to one shard and one holding the edge keys of shard 3
+    b = shard_bounds(S)
+    pushes.append((np.arange(b[5] + 10, b[5] + 3000, dtype=np.uint64),
+                   [np.full(2990, 0.5, dtype)] * m))
+    edge = np.array([b[3] - 1, b[3], b[4] - 1, b[4]], np.uint64)
+    pushes.append((edge, [np.arange(4, dtype=dtype) + 1] * m))
+    dev = torch.device("cuda", 0)
+    dp = _dev_pushes(pushes, dev)
+    x = shard.LocalExchange(0, dp, S, PSG_F32 if dtype == np.float32 else PSG_F64)
+    for _ in range(2):
+        x.run()
+    torch.cuda.synchronize()
+    assert x.status() == 0
+    sv = np.dtype(dtype).itemsize
+    ntot = int(x.send_cnt.sum())
+    assert ntot == sum(k.size for k, _ in pushes)
+    keys = d2h(x.keys_ptr, 8 * ntot).view(np.uint64)
+    vals = [d2h(p, sv * ntot).view(dtype) for p in x.vals_ptr]
+    ALL = (0, (1 << 64) - 1)
+    for p, (k, vs) in enumerate(pushes):
+        pos, _ = O.slice_key_ordered(k, *ALL, b)
+        for s in range(S):
+            a, e = int(pos[s]), int(pos[s + 1])
+            assert x.send_cnt[s, p] == e - a
+            o = int(x.send_off[s, p])
+            assert np.array_equal(keys[o:o + e - a], k[a:e])
+            for i in range(m):
+                assert vals[i][o:o + e - a].tobytes() == vs[i][a:e].tobytes()
+    # each shard merged by the HIP plan = the oracle over that shard's range
+    D = np.unique(np.concatenate([k for k, _ in pushes]))
+    jobs, outs, wants = [], [], []
+    for s in range(S):
+        lo, hi = O.find_range(D, int(b[s]), int(b[s + 1]))
+        Ds = D[lo:hi]
+        dD = torch.from_numpy(Ds.view(np.int64)).to(dev)
+        o = [torch.empty(max(1, Ds.size), dtype=torch.float32 if dtype == np.float32
+                         else torch.float64, device=dev) for _ in range(m)]
+        pcs = x.pieces(s)
+        jobs.append({"keys": dD.data_ptr(), "nslots": int(Ds.size),
+                     "push_keys": [x.keys_ptr + 8 * a for a, _ in pcs],
+                     "push_vals": [[x.vals_ptr[i] + sv * a for i in range(m)] for a, _ in pcs],
+                     "push_n": [c for _, c in pcs], "out": [t.data_ptr() for t in o]})
+        outs.append((dD, o, Ds.size))
+        pieces = [(keys[a:a + c], [v[a:a + c] for v in vals]) for a, c in pcs]
+        rc, _, _, want, _ = O.aggregate(D, int(b[s]), int(b[s + 1]), pieces, dtype=dtype)
+        assert rc == 0
+        wants.append(want)
+    plan = MergePlan(0, PSG_F32 if dtype == np.float32 else PSG_F64, m, jobs)
+    plan.run()
+    torch.cuda.synchronize()
+    want_n = [c for s in range(S) for _, c in x.pieces(s)]
+    assert list(plan.matched()) == want_n
+    for (dD, o, n), want in zip(outs, wants):
+        for i in range(m):
+            got = o[i].cpu().numpy()[:n]
+            assert got.tobytes() == np.asarray(want[i], dtype).tobytes()
+    plan.close()
+    x.close()
+
+
+def test_local_exchange_detects_changed_keys():
+    """A run re-cuts the pushes on the device: keys changed after set-up so
+    that a piece boundary moves are reported by psg_exchange_status
+    (PSG_ERR_SIZE) instead of being shipped silently with the old cut."""
+    import torch
+    from parameter_server_amd import shard, synth
+    from parameter_server_amd._lib import PSG_F32, PSGError
+    from parameter_server_amd.kv_vector import shard_bounds
+    _, pushes = synth.uniform_pushes(seed=43, npush=4, n=5000, union=False)
+    dp = _dev_pushes(pushes, torch.device("cuda", 0))
+    x = shard.LocalExchange(0, dp, 8, PSG_F32)
+    x.run()
+    assert x.status() == 0
+    # move push 2's first key of shard 5 below the shard 5 boundary
+    k = pushes[2][0]
+    b = shard_bounds(8)
+    i = int(np.searchsorted(k, b[5]))
+    newk = k.copy()
+    newk[i] = np.uint64(b[5] - 1)
+    assert newk[i - 1] < newk[i]
+    dp[2][0].copy_(torch.from_numpy(newk.view(np.int64)))
+    x.run()
+    with pytest.raises(PSGError):
+        x.status()
+    x.close()

@@ -28,10 +28,10 @@ def torch_cuda():
     return torch
 
 
-def kvv(dtype=np.float32, parallel=False):
+def kvv(dtype=np.float32, parallel=False, flags=0):
     from parameter_server_amd.kv_vector import KVVector
     from parameter_server_amd._lib import PSG_F32, PSG_F64
-    return KVVector(0, PSG_F32 if dtype == np.float32 else PSG_F64, parallel)
+    return KVVector(0, PSG_F32 if dtype == np.float32 else PSG_F64, parallel, flags)
 
 
 def msg(keys, vals=None, t=0, ch=0, rng=ALL):
@@ -47,15 +47,20 @@ def bits(a):
 
 
 def assert_bitexact(got, want):
+    """Every bit, NaN payloads included (test_nan_payloads covers the one
+    case where payloads may legitimately differ)."""
     got, want = np.asarray(got), np.asarray(want)
     assert got.shape == want.shape
     gn, wn = np.isnan(got), np.isnan(want)
     assert np.array_equal(gn, wn)
-    assert np.array_equal(bits(got)[~gn], bits(want)[~wn])
+    assert np.array_equal(bits(got), bits(want))
 
 
-def run_ctx(D, pushes, kb=0, ke=(1 << 64) - 1, dtype=np.float32, parallel=False, t=7):
-    v = kvv(dtype, parallel)
+def run_ctx(D, pushes, kb=0, ke=(1 << 64) - 1, dtype=np.float32, parallel=False, t=7,
+            flags=0, flush=None):
+    v = kvv(dtype, parallel, flags)
+    if flush:
+        v.set_flush_pushes(flush)
     v.setValue(msg(D))
     for k, vals in pushes:
         v.setValue(msg(k, [np.asarray(x, dtype) for x in vals], t=t, rng=(kb, ke)))
@@ -147,14 +152,14 @@ def test_random_vs_oracle(torch_cuda, seed, parallel):
 
 
 @pytest.mark.parametrize("per_launch", [7, 64, 4096])
-def test_launch_seams(torch_cuda, per_launch, monkeypatch):
-    """600 pushes for one time split into launches of `per_launch` pushes,
-    each continuing the aggregate (serial zero semantics across seams)."""
-    monkeypatch.setenv("PSG_FLUSH_PUSHES", str(per_launch))
+def test_launch_seams(torch_cuda, per_launch):
+    """600 pushes for one time split into launches of `per_launch` pushes
+    (psg_set_flush_pushes), each continuing the aggregate (serial zero
+    semantics across seams)."""
     D, pushes = random_case(11, np.float32, 1, 600, 0.02, 4000)
     pushes = [p for p in pushes if p[0].size]
     for parallel in (False, True):
-        out = run_ctx(D, pushes, dtype=np.float32, parallel=parallel)
+        out = run_ctx(D, pushes, dtype=np.float32, parallel=parallel, flush=per_launch)
         _, lo, hi, want, _ = O.aggregate(D, *ALL, pushes, parallel, 1, np.float32)
         assert_bitexact(out[0][1], want[0])
 
@@ -171,15 +176,15 @@ def test_dense_and_crowded_tiles(torch_cuda):
 
 @pytest.mark.parametrize("dtype,m", [(np.float64, 1), (np.float64, 2), (np.float32, 3),
                                      (np.float32, 4), (np.float64, 4)])
-def test_packed_rounds_value_types(torch_cuda, dtype, m, monkeypatch):
+def test_packed_rounds_value_types(torch_cuda, dtype, m):
     """The packed kernel (2048-slot tiles) for every value type and array
     count it instantiates, sparse pushes spanning several tiles and push
     groups, serial and parallel, bit-exact against the oracle."""
-    monkeypatch.setenv("PSG_PACK", "1")
+    from parameter_server_amd._lib import PSG_FORM_PACKED
     D, pushes = random_case(31 + m, dtype, m, 150, 0.004, 30000)
     pushes = [p for p in pushes if p[0].size]
     for parallel in (False, True):
-        out = run_ctx(D, pushes, dtype=dtype, parallel=parallel)
+        out = run_ctx(D, pushes, dtype=dtype, parallel=parallel, flags=PSG_FORM_PACKED)
         rc, lo, hi, want, _ = O.aggregate(D, *ALL, pushes, parallel, 1, dtype)
         assert rc == 0 and len(out) == m
         for i in range(m):
@@ -205,10 +210,11 @@ def extreme_range_keys():
 
 
 @pytest.mark.parametrize("pack", ["0", "1"])
-def test_extreme_key_ranges(torch_cuda, pack, monkeypatch):
+def test_extreme_key_ranges(torch_cuda, pack):
     """Bucket scale (f32 reciprocal with a margin) at the key-range edges,
     crowded buckets, both round forms and both match modes, bit-exact."""
-    monkeypatch.setenv("PSG_PACK", pack)
+    from parameter_server_amd._lib import PSG_FORM_PACKED, PSG_FORM_UNIFORM
+    flags = PSG_FORM_PACKED if pack == "1" else PSG_FORM_UNIFORM
     D = extreme_range_keys()
     rng = np.random.default_rng(77)
     pushes = []
@@ -218,7 +224,7 @@ def test_extreme_key_ranges(torch_cuda, pack, monkeypatch):
         v[rng.random(k.size) < 0.05] = -0.0
         pushes.append((k, [v]))
     for parallel in (False, True):
-        out = run_ctx(D, pushes, parallel=parallel)
+        out = run_ctx(D, pushes, parallel=parallel, flags=flags)
         rc, lo, hi, want, _ = O.aggregate(D, *ALL, pushes, parallel, 1, np.float32)
         assert rc == 0
         assert_bitexact(out[0][1], want[0])
@@ -325,7 +331,7 @@ def to_dev(torch, a):
     return torch.from_numpy(a).cuda()
 
 
-def plan_for(torch, cases, dtype=np.float32, parallel=False):
+def plan_for(torch, cases, dtype=np.float32, parallel=False, flags=0):
     from parameter_server_amd.kv_vector import MergePlan
     from parameter_server_amd._lib import PSG_F32, PSG_F64
     keep, jobs = [], []
@@ -341,7 +347,7 @@ def plan_for(torch, cases, dtype=np.float32, parallel=False):
                      "push_vals": [[t.data_ptr() for t in vs] for vs in pv],
                      "push_n": [k.size for k, _ in pushes],
                      "out": [o.data_ptr() for o in out]})
-    plan = MergePlan(0, PSG_F32 if dtype == np.float32 else PSG_F64, m, jobs, parallel)
+    plan = MergePlan(0, PSG_F32 if dtype == np.float32 else PSG_F64, m, jobs, parallel, flags)
     return plan, keep
 
 
@@ -425,15 +431,16 @@ def test_plan_dense_slices(torch_cuda, dtype, parallel):
 
 
 @pytest.mark.parametrize("pack", ["0", "1"])
-def test_plan_round_forms_agree(torch_cuda, pack, monkeypatch):
-    """Both aggregate kernels on the same jobs, forced with PSG_PACK (read at
-    plan creation): push-uniform rounds (psg_tile.hip) and packed multi-push
+def test_plan_round_forms_agree(torch_cuda, pack):
+    """Both aggregate kernels on the same jobs, forced with the plan flags
+    PSG_FORM_PACKED / PSG_FORM_UNIFORM: push-uniform rounds (psg_tile.hip) and packed multi-push
     rounds (psg_tile_packed.hip), whose rounds hold several pushes that can
     hit one slot (heavy overlap: many same-slot lanes per round, resolved in
     push order) -- bit-exact either way, serial and parallel."""
     torch = torch_cuda
     from parameter_server_amd import synth
-    monkeypatch.setenv("PSG_PACK", pack)
+    from parameter_server_amd._lib import PSG_FORM_PACKED, PSG_FORM_UNIFORM
+    flags = PSG_FORM_PACKED if pack == "1" else PSG_FORM_UNIFORM
     rng = np.random.default_rng(5)
     D = np.unique(rng.integers(0, 1 << 50, 20000, dtype=np.uint64))
     tiny = [(np.sort(rng.choice(D, n, replace=False)),
@@ -444,7 +451,7 @@ def test_plan_round_forms_agree(torch_cuda, pack, monkeypatch):
     cases = [(D, tiny), synth.overlap_pushes(8, npush=70, n=2000, overlap=0.9),
              synth.zipf_pushes(9, npush=24, n=3000)]
     for parallel in (False, True):
-        plan, keep = plan_for(torch, cases, parallel=parallel)
+        plan, keep = plan_for(torch, cases, parallel=parallel, flags=flags)
         plan.run()
         assert plan.matched().tolist() == [k.size for _, ps in cases for k, _ in ps]
         for j, (Dj, pushes) in enumerate(cases):
@@ -454,15 +461,16 @@ def test_plan_round_forms_agree(torch_cuda, pack, monkeypatch):
 
 
 @pytest.mark.parametrize("mode", ["search", "stream"])
-def test_plan_partition_modes_agree(torch_cuda, mode, monkeypatch):
+def test_plan_partition_modes_agree(torch_cuda, mode):
     """Both partition modes on dense and sparse jobs, forced
-    with PSG_PART_MODE (read at plan creation): every (push, tile) piece must
+    with the plan flags PSG_PART_SEARCH / PSG_PART_STREAM: every (push, tile) piece must
     come out the same, so the merge is bit-exact either way, including
     pushes much sparser than the tiles (window fallback of the stream mode)
     and pushes with keys below D[0] or above D[-1] only in other tiles."""
     torch = torch_cuda
     from parameter_server_amd import synth
-    monkeypatch.setenv("PSG_PART_MODE", mode)
+    from parameter_server_amd._lib import PSG_PART_SEARCH, PSG_PART_STREAM
+    flags = PSG_PART_SEARCH if mode == "search" else PSG_PART_STREAM
     rng = np.random.default_rng(77)
     D = np.unique(rng.integers(0, 1 << 60, 300000, dtype=np.uint64))
     sparse = [(np.sort(rng.choice(D, n, replace=False)),
@@ -471,7 +479,7 @@ def test_plan_partition_modes_agree(torch_cuda, mode, monkeypatch):
              (D, sparse),
              synth.zipf_pushes(22, npush=20, n=4000)]
     for parallel in (False, True):
-        plan, keep = plan_for(torch, cases, parallel=parallel)
+        plan, keep = plan_for(torch, cases, parallel=parallel, flags=flags)
         plan.run()
         assert plan.matched().tolist() == [k.size for _, ps in cases for k, _ in ps]
         for (Dj, pushes), out in zip(cases, keep[3::4]):
@@ -623,3 +631,104 @@ def test_device_entry_points(torch_cuda):
         torch.cuda.synchronize()
         pos, _ = O.slice_key_ordered(D, kb, ke, sep)
         assert np.array_equal(dpos.cpu().numpy().view(np.uint64), pos)
+
+
+# --------------------------------------------- dense slices through psg_push
+@pytest.mark.parametrize("parallel", [False, True])
+def test_push_dense_slices_server_api(torch_cuda, parallel):
+    """psg_push's dense test: pushes that are contiguous
+    slices of a contiguous key range take the dense kernel (no key reads;
+    their keys are only checked strictly increasing on the copy stream);
+    mixed with a sparse push they take the general kernels with D's slice
+    standing in for the keys.  Bit-exact against the oracle either way, with
+    launch seams, -0.0 and sub-ranges."""
+    rng = np.random.default_rng(3)
+    D = np.arange(1000, 1000 + 200000, dtype=np.uint64)
+    pushes = []
+    for a, n in [(0, 200000), (5000, 70000), (0, 200000), (150000, 50000), (1, 4096)]:
+        v = rng.standard_normal(n).astype(np.float32)
+        v[rng.random(n) < 0.03] = -0.0
+        pushes.append((D[a:a + n].copy(), [v]))
+    for flush in (None, 2):
+        out = run_ctx(D, pushes, parallel=parallel, flush=flush)
+        _, lo, hi, want, _ = O.aggregate(D, *ALL, pushes, parallel, 1, np.float32)
+        assert_bitexact(out[0][1], want[0])
+    # a sparse push among them: general kernels, same bits
+    sp = np.sort(rng.choice(D, 3000, replace=False))
+    mixed = pushes[:2] + [(sp, [rng.standard_normal(sp.size).astype(np.float32)])] + pushes[2:]
+    out = run_ctx(D, mixed, parallel=parallel)
+    _, lo, hi, want, _ = O.aggregate(D, *ALL, mixed, parallel, 1, np.float32)
+    assert_bitexact(out[0][1], want[0])
+    # a sub-range push (key_range [2000, 90000))
+    kb, ke = 2000, 90000
+    sub = [(np.arange(3000, 50000, dtype=np.uint64), [np.ones(47000, np.float32)])]
+    out = run_ctx(D, sub, kb, ke, parallel=parallel)
+    _, lo, hi, want, _ = O.aggregate(D, kb, ke, sub, parallel, 1, np.float32)
+    assert tuple(out[0][0]) == (lo, hi)
+    assert_bitexact(out[0][1], want[0])
+
+
+def test_push_dense_slice_order_violation_is_unmatched(torch_cuda):
+    """End keys of a slice but two interior keys swapped: the reference's
+    merge walk matches fewer than n keys (CHECK_EQ, kv_vector.h:192); the
+    dense path reports it through the copy-stream order check."""
+    from parameter_server_amd._lib import PSGError, PSG_ERR_UNMATCHED
+    D = np.arange(50000, dtype=np.uint64)
+    k = D.copy()
+    k[100], k[101] = k[101], k[100]
+    v = kvv()
+    v.setValue(msg(D))
+    v.setValue(msg(k, [np.ones(k.size, np.float32)], t=3))
+    with pytest.raises(PSGError) as e:
+        v.received(3)
+    assert e.value.status == PSG_ERR_UNMATCHED
+    v.close()
+
+
+@pytest.mark.parametrize("dtype", [np.float32, np.float64])
+@pytest.mark.parametrize("parallel", [False, True])
+def test_nan_payloads(torch_cuda, dtype, parallel):
+    """NaN payload bits through the fold: quiet and signalling NaNs of both
+    signs with distinct payloads.  A slot with ONE NaN contributor must come
+    out as the reference's IEEE add gives it (the input NaN, quieted) bit
+    for bit.  A slot with two or more NaN contributors is compared only as
+    "one of the input NaNs, quieted": which operand's payload an add of two
+    NaNs keeps is not fixed by IEEE 754 (x86 SSE keeps the first source,
+    and the compiler may commute the reference's `+=`), so the reference
+    itself does not pin it."""
+    ut = np.uint32 if dtype == np.float32 else np.uint64
+    if dtype == np.float32:
+        pays = [0x7fc12345, 0xffc00001, 0x7f800001, 0xff812345, 0x7fffffff]
+        quiet = 1 << 22
+    else:
+        pays = [0x7ff8000000012345, 0xfff8000000000001, 0x7ff0000000000001,
+                0xfff0000000abcdef, 0x7fffffffffffffff]
+        quiet = 1 << 51
+    rng = np.random.default_rng(11)
+    D = np.arange(4000, dtype=np.uint64) * np.uint64(5)
+    pushes = []
+    owner = rng.integers(0, 6, D.size)        # the push that carries a NaN at slot i
+    second = rng.random(D.size) < 0.1          # ... and a second NaN from push owner+1
+    for p in range(6):
+        k = D.copy()
+        v = rng.standard_normal(D.size).astype(dtype)
+        b = v.view(ut)
+        one = owner == p
+        b[one] = np.array(pays, ut)[np.arange(D.size)[one] % len(pays)]
+        two = second & ((owner + 1) % 6 == p)
+        b[two] = np.array(pays, ut)[(np.arange(D.size)[two] + 2) % len(pays)]
+        drop = rng.random(D.size) < 0.2
+        drop[one | two] = False
+        pushes.append((k[~drop], [v[~drop]]))
+    out = run_ctx(D, pushes, dtype=dtype, parallel=parallel)
+    _, _, _, want, _ = O.aggregate(D, *ALL, pushes, parallel, 1, dtype)
+    got = np.asarray(out[0][1])
+    gb, wb = bits(got), bits(np.asarray(want[0], dtype))
+    assert np.array_equal(np.isnan(got), np.isnan(want[0]))
+    single = ~second
+    assert np.array_equal(gb[single], wb[single])
+    # two NaN contributors: one of the two inputs' payloads, quieted
+    idx = np.nonzero(second)[0]
+    pa = np.array(pays, ut)
+    cand = np.stack([pa[idx % len(pays)], pa[(idx + 2) % len(pays)]]) | ut(quiet)
+    assert np.all((gb[idx] == cand[0]) | (gb[idx] == cand[1]))
