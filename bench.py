@@ -642,7 +642,9 @@ def load_traffic(bytes_per_launch, workload):
 def bench_rows(device, reps=5):
     """The SURVEY 8(f) rows beside the merge, each on device-resident input
     with its own HBM roofline: algorithmic bytes / mean kernel time (HIP
-    events on the stream the kernel runs on).  Shapes: the pull of a cfg2
+    events on the stream the kernel runs on).  Shapes: the N-way merge of
+    cfg2's pushes (keys only: the key union; with values: union + sums;
+    a run is 5 small kernels), the pull of a cfg2
     shard, crc32c key signatures of 65,536 pushes and one 1 GiB stream,
     snappy parts of 64 KB, Darling over 16.8 M f64 positions, CountMin
     insert/query of 16.8 M keys into 2^26 counters."""
@@ -672,8 +674,43 @@ def bench_rows(device, reps=5):
                      "unit": unit}
 
     rng = np.random.default_rng(3)
-    # pull gather (getValue) of 1 M sorted request keys from a cfg2 shard
     D, pushes = synth.overlap_pushes(1)
+    # N-way merge (psg_nway): cfg2's 8 key-only pushes ->
+    # the merged key set (BatchSolver's key pushes, setUnion push after
+    # push), and the same pushes with their f32 values -> union + sums
+    from parameter_server_amd.kv_vector import NWayMerge
+    dk = [torch.from_numpy(k.view(np.int64)).to(dev) for k, _ in pushes]
+    dv = [torch.from_numpy(vs[0]).to(dev) for _, vs in pushes]
+    tot = sum(k.size for k, _ in pushes)
+    ok = torch.empty(tot, dtype=torch.int64, device=dev)
+    ov = torch.empty(tot, dtype=torch.float32, device=dev)
+    for name, m in (("key_union", 0), ("nway_merge", 1)):
+        u = NWayMerge(device, _lib.PSG_F32, [t.data_ptr() for t in dk], [k.size for k, _ in pushes],
+                      [[t.data_ptr()] for t in dv] if m else [[] for _ in dk], ok.data_ptr(),
+                      [ov.data_ptr()] if m else [])
+        u.run()
+        nu = u.result()
+        assert nu == D.size, "N-way union size"
+        ms = timed(lambda: u.run(st.cuda_stream))
+        assert u.result() == D.size
+        u.close()
+        row(name, ms, tot * (8 + 4 * m) + D.size * (8 + 4 * m), tot, "keys/s")
+        out[name]["shape"] = ("8 pushes x 131,072 sorted keys (cfg2) -> U = 956,827 merged keys" +
+                              (" + f32 sums" if m else ""))
+    assert np.array_equal(ok[:D.size].cpu().numpy().view(np.uint64), D)
+    del dk, dv, ok, ov
+    # the reference's way: setUnion push after push on one CPU core (oracle)
+    sys.path.insert(0, os.path.join(ROOT, "tests"))
+    import oracle_py as O
+    t0, reps = time.perf_counter(), 0
+    while time.perf_counter() - t0 < 1.0:
+        acc = np.zeros(0, np.uint64)
+        for k, _ in pushes:
+            acc = O.set_union(acc, k)
+        reps += 1
+    el = time.perf_counter() - t0
+    out["key_union"]["cpu_setUnion_keys_per_s"] = reps * tot / el
+    # pull gather (getValue) of 1 M sorted request keys from a cfg2 shard
     req = np.sort(np.concatenate([k for k, _ in pushes[:8]]))[::1]
     dD = torch.from_numpy(D.view(np.int64)).to(dev)
     dW = torch.from_numpy(rng.standard_normal(D.size).astype(np.float32)).to(dev)

@@ -106,6 +106,12 @@ int psg_set_flush_pushes(psg_ctx* ctx, int n);
 /* Key-only push: key_[chl] = key_[chl].setUnion(keys); val_[chl].clear()
  * (kv_vector.h:177-182).  keys must be strictly increasing. */
 int psg_key_union(psg_ctx* ctx, int chl, const uint64_t* keys, size_t n);
+/* npush key-only pushes at once: the same key set as psg_key_union of each
+ * in order (the union is order-free), merged on the device in one N-way
+ * pass per psg_nway_max_push() - 1 pushes (BatchSolver::preprocessData's
+ * key pushes, batch_solver.cc:318-323).  Empty pushes are ignored. */
+int psg_key_union_batch(psg_ctx* ctx, int chl, const uint64_t* const* keys, const size_t* n,
+                        int npush);
 /* key(chl).size() / copy of key(chl)[off, off+n) (kv_vector.h:17). */
 int psg_key_size(psg_ctx* ctx, int chl, size_t* n);
 int psg_key_copy(psg_ctx* ctx, int chl, size_t off, size_t n, uint64_t* out);
@@ -156,9 +162,9 @@ int psg_push_compressed(psg_ctx* ctx, int chl, int time, uint64_t kb, uint64_t k
  * Signature without keys: the cached keys are used in place (no key bytes
  * cross PCIe); a missing entry or another signature is PSG_ERR_SIGNATURE
  * (sig 0 against a missing entry restores no keys: the message is
- * ignored, as the reference's empty key list is).  m == 0 (or nvals == 0)
- * is a key-only message (setUnion); otherwise nvals must equal the key
- * count (PSG_ERR_SIZE). */
+ * ignored, as the reference's empty key list is).  m == 0 is a key-only
+ * message (setUnion, merged on the device); otherwise nvals must equal the
+ * key count (PSG_ERR_SIZE, nvals == 0 included: kv_vector.h:108,187). */
 #define PSG_KC_SIG 1u
 #define PSG_KC_KEYS 2u
 #define PSG_KC_ERASE 4u
@@ -223,11 +229,42 @@ int psg_gather_dev(int dtype, const uint64_t* dkeys, uint64_t nd,
                    const void* dvals, const uint64_t* req, uint64_t nreq,
                    void* out, unsigned long long* matched, void* stream);
 
-/* Device-resident key union: out = a U b (both strictly increasing);
- * out must hold na+nb; *nout (host) receives |a U b|.  Synchronises. */
+/* Device-resident key union: out = a U b (both strictly increasing, else
+ * PSG_ERR_UNSORTED); out must hold na+nb; *nout (host) receives |a U b|.
+ * The N-way merge of psg_nway_* with two pushes.  Synchronises. */
 int psg_key_union_dev(const uint64_t* a, uint64_t na, const uint64_t* b,
                       uint64_t nb, uint64_t* out, uint64_t* nout,
                       void* stream);
+
+/* ------------------------------------------------------------------ */
+/* N-way merge of sorted pushes into their merged key set  */
+/* ------------------------------------------------------------------ */
+/* out_keys = the union of the npush pushes' keys (SArray::setUnion applied
+ * push after push, shared_array_inl.h:155-162), sorted; with m > 0 value
+ * arrays, out_vals[i][j] = the sum over the pushes holding out_keys[j] in
+ * arrival order -- KVVector::serialSetValue / parallelSetValue over that
+ * key set (kv_vector.h:84-204; flags PSG_SERIAL_MATCH / PSG_PARALLEL_MATCH).
+ * Empty pushes are ignored (kv_vector.h:90,177); at most psg_nway_max_push()
+ * non-empty pushes and < 2^32 keys in total.  All pointers are device
+ * pointers except the host arrays keys[npush], n[npush], vals[npush * m]
+ * and out_vals[m]; out_keys / out_vals hold sum(n) entries.  The pushes'
+ * buffers are read again by every run (a prepared merge, like psg_plan).
+ * Run: no host wait, capturable; the merged count is a device word
+ * (psg_nway_count_dev).  psg_nway_result synchronises and returns
+ * PSG_ERR_UNSORTED if a push was not strictly increasing (the reference's
+ * std::set_union precondition; the output is then unspecified). */
+typedef struct psg_nway psg_nway;
+int psg_nway_max_push(void);
+int psg_nway_create(int device, int dtype, int m, unsigned flags, int npush,
+                    const uint64_t* const* keys, const uint64_t* n, const void* const* vals,
+                    uint64_t* out_keys, void* const* out_vals, psg_nway** out);
+int psg_nway_run(psg_nway* u, void* stream);
+int psg_nway_count_dev(psg_nway* u, unsigned long long** nout);
+int psg_nway_result(psg_nway* u, uint64_t* nout);
+/* Algorithmic bytes read by a run (sum(n) * (8 + m s_V)) and keys read;
+ * the merged output adds |union| * (8 + m s_V). */
+int psg_nway_bytes(psg_nway* u, uint64_t* bytes, uint64_t* kv_pairs);
+int psg_nway_destroy(psg_nway* u);
 
 /* ------------------------------------------------------------------ */
 /* Shard exchange over RCCL ("unsliced" ingress)          */

@@ -137,6 +137,15 @@ SIGNATURES = {
     "psg_exchange_create_local": (C.c_int, [C.c_int, C.c_int, C.c_int, C.c_int, C.c_int, _p,
                                             _p, _p, C.POINTER(_p)]),
     "psg_exchange_send_layout": (C.c_int, [_p, C.POINTER(_p), _p, _p]),
+    "psg_key_union_batch": (C.c_int, [_p, C.c_int, _p, _p, C.c_int]),
+    "psg_nway_max_push": (C.c_int, []),
+    "psg_nway_create": (C.c_int, [C.c_int, C.c_int, C.c_int, C.c_uint, C.c_int, _p, _p, _p, _p,
+                                  _p, C.POINTER(_p)]),
+    "psg_nway_run": (C.c_int, [_p, _p]),
+    "psg_nway_count_dev": (C.c_int, [_p, C.POINTER(_p)]),
+    "psg_nway_result": (C.c_int, [_p, _pu64]),
+    "psg_nway_bytes": (C.c_int, [_p, _pu64, _pu64]),
+    "psg_nway_destroy": (C.c_int, [_p]),
     "psg_darling_init": (C.c_int, [_p, C.c_int, C.c_double]),
     "psg_darling_reset_active": (C.c_int, [_p, C.c_int]),
     "psg_darling_update": (C.c_int, [_p, C.c_int, C.c_int, _p, C.POINTER(C.c_double)]),

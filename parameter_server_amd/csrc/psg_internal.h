@@ -122,11 +122,14 @@ hipError_t launch_host_copy_batch(const HostCopyBatch& b, hipStream_t stream);
 hipError_t launch_check_sorted(const uint64_t* keys, uint64_t n,
                                unsigned long long* bad, hipStream_t stream,
                                bool strict = true);
-// out = a U b (strictly increasing inputs).  scratch: >= union_scratch_bytes(nb).
-size_t union_scratch_bytes(uint64_t nb);
-hipError_t launch_union(const uint64_t* a, uint64_t na, const uint64_t* b,
-                        uint64_t nb, uint64_t* out, void* scratch,
-                        uint64_t* d_nout, hipStream_t stream);
+// keys-only N-way union of K (<= 64) non-empty sorted device arrays into
+// out_keys (psg_nway.hip); scratch >= nway_scratch_bytes(K, n).  Uploads its
+// tables with a synchronous copy on `stream`, then enqueues the merge;
+// (*d_bad)[0] = order violations, (*d_bad)[1] = |union| after the stream ran.
+size_t nway_scratch_bytes(uint32_t K, const uint64_t* n);
+hipError_t nway_union_enqueue(uint32_t K, const uint64_t* const* keys, const uint64_t* n,
+                              uint64_t* out_keys, void* scratch, unsigned long long** d_bad,
+                              hipStream_t stream);
 hipError_t launch_slice(const uint64_t* keys, uint64_t n, uint64_t kb,
                         uint64_t ke, const uint64_t* sep, int nsep,
                         uint64_t* pos, hipStream_t stream);

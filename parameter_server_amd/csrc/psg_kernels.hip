@@ -9,7 +9,6 @@
 //   partition  <- SArray::findRange + sliceKeyOrderedMsg lower_bounds
 //                 (src/base/shared_array_inl.h:164-171, message.h:96-99)
 //   gather     <- KVVector::serialGetValue (kv_vector.h:215-227)
-//   union      <- SArray::setUnion (shared_array_inl.h:155-162)
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
@@ -136,123 +135,6 @@ __global__ __launch_bounds__(256) void check_sorted_kernel(
   if ((threadIdx.x & 63) == 0 && m) atomicAdd(bad, (unsigned long long)__popcll(m));
 }
 
-// ----------------------------------------------------------------------
-// two-input union (strictly increasing a, b):
-//   keep[j] = b[j] not in a;  kb = exclusive scan of keep;
-//   out[kb[j] + |a < b[j]|] = b[j] for kept j;  out[i + kb(|b < a[i]|)] = a[i]
-// ----------------------------------------------------------------------
-constexpr int kScanBlock = 256;
-constexpr int kScanItems = 16;
-constexpr int kScanTile = kScanBlock * kScanItems;
-
-__device__ __forceinline__ uint32_t wg256_excl_scan(uint32_t v, uint32_t* ws,
-                                                    uint32_t* total) {
-  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
-  uint32_t x = v;
-#pragma unroll
-  for (int d = 1; d < 64; d <<= 1) {
-    const uint32_t y = __shfl_up(x, d, 64);
-    if (lane >= d) x += y;
-  }
-  if (lane == 63) ws[w] = x;
-  __syncthreads();
-  uint32_t pre = 0, tot = 0;
-#pragma unroll
-  for (int q = 0; q < kScanBlock / 64; ++q) {
-    if (q < w) pre += ws[q];
-    tot += ws[q];
-  }
-  __syncthreads();
-  *total = tot;
-  return pre + x - v;
-}
-
-__global__ __launch_bounds__(kScanBlock) void union_mark_kernel(
-    const uint64_t* __restrict__ a, uint64_t na, const uint64_t* __restrict__ b,
-    uint64_t nb, uint32_t* __restrict__ keep, uint32_t* __restrict__ bsum) {
-  __shared__ uint32_t ws[kScanBlock / 64];
-  const uint64_t base = (uint64_t)blockIdx.x * kScanTile;
-  uint32_t cnt = 0;
-#pragma unroll 4
-  for (int q = 0; q < kScanItems; ++q) {
-    const uint64_t j = base + (uint64_t)q * kScanBlock + threadIdx.x;
-    if (j < nb) {
-      const uint64_t k = b[j];
-      const uint64_t pos = gl_lower_bound(a, na, k);
-      const uint32_t kp = (pos < na && a[pos] == k) ? 0u : 1u;
-      keep[j] = kp;
-      cnt += kp;
-    }
-  }
-  uint32_t tot;
-  wg256_excl_scan(cnt, ws, &tot);
-  if (threadIdx.x == 0) bsum[blockIdx.x] = tot;
-}
-
-// single workgroup: exclusive scan of nblk block sums; d_nout = na + total
-__global__ __launch_bounds__(kScanBlock) void union_scan_kernel(
-    uint32_t* __restrict__ bsum, uint32_t nblk, uint64_t na,
-    uint64_t* __restrict__ d_nout, uint32_t* __restrict__ d_total) {
-  __shared__ uint32_t ws[kScanBlock / 64];
-  uint32_t carry = 0;
-  for (uint32_t c0 = 0; c0 < nblk; c0 += kScanBlock) {
-    const uint32_t idx = c0 + threadIdx.x;
-    const uint32_t v = idx < nblk ? bsum[idx] : 0u;
-    uint32_t tot;
-    const uint32_t ex = wg256_excl_scan(v, ws, &tot);
-    if (idx < nblk) bsum[idx] = carry + ex;
-    carry += tot;
-  }
-  if (threadIdx.x == 0) {
-    *d_total = carry;
-    *d_nout = na + carry;
-  }
-}
-
-__global__ __launch_bounds__(kScanBlock) void union_scatter_b_kernel(
-    const uint64_t* __restrict__ a, uint64_t na, const uint64_t* __restrict__ b,
-    uint64_t nb, uint32_t* __restrict__ keep, const uint32_t* __restrict__ bsum,
-    uint64_t* __restrict__ out) {
-  __shared__ uint32_t ws[kScanBlock / 64];
-  const uint64_t base = (uint64_t)blockIdx.x * kScanTile;
-  // thread-contiguous items so one scan covers the block in order
-  const uint64_t j0 = base + (uint64_t)threadIdx.x * kScanItems;
-  uint32_t f[kScanItems];
-  uint32_t cnt = 0;
-#pragma unroll
-  for (int q = 0; q < kScanItems; ++q) {
-    const uint64_t j = j0 + q;
-    f[q] = j < nb ? keep[j] : 0u;
-    cnt += f[q];
-  }
-  uint32_t tot;
-  uint32_t run = bsum[blockIdx.x] + wg256_excl_scan(cnt, ws, &tot);
-#pragma unroll
-  for (int q = 0; q < kScanItems; ++q) {
-    const uint64_t j = j0 + q;
-    if (j < nb) {
-      keep[j] = run;  // becomes kb[j]
-      if (f[q]) {
-        const uint64_t k = b[j];
-        out[run + gl_lower_bound(a, na, k)] = k;
-      }
-      run += f[q];
-    }
-  }
-}
-
-__global__ __launch_bounds__(256) void union_scatter_a_kernel(
-    const uint64_t* __restrict__ a, uint64_t na, const uint64_t* __restrict__ b,
-    uint64_t nb, const uint32_t* __restrict__ kb,
-    const uint32_t* __restrict__ d_total, uint64_t* __restrict__ out) {
-  const uint64_t i = (uint64_t)blockIdx.x * 256u + threadIdx.x;
-  if (i >= na) return;
-  const uint64_t k = a[i];
-  const uint64_t lb = gl_lower_bound(b, nb, k);
-  const uint64_t c = lb < nb ? kb[lb] : *d_total;
-  out[i + c] = k;
-}
-
 // sliceKeyOrderedMsg positions: one wave per separator (message.h:96-99)
 __global__ __launch_bounds__(256) void slice_kernel(
     const uint64_t* __restrict__ keys, uint64_t n, uint64_t kb, uint64_t ke,
@@ -339,35 +221,6 @@ hipError_t launch_check_sorted(const uint64_t* keys, uint64_t n,
   if (n < 2) return hipSuccess;
   hipLaunchKernelGGL(check_sorted_kernel, dim3((uint32_t)((n + 255) / 256)),
                      dim3(256), 0, stream, keys, n, bad, strict);
-  return hipGetLastError();
-}
-
-size_t union_scratch_bytes(uint64_t nb) {
-  const uint64_t nblk = (nb + kScanTile - 1) / kScanTile;
-  return (size_t)(nb * 4 + nblk * 4 + 64);
-}
-
-hipError_t launch_union(const uint64_t* a, uint64_t na, const uint64_t* b,
-                        uint64_t nb, uint64_t* out, void* scratch,
-                        uint64_t* d_nout, hipStream_t stream) {
-  uint32_t* keep = (uint32_t*)scratch;
-  const uint32_t nblk = (uint32_t)((nb + kScanTile - 1) / kScanTile);
-  uint32_t* bsum = keep + nb;
-  uint32_t* d_total = bsum + nblk;
-  if (nb > 0) {
-    hipLaunchKernelGGL(union_mark_kernel, dim3(nblk), dim3(kScanBlock), 0,
-                       stream, a, na, b, nb, keep, bsum);
-  }
-  hipLaunchKernelGGL(union_scan_kernel, dim3(1), dim3(kScanBlock), 0, stream,
-                     bsum, nblk, na, d_nout, d_total);
-  if (nb > 0) {
-    hipLaunchKernelGGL(union_scatter_b_kernel, dim3(nblk), dim3(kScanBlock), 0,
-                       stream, a, na, b, nb, keep, bsum, out);
-  }
-  if (na > 0) {
-    hipLaunchKernelGGL(union_scatter_a_kernel, dim3((uint32_t)((na + 255) / 256)),
-                       dim3(256), 0, stream, a, na, b, nb, keep, d_total, out);
-  }
   return hipGetLastError();
 }
 

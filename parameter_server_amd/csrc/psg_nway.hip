@@ -1,0 +1,693 @@
+// psg_nway.hip -- N-way merge of sorted pushes into their merged key set
+// (SURVEY 7 step 4): the union of the pushes' keys and, with values, the
+// per-key sums over the pushes in arrival order.
+//
+// Reference semantics:
+//   keys  SArray::setUnion applied push after push (shared_array_inl.h:
+//         155-162, std::set_union; the key-only branch of
+//         KVVector::serialSetValue, kv_vector.h:177-182): the sorted set of
+//         every pushed key, duplicates across pushes collapsed;
+//   sums  KVVector::serialSetValue / parallelSetValue (kv_vector.h:84-204)
+//         over D = that union: per key, push 0 assigns if it holds the key
+//         (the others start from the memset +0.0), later pushes add in
+//         arrival order, and the serial path adds one +0.0 when some push
+//         lacked the key (the dense `+=` of absent pushes).
+//
+// Pipeline (one stream, no host wait; psg_union_run):
+//   1. candidates: every s-th key of every push; its global rank
+//      R(c) = sum_q lower_bound(push q, c)                     (nw_cand)
+//   2. splitter of rank bucket b = the largest candidate with
+//      floor(R / C') == b (atomic max on the key: R is monotone in the key)
+//                                                              (nw_bucket)
+//   3. prefix max over the buckets (empty buckets: empty tiles) (nw_split)
+//   4. per (tile, push) the piece bounds: lower_bound of the splitters
+//                                                              (nw_seg)
+//   5. one workgroup per tile (nw_tile):
+//      - loads its K pieces (keys, and values into LDS), checks each piece
+//        strictly increasing and inside the tile's key range;
+//      - merges the K sorted runs in LDS with a merge-path tree
+//        (ceil(log2 K) rounds; each thread merges 8 outputs in registers,
+//        stable, so equal keys keep push order);
+//      - wavefront ballot for run heads (key != previous), block prefix
+//        scan for the unique index; decoupled look-back across tiles (tiles
+//        in ticket order) for the global offset;
+//      - segmented sum of each run in push order; the merged keys and sums
+//        staged compacted in LDS and written coalesced.
+// Tile size: a candidate every s keys of each push puts consecutive
+// candidates at most K*s ranks apart, so every rank bucket of width C' has a
+// candidate and a tile spans at most C' + K*s + K elements (equal keys of K
+// pushes at its start) <= kCap: no tile overflows, whatever the key
+// distribution.
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include <algorithm>
+#include <cstring>
+#include <vector>
+
+#include "psg_device.h"
+#include "psg_host.h"
+#include "psg_internal.h"
+
+namespace psg {
+
+namespace {
+
+constexpr int kNT = 256;            // threads per tile workgroup
+constexpr int kPer = 8;             // merged elements per thread
+constexpr int kCap = kNT * kPer;    // elements per tile (LDS)
+constexpr int kMaxRuns = 64;        // pushes per merge (runs per tile)
+
+__device__ __forceinline__ uint32_t uni(uint32_t v) { return __builtin_amdgcn_readfirstlane(v); }
+
+// lower_bound over a sorted global array
+__device__ __forceinline__ uint64_t lb_global(const uint64_t* __restrict__ a, uint64_t n,
+                                              uint64_t k) {
+  uint64_t lo = 0, len = n;
+  while (len > 0) {
+    const uint64_t half = len >> 1;
+    if (a[lo + half] < k) {
+      lo += half + 1;
+      len -= half + 1;
+    } else {
+      len = half;
+    }
+  }
+  return lo;
+}
+
+struct NwArgs {
+  const uint64_t* const* keys;  // [K] push keys
+  const void* const* vals;      // [K * M] push values (M > 0)
+  const uint64_t* n;            // [K]
+  const uint64_t* cbase;        // [K + 1] first candidate of each push
+  uint32_t* rank;               // [ncand] R(c)
+  uint64_t* split;              // [B] splitter keys
+  uint32_t* seg;                // [(T + 1) * K] piece starts, tile-major
+  unsigned long long* state;    // [T] look-back words
+  unsigned int* ticket;         // tile tickets
+  unsigned long long* bad;      // order violations / overflow
+  unsigned long long* nout;     // merged key count
+  uint64_t* out_keys;
+  void* const* out_vals;        // [M]
+  uint64_t ncand;
+  uint32_t K, B, T, s, cw;      // pushes, buckets, tiles, sample stride, bucket width C'
+  uint32_t flags;
+};
+
+// 1. R(c) for every candidate c: one thread per (candidate, push)
+__global__ __launch_bounds__(256) void nw_cand_kernel(NwArgs a) {
+  const uint64_t id = (uint64_t)blockIdx.x * 256u + threadIdx.x;
+  if (id >= a.ncand * a.K) return;
+  const uint64_t c = id / a.K;
+  const uint32_t r = (uint32_t)(id - c * a.K);
+  // the push that owns candidate c (K <= 64: linear)
+  uint32_t q = 0;
+  while (q + 1 < a.K && a.cbase[q + 1] <= c) ++q;
+  const uint64_t key = a.keys[q][(c - a.cbase[q]) * a.s + a.s - 1];
+  const uint64_t l = lb_global(a.keys[r], a.n[r], key);
+  atomicAdd(a.rank + c, (uint32_t)l);
+}
+
+// 2. splitter of bucket floor(R / C') = its largest candidate key
+__global__ __launch_bounds__(256) void nw_bucket_kernel(NwArgs a) {
+  const uint64_t c = (uint64_t)blockIdx.x * 256u + threadIdx.x;
+  if (c >= a.ncand) return;
+  uint32_t q = 0;
+  while (q + 1 < a.K && a.cbase[q + 1] <= c) ++q;
+  const uint64_t key = a.keys[q][(c - a.cbase[q]) * a.s + a.s - 1];
+  const uint32_t b = a.rank[c] / a.cw;
+  if (b < a.B) atomicMax((unsigned long long*)a.split + b, (unsigned long long)key);
+}
+
+// 3. prefix max (one workgroup): splitters non-decreasing, empty buckets
+// repeat the previous splitter (an empty tile)
+__global__ __launch_bounds__(256) void nw_split_kernel(NwArgs a) {
+  __shared__ uint64_t wmax[4];
+  __shared__ uint64_t carry;
+  if (threadIdx.x == 0) carry = 0;
+  __syncthreads();
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  for (uint32_t b0 = 0; b0 < a.B; b0 += 256) {
+    const uint32_t b = b0 + threadIdx.x;
+    uint64_t x = b < a.B ? a.split[b] : 0;
+#pragma unroll
+    for (int d = 1; d < 64; d <<= 1) {
+      const uint64_t y = __shfl_up(x, d, 64);
+      if (lane >= d && y > x) x = y;
+    }
+    if (lane == 63) wmax[w] = x;
+    __syncthreads();
+    uint64_t pre = carry;
+    for (int v = 0; v < w; ++v) pre = wmax[v] > pre ? wmax[v] : pre;
+    x = x > pre ? x : pre;
+    if (b < a.B) a.split[b] = x;
+    __syncthreads();
+    if (threadIdx.x == 255) carry = x;
+    __syncthreads();
+  }
+}
+
+// 4. seg[t * K + q] = first index of push q in tile t: 0 (t = 0),
+// lower_bound(push q, split[t - 1]) (0 < t < T), n_q (t = T)
+__global__ __launch_bounds__(256) void nw_seg_kernel(NwArgs a) {
+  const uint64_t id = (uint64_t)blockIdx.x * 256u + threadIdx.x;
+  const uint64_t tot = (uint64_t)(a.T + 1) * a.K;
+  if (id >= tot) return;
+  const uint32_t t = (uint32_t)(id / a.K), q = (uint32_t)(id - (uint64_t)t * a.K);
+  uint64_t v;
+  if (t == 0) v = 0;
+  else if (t == a.T) v = a.n[q];
+  else v = lb_global(a.keys[q], a.n[q], a.split[t - 1]);
+  a.seg[id] = (uint32_t)v;
+}
+
+constexpr uint64_t kFlagAgg = 1ull << 62, kFlagPre = 2ull << 62;
+constexpr uint64_t kValMask = (1ull << 62) - 1;
+
+// 5. the tile merge
+template <typename V, int M>
+__global__ __launch_bounds__(kNT) void nw_tile_kernel(NwArgs a) {
+  constexpr int kM = M > 0 ? M : 1;
+  constexpr int kVC = M > 0 ? kCap : 1;
+  __shared__ __attribute__((aligned(16))) uint64_t sk[kCap];  // keys (merged in place)
+  __shared__ uint16_t si[kCap];                               // source position of each key
+  __shared__ __attribute__((aligned(16))) V sv[kM][kVC];      // values by source position
+  __shared__ uint32_t roff[kMaxRuns + 1];                     // run offsets (never changed)
+  __shared__ uint32_t pstart[kMaxRuns];                       // piece start in its push
+  __shared__ uint32_t wsum[kNT / 64];
+  __shared__ uint32_t sh_t, sh_err;
+  __shared__ unsigned long long sh_base;
+  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+  const uint32_t K = a.K;
+  const bool parallel = (a.flags & kFlagParallel) != 0;
+
+  // ---- ticket: tiles in dispatch order (the look-back waits only on
+  // tickets taken by workgroups that are already running)
+  if (tid == 0) {
+    sh_t = atomicAdd(a.ticket, 1u);
+    sh_err = 0;
+  }
+  __syncthreads();
+  const uint32_t t = sh_t;
+
+  // ---- piece table: wave 0, one lane per push
+  if (w == 0) {
+    uint32_t len = 0;
+    if ((uint32_t)lane < K) {
+      const uint32_t s0 = a.seg[(size_t)t * K + lane], s1 = a.seg[(size_t)(t + 1) * K + lane];
+      len = s1 > s0 ? s1 - s0 : 0u;
+      pstart[lane] = s0;
+    }
+    uint32_t x = len;
+#pragma unroll
+    for (int d = 1; d < 64; d <<= 1) {
+      const uint32_t y = __shfl_up(x, d, 64);
+      if (lane >= d) x += y;
+    }
+    if ((uint32_t)lane < K) roff[lane + 1] = x;
+    if (lane == 0) roff[0] = 0;
+    if (lane == 63 && x > (uint32_t)kCap) sh_err = 1;  // excluded by the splitters (header)
+  }
+  __syncthreads();
+  if (sh_err) {
+    // never expected: report, and merge nothing (an empty tile still
+    // publishes its count, so later tiles' look-back ends)
+    if (tid == 0) {
+      atomicAdd(a.bad, 1ull << 32);
+      roff[K] = 0;
+      for (uint32_t q = 0; q < K; ++q) roff[q] = 0;
+    }
+    __syncthreads();
+  }
+  const uint32_t E = uni(roff[K]);
+
+  // ---- load the pieces: keys, source positions, values
+  for (uint32_t q = 0; q < K; ++q) {
+    const uint32_t o = roff[q], len = roff[q + 1] - o;
+    const uint64_t* kp = a.keys[q] + pstart[q];
+    for (uint32_t e = tid; e < len; e += kNT) {
+      sk[o + e] = kp[e];
+      si[o + e] = (uint16_t)(o + e);
+#pragma unroll
+      for (int mi = 0; mi < M; ++mi)
+        sv[mi][o + e] = ((const V*)a.vals[(size_t)q * M + mi] + pstart[q])[e];
+    }
+  }
+  __syncthreads();
+  // order check: each piece strictly increasing and inside the tile's key
+  // range [split[t-1], split[t]), so the pieces concatenate to the sorted
+  // pushes (std::set_union's precondition)
+  uint32_t viol = 0;
+  {
+    const uint64_t klo = t > 0 ? a.split[t - 1] : 0ull;
+    const bool open = t + 1 >= a.T;
+    const uint64_t khi = open ? ~0ull : a.split[t];
+    for (uint32_t q = 0; q < K; ++q) {
+      const uint32_t o = roff[q], len = roff[q + 1] - o;
+      for (uint32_t e = tid; e < len; e += kNT) {
+        const uint64_t k = sk[o + e];
+        const bool ok = k >= klo && (open || k < khi) && (e == 0 || sk[o + e - 1] < k);
+        viol += ok ? 0u : 1u;
+      }
+    }
+  }
+
+  // ---- merge-path tree: round `width` merges runs [r0, r0 + width) and
+  // [r0 + width, r0 + 2 width) (original run indices; the offsets of merged
+  // runs are original run offsets); stable, so equal keys keep push order
+  const uint32_t k0 = (uint32_t)tid * kPer;
+  for (uint32_t width = 1; width < K; width <<= 1) {
+    uint64_t rk[kPer];
+    uint16_t ri[kPer];
+    uint32_t A0 = 0, B0 = 0, B1 = 0, i = 0, j = 0;  // current pair and merge position
+#pragma unroll
+    for (int x = 0; x < kPer; ++x) {
+      const uint32_t k = k0 + x;
+      rk[x] = 0;
+      ri[x] = 0;
+      if (k < E) {
+        if (x == 0 || k >= B1) {
+          // the pair whose merged region holds k, and the merge path there
+          uint32_t r0 = 0;
+          while (r0 + 2 * width < K && roff[r0 + 2 * width] <= k) r0 += 2 * width;
+          const uint32_t r1 = r0 + width < K ? r0 + width : K;
+          const uint32_t r2 = r0 + 2 * width < K ? r0 + 2 * width : K;
+          A0 = roff[r0];
+          B0 = roff[r1];
+          B1 = roff[r2];
+          const uint32_t la = B0 - A0, lb = B1 - B0, d = k - A0;
+          uint32_t lo = d > lb ? d - lb : 0u, hi = d < la ? d : la;
+          while (lo < hi) {  // A elements among the first d outputs
+            const uint32_t mid = (lo + hi) >> 1;
+            if (sk[A0 + mid] <= sk[B0 + d - mid - 1]) lo = mid + 1;
+            else hi = mid;
+          }
+          i = lo;
+          j = d - lo;
+        }
+        const uint32_t la = B0 - A0, lb = B1 - B0;
+        const bool takeA = j >= lb || (i < la && sk[A0 + i] <= sk[B0 + j]);
+        const uint32_t src = takeA ? A0 + i : B0 + j;
+        rk[x] = sk[src];
+        ri[x] = si[src];
+        i += takeA ? 1u : 0u;
+        j += takeA ? 0u : 1u;
+      }
+    }
+    __syncthreads();
+#pragma unroll
+    for (int x = 0; x < kPer; ++x)
+      if (k0 + x < E) {
+        sk[k0 + x] = rk[x];
+        si[k0 + x] = ri[x];
+      }
+    __syncthreads();
+  }
+
+  // ---- run heads (a key differing from the previous one), unique index
+  uint32_t heads = 0, nh = 0;
+#pragma unroll
+  for (int x = 0; x < kPer; ++x) {
+    const uint32_t e = k0 + x;
+    if (e < E && (e == 0 || sk[e] != sk[e - 1])) {
+      heads |= 1u << x;
+      ++nh;
+    }
+  }
+  uint32_t incl = nh;
+#pragma unroll
+  for (int d = 1; d < 64; d <<= 1) {
+    const uint32_t y = __shfl_up(incl, d, 64);
+    if (lane >= d) incl += y;
+  }
+  if (lane == 63) wsum[w] = incl;
+  for (int d = 32; d > 0; d >>= 1) viol += __shfl_xor(viol, d, 64);
+  if (lane == 0 && viol) atomicAdd(a.bad, (unsigned long long)viol);
+  __syncthreads();
+  uint32_t U = 0, first_u = incl - nh;
+#pragma unroll
+  for (int v = 0; v < kNT / 64; ++v) {
+    first_u += v < w ? wsum[v] : 0u;
+    U += wsum[v];
+  }
+
+  // ---- decoupled look-back (wave 0): this tile's global offset
+  if (w == 0) {
+    unsigned long long excl = 0;
+    if (t > 0) {
+      if (lane == 0)
+        __hip_atomic_store(a.state + t, kFlagAgg | (unsigned long long)U, __ATOMIC_RELAXED,
+                           __HIP_MEMORY_SCOPE_AGENT);
+      int64_t j = (int64_t)t - 1;
+      uint32_t spins = 0;
+      for (;;) {
+        const int64_t idx = j - lane;  // lane 0: the nearest predecessor
+        const unsigned long long s =
+            idx >= 0 ? __hip_atomic_load(a.state + idx, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)
+                     : kFlagPre;  // before tile 0: an inclusive prefix of 0
+        const unsigned long long fl = s & ~kValMask;
+        const unsigned long long pm = __ballot(fl == kFlagPre);
+        const unsigned long long inv = __ballot(fl == 0);
+        const int fp = pm ? __ffsll((long long)pm) - 1 : 64;
+        const unsigned long long upto = fp >= 63 ? ~0ull : ((2ull << fp) - 1);  // lanes 0..fp
+        if (inv & upto) {  // a predecessor has not published yet
+          if (++spins > (1u << 22)) {  // never expected: report and stop waiting
+            if (lane == 0) atomicAdd(a.bad, 1ull << 40);
+            break;
+          }
+          __builtin_amdgcn_s_sleep(2);
+          continue;
+        }
+        unsigned long long v = ((upto >> lane) & 1ull) ? (s & kValMask) : 0ull;
+        for (int d = 32; d > 0; d >>= 1) v += __shfl_xor(v, d, 64);
+        excl += v;
+        if (fp < 64) break;
+        j -= 64;
+      }
+    }
+    if (lane == 0) {
+      __hip_atomic_store(a.state + t, kFlagPre | (excl + U), __ATOMIC_RELAXED,
+                         __HIP_MEMORY_SCOPE_AGENT);
+      if (t + 1 == a.T) *a.nout = excl + U;
+      sh_base = excl;
+    }
+  }
+
+  // ---- segmented sums of this thread's runs, in push order
+  uint64_t hk[kPer];
+  V hs[kPer][kM];
+#pragma unroll
+  for (int x = 0; x < kPer; ++x) {
+    hk[x] = 0;
+#pragma unroll
+    for (int mi = 0; mi < kM; ++mi) hs[x][mi] = V(0);
+    if ((heads >> x) & 1u) {
+      const uint32_t e = k0 + x;
+      const uint64_t key = sk[e];
+      hk[x] = key;
+      if constexpr (M > 0) {
+        // the run [e, f): push 0 (run 0's sources) assigns, later pushes
+        // add to the memset +0.0 or to it; serial: one trailing +0.0 when
+        // a push lacked the key (kv_vector.h:195-201)
+        V acc[M];
+#pragma unroll
+        for (int mi = 0; mi < M; ++mi) acc[mi] = V(0);
+        const uint32_t p0 = roff[1];
+        uint32_t f = e, cnt = 0;
+        while (f < E && sk[f] == key) {
+          const uint32_t src = si[f];
+#pragma unroll
+          for (int mi = 0; mi < M; ++mi) acc[mi] = src < p0 ? sv[mi][src] : acc[mi] + sv[mi][src];
+          ++cnt;
+          ++f;
+        }
+#pragma unroll
+        for (int mi = 0; mi < M; ++mi)
+          hs[x][mi] = (!parallel && cnt < K) ? acc[mi] + V(0) : acc[mi];
+      }
+    }
+  }
+  __syncthreads();  // every read of sk / si / sv is done; sh_base is set
+  // compacted: unique u of the tile at LDS position u
+  {
+    uint32_t u = first_u;
+#pragma unroll
+    for (int x = 0; x < kPer; ++x) {
+      if ((heads >> x) & 1u) {
+        sk[u] = hk[x];
+#pragma unroll
+        for (int mi = 0; mi < M; ++mi) sv[mi][u] = hs[x][mi];
+        ++u;
+      }
+    }
+  }
+  __syncthreads();
+  const unsigned long long base = sh_base;
+  for (uint32_t e = tid; e < U; e += kNT) {
+    a.out_keys[base + e] = sk[e];
+#pragma unroll
+    for (int mi = 0; mi < M; ++mi) ((V*)a.out_vals[mi])[base + e] = sv[mi][e];
+  }
+}
+
+template <typename V, int M>
+hipError_t launch_tile(const NwArgs& a, hipStream_t s) {
+  hipLaunchKernelGGL((nw_tile_kernel<V, M>), dim3(a.T), dim3(kNT), 0, s, a);
+  return hipGetLastError();
+}
+
+template <typename V>
+hipError_t launch_tile_m(int m, const NwArgs& a, hipStream_t s) {
+  switch (m) {
+    case 0: return launch_tile<V, 0>(a, s);
+    case 1: return launch_tile<V, 1>(a, s);
+    case 2: return launch_tile<V, 2>(a, s);
+    case 3: return launch_tile<V, 3>(a, s);
+    case 4: return launch_tile<V, 4>(a, s);
+    default: return hipErrorInvalidValue;
+  }
+}
+
+size_t al256(size_t x) { return (x + 255) / 256 * 256; }
+
+}  // namespace
+
+// Layout of one merge's device scratch (tables, per-run cleared region,
+// piece starts) for K non-empty pushes of ntot keys, m value arrays.
+struct NwLayout {
+  uint32_t K = 0, s = 1, cw = 1, B = 1, T = 2;
+  uint64_t ncand = 0;
+  size_t o_k = 0, o_v = 0, o_n = 0, o_cb = 0, o_ov = 0, o_zero = 0, o_rank = 0, o_split = 0,
+         o_state = 0, o_misc = 0, zero_len = 0, o_seg = 0, bytes = 0;
+  std::vector<uint64_t> cbase;
+
+  void plan(uint32_t k, const uint64_t* pn, int m) {
+    K = k;
+    uint64_t ntot = 0;
+    for (uint32_t q = 0; q < K; ++q) ntot += pn[q];
+    // sample stride s and bucket width C' (header: a tile holds <= C' + K s)
+    s = K <= 16 ? std::max<uint32_t>(1, kCap / (8 * std::max<uint32_t>(K, 1))) : 16u;
+    cw = kCap - K * s - K;
+    cbase.assign(K + 1, 0);
+    for (uint32_t q = 0; q < K; ++q) cbase[q + 1] = cbase[q] + pn[q] / s;
+    ncand = cbase[K];
+    B = (uint32_t)(ntot / cw + 1);
+    T = B + 1;
+    size_t off = 0;
+    o_k = off; off = al256(off + 8 * K);
+    o_v = off; off = al256(off + 8 * (size_t)K * m);
+    o_n = off; off = al256(off + 8 * K);
+    o_cb = off; off = al256(off + 8 * (K + 1));
+    o_ov = off; off = al256(off + 8 * (size_t)std::max(m, 1));
+    o_zero = off;
+    o_rank = off; off = al256(off + 4 * ncand);
+    o_split = off; off = al256(off + 8 * (size_t)B);
+    o_state = off; off = al256(off + 8 * (size_t)T);
+    o_misc = off; off = al256(off + 32);  // ticket, bad, nout
+    zero_len = off - o_zero;
+    o_seg = off; off = al256(off + 4 * (size_t)(T + 1) * K);
+    bytes = off;
+  }
+
+  NwArgs args(char* b, uint64_t* out_keys, uint32_t flags) const {
+    NwArgs A{};
+    A.keys = (const uint64_t* const*)(b + o_k);
+    A.vals = (const void* const*)(b + o_v);
+    A.n = (const uint64_t*)(b + o_n);
+    A.cbase = (const uint64_t*)(b + o_cb);
+    A.out_vals = (void* const*)(b + o_ov);
+    A.rank = (uint32_t*)(b + o_rank);
+    A.split = (uint64_t*)(b + o_split);
+    A.state = (unsigned long long*)(b + o_state);
+    A.ticket = (unsigned int*)(b + o_misc);
+    A.bad = (unsigned long long*)(b + o_misc + 8);
+    A.nout = (unsigned long long*)(b + o_misc + 16);
+    A.seg = (uint32_t*)(b + o_seg);
+    A.out_keys = out_keys;
+    A.ncand = ncand;
+    A.K = K;
+    A.B = B;
+    A.T = T;
+    A.s = s;
+    A.cw = cw;
+    A.flags = flags;
+    return A;
+  }
+
+  // the tables (pointer arrays, lengths, candidate bases) into the scratch
+  hipError_t upload(char* b, const uint64_t* const* pk, const void* const* pv, const uint64_t* pn,
+                    const void* const* ov, int m, hipStream_t st, bool sync) const {
+    std::vector<char> h(o_zero);
+    if (K) memcpy(h.data() + o_k, pk, 8 * K);
+    if (K && m) memcpy(h.data() + o_v, pv, 8 * (size_t)K * m);
+    if (K) memcpy(h.data() + o_n, pn, 8 * K);
+    memcpy(h.data() + o_cb, cbase.data(), 8 * (K + 1));
+    if (m) memcpy(h.data() + o_ov, ov, 8 * (size_t)m);
+    hipError_t e = hipMemcpyAsync(b, h.data(), o_zero, hipMemcpyHostToDevice, st);
+    // the host vector is freed on return: wait for the copy
+    if (e == hipSuccess) e = hipStreamSynchronize(st);
+    (void)sync;
+    return e;
+  }
+};
+
+hipError_t nway_enqueue(const NwArgs& A, char* b, const NwLayout& L, int dtype, int m,
+                        hipStream_t st) {
+  hipError_t e = hipMemsetAsync(b + L.o_zero, 0, L.zero_len, st);
+  if (e != hipSuccess || A.K == 0) return e;
+  if (A.ncand) {
+    const uint64_t th = A.ncand * A.K;
+    hipLaunchKernelGGL(nw_cand_kernel, dim3((uint32_t)((th + 255) / 256)), dim3(256), 0, st, A);
+    hipLaunchKernelGGL(nw_bucket_kernel, dim3((uint32_t)((A.ncand + 255) / 256)), dim3(256), 0, st,
+                       A);
+  }
+  hipLaunchKernelGGL(nw_split_kernel, dim3(1), dim3(256), 0, st, A);
+  const uint64_t ns = (uint64_t)(A.T + 1) * A.K;
+  hipLaunchKernelGGL(nw_seg_kernel, dim3((uint32_t)((ns + 255) / 256)), dim3(256), 0, st, A);
+  if ((e = hipGetLastError()) != hipSuccess) return e;
+  return dtype == PSG_F32 ? launch_tile_m<float>(m, A, st) : launch_tile_m<double>(m, A, st);
+}
+
+// One keys-only union on `st` into out_keys (>= sum(n) entries), scratch
+// from the caller (>= nway_scratch_bytes): the context's key union
+// (psg_key_union*).  *d_bad / *d_nout: the device words psg_nway_result reads.
+size_t nway_scratch_bytes(uint32_t K, const uint64_t* pn) {
+  NwLayout L;
+  L.plan(K, pn, 0);
+  return L.bytes;
+}
+
+hipError_t nway_union_enqueue(uint32_t K, const uint64_t* const* pk, const uint64_t* pn,
+                              uint64_t* out_keys, void* scratch, unsigned long long** d_bad,
+                              hipStream_t st) {
+  NwLayout L;
+  L.plan(K, pn, 0);
+  char* b = (char*)scratch;
+  hipError_t e = L.upload(b, pk, nullptr, pn, nullptr, 0, st, true);
+  if (e != hipSuccess) return e;
+  const NwArgs A = L.args(b, out_keys, 0);
+  *d_bad = A.bad;  // [bad, nout]
+  return nway_enqueue(A, b, L, PSG_F32, 0, st);
+}
+
+}  // namespace psg
+
+using psg::fail;
+
+struct psg_nway {
+  int device = 0, dtype = 0, m = 0;
+  uint64_t ntot = 0;              // keys over all pushes
+  uint64_t bytes = 0;             // algorithmic bytes read by a run
+  void* blob = nullptr;
+  psg::NwLayout layout;
+  psg::NwArgs args{};
+  hipStream_t last = nullptr;
+};
+
+extern "C" {
+
+int psg_nway_max_push(void) { return psg::kMaxRuns; }
+
+int psg_nway_create(int device, int dtype, int m, unsigned flags, int npush,
+                    const uint64_t* const* keys, const uint64_t* n, const void* const* vals,
+                    uint64_t* out_keys, void* const* out_vals, psg_nway** out) {
+  using namespace psg;
+  if (!out || npush < 0 || (npush && (!keys || !n)) || !out_keys)
+    return fail(PSG_ERR_ARG, "null argument");
+  if (dtype != PSG_F32 && dtype != PSG_F64) return fail(PSG_ERR_ARG, "dtype %d", dtype);
+  if (m < 0 || m > PSG_MAX_VALUE_ARRAYS || (m > 0 && (!vals || !out_vals)))
+    return fail(PSG_ERR_ARG, "m=%d", m);
+  HIP_TRY(hipSetDevice(device));
+  // empty pushes are ignored (kv_vector.h:90,177): push 0 is the first non-empty one
+  std::vector<const uint64_t*> pk;
+  std::vector<const void*> pv;
+  std::vector<uint64_t> pn;
+  uint64_t ntot = 0;
+  for (int p = 0; p < npush; ++p) {
+    if (n[p] == 0) continue;
+    if (!keys[p]) return fail(PSG_ERR_ARG, "push %d: null keys", p);
+    pk.push_back(keys[p]);
+    for (int i = 0; i < m; ++i) {
+      if (!vals[(size_t)p * m + i]) return fail(PSG_ERR_ARG, "push %d: null values", p);
+      pv.push_back(vals[(size_t)p * m + i]);
+    }
+    pn.push_back(n[p]);
+    ntot += n[p];
+  }
+  const uint32_t K = (uint32_t)pk.size();
+  if (K > (uint32_t)kMaxRuns) return fail(PSG_ERR_ARG, "%u pushes > %d per merge", K, kMaxRuns);
+  if (ntot >= (1ull << 32)) return fail(PSG_ERR_ARG, "%llu keys >= 2^32", (unsigned long long)ntot);
+  psg_nway* u = new psg_nway();
+  u->device = device;
+  u->dtype = dtype;
+  u->m = m;
+  u->ntot = ntot;
+  u->layout.plan(K, pn.data(), m);
+  if (hipMalloc(&u->blob, u->layout.bytes) != hipSuccess) {
+    delete u;
+    return fail(PSG_ERR_OOM, "nway: %zu bytes", u->layout.bytes);
+  }
+  const hipError_t e = u->layout.upload((char*)u->blob, pk.data(), pv.data(), pn.data(),
+                                        (const void* const*)out_vals, m, nullptr, true);
+  if (e != hipSuccess) {
+    (void)hipFree(u->blob);
+    delete u;
+    return fail(PSG_ERR_DEVICE, "nway set-up: %s", hipGetErrorString(e));
+  }
+  u->args = u->layout.args((char*)u->blob, out_keys,
+                           (flags & PSG_PARALLEL_MATCH) ? kFlagParallel : 0u);
+  // SURVEY 8d general form, the read side: every push's keys and values
+  // (the merged output adds |union| * (8 + m s_V), known after a run)
+  u->bytes = ntot * (8 + (uint64_t)m * (dtype == PSG_F32 ? 4 : 8));
+  *out = u;
+  return PSG_OK;
+}
+
+int psg_nway_run(psg_nway* u, void* stream) {
+  if (!u) return fail(PSG_ERR_ARG, "null merge");
+  HIP_TRY(hipSetDevice(u->device));
+  hipStream_t st = (hipStream_t)stream;
+  u->last = st;
+  HIP_TRY(psg::nway_enqueue(u->args, (char*)u->blob, u->layout, u->dtype, u->m, st));
+  return PSG_OK;
+}
+
+int psg_nway_count_dev(psg_nway* u, unsigned long long** nout) {
+  if (!u || !nout) return fail(PSG_ERR_ARG, "null argument");
+  *nout = u->args.nout;
+  return PSG_OK;
+}
+
+int psg_nway_result(psg_nway* u, uint64_t* nout) {
+  if (!u) return fail(PSG_ERR_ARG, "null merge");
+  HIP_TRY(hipSetDevice(u->device));
+  if (u->last) HIP_TRY(hipStreamSynchronize(u->last));
+  unsigned long long h[2] = {0, 0};
+  HIP_TRY(hipMemcpy(h, u->args.bad, 16, hipMemcpyDeviceToHost));  // bad, nout
+  if (nout) *nout = h[1];
+  if (h[0] >> 32)
+    return fail(PSG_ERR_DEVICE, "nway: tile overflow / look-back timeout (%llx)", h[0]);
+  if (h[0])
+    return fail(PSG_ERR_UNSORTED, "nway: %llu keys out of order (pushes must be strictly "
+                "increasing)", h[0]);
+  return PSG_OK;
+}
+
+int psg_nway_bytes(psg_nway* u, uint64_t* bytes, uint64_t* kv) {
+  if (!u) return fail(PSG_ERR_ARG, "null merge");
+  if (bytes) *bytes = u->bytes;
+  if (kv) *kv = u->ntot;
+  return PSG_OK;
+}
+
+int psg_nway_destroy(psg_nway* u) {
+  if (!u) return PSG_OK;
+  (void)hipSetDevice(u->device);
+  if (u->last) (void)hipStreamSynchronize(u->last);
+  (void)hipFree(u->blob);
+  delete u;
+  return PSG_OK;
+}
+
+}  // extern "C"

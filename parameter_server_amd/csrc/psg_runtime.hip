@@ -515,7 +515,20 @@ using KeyRef = std::shared_ptr<KeyBuf>;
 struct Channel {
   uint64_t* d_keys = nullptr;
   size_t n = 0, kbytes = 0;
-  std::vector<uint64_t> h_keys;  // host mirror of key_[chl] (findRange)
+  // host mirror of key_[chl] (findRange, key copies, psg_push's dense
+  // test): after a key union the device key set is copied into pinned
+  // memory asynchronously; readers wait for that copy (mirror())
+  uint64_t* hk = nullptr;
+  size_t hcap = 0;
+  hipEvent_t hev = nullptr;
+  bool hpend = false;
+  const uint64_t* mirror() {
+    if (hpend) {
+      (void)hipEventSynchronize(hev);
+      hpend = false;
+    }
+    return hk;
+  }
   void* d_vals = nullptr;
   size_t nvals = 0;
   // Darling server state (darling.h:38-39): delta_[grp], active_set_[grp]
@@ -1018,24 +1031,24 @@ int psg_gather_dev(int dtype, const uint64_t* dkeys, uint64_t nd,
 int psg_key_union_dev(const uint64_t* a, uint64_t na, const uint64_t* b,
                       uint64_t nb, uint64_t* out, uint64_t* nout, void* stream) {
   if (!out || !nout || (na && !a) || (nb && !b)) return fail(PSG_ERR_ARG, "null");
-  if (nb >= (1ull << 32)) return fail(PSG_ERR_ARG, "nb >= 2^32");
+  if (na + nb >= (1ull << 32)) return fail(PSG_ERR_ARG, "na + nb >= 2^32");
   hipStream_t s = (hipStream_t)stream;
+  std::vector<const uint64_t*> pk;
+  std::vector<uint64_t> pn;
+  if (na) { pk.push_back(a); pn.push_back(na); }
+  if (nb) { pk.push_back(b); pn.push_back(nb); }
   void* scratch = nullptr;
-  unsigned long long* bad = nullptr;
-  const size_t sb = psg::union_scratch_bytes(nb);
-  HIP_TRY(hipMalloc(&scratch, sb + 64));
-  uint64_t* d_nout = (uint64_t*)((char*)scratch + align_up(sb, 16));
-  bad = (unsigned long long*)(d_nout + 1);
-  HIP_TRY(hipMemsetAsync(bad, 0, 16, s));
-  HIP_TRY(psg::launch_check_sorted(a, na, bad, s));
-  HIP_TRY(psg::launch_check_sorted(b, nb, bad, s));
-  HIP_TRY(psg::launch_union(a, na, b, nb, out, scratch, d_nout, s));
+  HIP_TRY(hipMalloc(&scratch, psg::nway_scratch_bytes((uint32_t)pk.size(), pn.data())));
+  unsigned long long* d_bad = nullptr;
   unsigned long long h[2] = {0, 0};
-  HIP_TRY(hipMemcpyAsync(h, d_nout, 16, hipMemcpyDeviceToHost, s));
-  HIP_TRY(hipStreamSynchronize(s));
-  HIP_TRY(hipFree(scratch));
-  if (h[1]) return fail(PSG_ERR_UNSORTED, "%llu order violations", h[1]);
-  *nout = h[0];
+  hipError_t e = psg::nway_union_enqueue((uint32_t)pk.size(), pk.data(), pn.data(), out, scratch,
+                                         &d_bad, s);
+  if (e == hipSuccess) e = hipMemcpyAsync(h, d_bad, 16, hipMemcpyDeviceToHost, s);
+  if (e == hipSuccess) e = hipStreamSynchronize(s);
+  (void)hipFree(scratch);
+  if (e != hipSuccess) return fail(PSG_ERR_DEVICE, "key union: %s", hipGetErrorString(e));
+  if (h[0]) return fail(PSG_ERR_UNSORTED, "%llu order violations", h[0]);
+  *nout = h[1];
   return PSG_OK;
 }
 
@@ -1128,6 +1141,9 @@ int psg_destroy(psg_ctx* c) {
     c->dev_put(kv.second.d_vals, kv.second.nvals * vsize(c->dtype));
     c->dev_put(kv.second.d_delta, 8 * kv.second.dn);
     c->dev_put(kv.second.d_active, 4 * ((kv.second.dn + 31) / 32));
+    (void)kv.second.mirror();
+    if (kv.second.hk) (void)hipHostFree(kv.second.hk);
+    if (kv.second.hev) (void)hipEventDestroy(kv.second.hev);
   }
   c->ch.clear();
   for (auto& kv : c->ff) c->dev_put(kv.second.d_table, 4 * (size_t)kv.second.n);
@@ -1168,10 +1184,32 @@ int psg_set_flush_pushes(psg_ctx* c, int n) {
 
 namespace {
 
-// key_[chl] = key_[chl].setUnion(keys); val_[chl].clear()  (kv_vector.h:
-// 177-182).  `keys` (host, n > 0) is merged into the host mirror on the CPU
-// and `d_new` (the same keys, resident) into the device key set.
-int key_union_impl(psg_ctx* c, int chl, const uint64_t* keys, size_t n, uint64_t* d_new) {
+// The host mirror of a changed key set: one asynchronous device-to-host copy
+// into pinned memory on `stream`, waited for by the first reader.
+int refresh_mirror(psg_ctx* c, Channel& C) {
+  (void)C.mirror();  // the previous copy may still target the buffer
+  if (C.n > C.hcap) {
+    if (C.hk) HIP_TRY(hipHostFree(C.hk));
+    C.hk = nullptr;
+    C.hcap = 0;
+    const size_t cap = std::max(C.n, C.n + C.n / 2);
+    HIP_TRY(hipHostMalloc((void**)&C.hk, 8 * cap));
+    C.hcap = cap;
+  }
+  if (!C.hev) HIP_TRY(hipEventCreateWithFlags(&C.hev, hipEventDisableTiming));
+  if (C.n) HIP_TRY(hipMemcpyAsync(C.hk, C.d_keys, 8 * C.n, hipMemcpyDeviceToHost, c->stream));
+  HIP_TRY(hipEventRecord(C.hev, c->stream));
+  C.hpend = true;
+  return PSG_OK;
+}
+
+// key_[chl] = key_[chl].setUnion(keys_0).setUnion(keys_1)...; val_[chl].clear()
+// (kv_vector.h:177-182, shared_array_inl.h:155-162) for resident key-only
+// pushes d_push[i] (n[i] keys): one N-way merge on the device (psg_nway.hip)
+// of the server keys and up to 63 pushes at a time; the host mirror is then
+// refreshed from the device result by an asynchronous copy (no CPU union).
+int key_union_impl(psg_ctx* c, int chl, const std::vector<const uint64_t*>& d_push,
+                   const std::vector<uint64_t>& n) {
   Channel& C = c->ch[chl];
   // Pending value pushes of this channel were matched against the current
   // key_[chl] in the reference (setValue matches at arrival,
@@ -1182,35 +1220,54 @@ int key_union_impl(psg_ctx* c, int chl, const uint64_t* keys, size_t n, uint64_t
     if (kv.second.chl == chl && !kv.second.pending.empty())
       if (int rc = c->flush(kv.second)) return rc;
   if (int rc = c->join_copy()) return rc;
-  if (int rc = c->ensure_scratch(psg::union_scratch_bytes(n))) return rc;
-  uint64_t* d_out = nullptr;
-  if (int rc = c->dev_get(8 * (C.n + n), (void**)&d_out, c->stream)) return rc;
-  HIP_TRY(hipMemsetAsync(c->d_small, 0, 16, c->stream));
-  HIP_TRY(psg::launch_check_sorted(d_new, n, c->d_small, c->stream));
-  HIP_TRY(psg::launch_union(C.d_keys, C.n, d_new, n, d_out, c->scratch,
-                            (uint64_t*)(c->d_small + 1), c->stream));
-  HIP_TRY(hipMemcpyAsync(c->h_small, c->d_small, 16, hipMemcpyDeviceToHost, c->stream));
-  HIP_TRY(hipStreamSynchronize(c->stream));
-  const unsigned long long bad = c->h_small[0], nu = c->h_small[1];
-  if (bad) {
-    c->dev_put(d_out, 8 * (C.n + n));
-    return fail(PSG_ERR_UNSORTED, "key-only push: %llu order violations", bad);
+  bool changed = false;
+  for (size_t i = 0; i < d_push.size();) {
+    std::vector<const uint64_t*> pk;
+    std::vector<uint64_t> pn;
+    if (C.n) {
+      pk.push_back(C.d_keys);
+      pn.push_back(C.n);
+    }
+    const size_t base = pk.size();
+    for (; i < d_push.size() && pk.size() < (size_t)psg_nway_max_push(); ++i)
+      if (n[i]) {
+        pk.push_back(d_push[i]);
+        pn.push_back(n[i]);
+      }
+    if (pk.size() == base) continue;  // only empty pushes: ignored (kv_vector.h:177)
+    uint64_t cap = 0;
+    for (uint64_t x : pn) cap += x;
+    if (cap >= (1ull << 32)) return fail(PSG_ERR_ARG, "key union of %llu keys >= 2^32",
+                                         (unsigned long long)cap);
+    const uint32_t K = (uint32_t)pk.size();
+    if (int rc = c->ensure_scratch(psg::nway_scratch_bytes(K, pn.data()))) return rc;
+    uint64_t* d_out = nullptr;
+    if (int rc = c->dev_get(8 * cap, (void**)&d_out, c->stream)) return rc;
+    unsigned long long* d_bad = nullptr;
+    hipError_t e = psg::nway_union_enqueue(K, pk.data(), pn.data(), d_out, c->scratch, &d_bad,
+                                           c->stream);
+    if (e == hipSuccess)
+      e = hipMemcpyAsync(c->h_small, d_bad, 16, hipMemcpyDeviceToHost, c->stream);
+    if (e == hipSuccess) e = hipStreamSynchronize(c->stream);
+    if (e != hipSuccess) {
+      c->dev_put(d_out, 8 * cap);
+      return fail(PSG_ERR_DEVICE, "key union: %s", hipGetErrorString(e));
+    }
+    const unsigned long long bad = c->h_small[0], nu = c->h_small[1];
+    if (bad) {  // the pushes of this merge are not applied; earlier ones are
+      c->dev_put(d_out, 8 * cap);
+      if (changed) (void)refresh_mirror(c, C);
+      return fail(bad >> 32 ? PSG_ERR_DEVICE : PSG_ERR_UNSORTED,
+                  "key-only push: %llu order violations", bad);
+    }
+    c->dev_put(C.d_keys, C.kbytes);
+    C.d_keys = d_out;
+    C.kbytes = 8 * cap;
+    C.n = (size_t)nu;
+    changed = true;
   }
-  // the host mirror: the same union on the CPU from the caller's keys (no
-  // device-to-host copy of the key set)
-  std::vector<uint64_t> merged;
-  merged.reserve(C.n + n);
-  std::set_union(C.h_keys.begin(), C.h_keys.end(), keys, keys + n, std::back_inserter(merged));
-  if (merged.size() != nu) {
-    c->dev_put(d_out, 8 * (C.n + n));
-    return fail(PSG_ERR_DEVICE, "key union: device %llu keys, host mirror %zu", nu,
-                merged.size());
-  }
-  c->dev_put(C.d_keys, C.kbytes);
-  C.d_keys = d_out;
-  C.kbytes = 8 * (C.n + n);
-  C.n = (size_t)nu;
-  C.h_keys.swap(merged);
+  if (!changed) return PSG_OK;
+  if (int rc = refresh_mirror(c, C)) return rc;
   // val_[chl].clear()  (kv_vector.h:180)
   c->dev_put(C.d_vals, C.nvals * vsize(c->dtype));
   C.d_vals = nullptr;
@@ -1227,9 +1284,10 @@ int check_push(psg_ctx* c, int chl, int time, uint64_t kb, uint64_t ke, size_t n
   auto cit = c->ch.find(chl);
   if (cit == c->ch.end() || cit->second.n == 0)
     return fail(PSG_ERR_EMPTY_KEYS, "channel %d has no server keys", chl);
-  const Channel& C = cit->second;
-  *lo = std::lower_bound(C.h_keys.begin(), C.h_keys.end(), kb) - C.h_keys.begin();
-  *hi = std::lower_bound(C.h_keys.begin(), C.h_keys.end(), ke) - C.h_keys.begin();
+  Channel& C = cit->second;
+  const uint64_t* h = C.mirror();
+  *lo = std::lower_bound(h, h + C.n, kb) - h;
+  *hi = std::lower_bound(h, h + C.n, ke) - h;
   if (*hi - *lo < n)  // pigeonhole: some key cannot match (CHECK_GE, kv_vector.h:121,191)
     return fail(PSG_ERR_UNMATCHED, "push of %zu keys into a range of %zu server keys", n,
                 *hi - *lo);
@@ -1255,9 +1313,10 @@ int psg_ctx::push_values(int chl, int time, uint64_t kb, uint64_t ke, const KeyR
   auto ait = agg.find(time);
   {
     // (re-derived: the caller checked before staging the keys)
-    const Channel& C = ch[chl];
-    lo = std::lower_bound(C.h_keys.begin(), C.h_keys.end(), kb) - C.h_keys.begin();
-    hi = std::lower_bound(C.h_keys.begin(), C.h_keys.end(), ke) - C.h_keys.begin();
+    Channel& C = ch[chl];
+    const uint64_t* h = C.mirror();
+    lo = std::lower_bound(h, h + C.n, kb) - h;
+    hi = std::lower_bound(h, h + C.n, ke) - h;
   }
   const size_t sv = vsize(dtype), n = keys->n;
   PendingPush pp;
@@ -1313,7 +1372,34 @@ int psg_key_union(psg_ctx* c, int chl, const uint64_t* keys, size_t n) {
   KeyRef k;
   if (int rc = c->new_keys(n, &k)) return rc;
   int rc = c->h2d(k->d, keys, 8 * n);
-  if (rc == PSG_OK) rc = key_union_impl(c, chl, keys, n, k->d);
+  if (rc == PSG_OK) rc = key_union_impl(c, chl, {k->d}, {(uint64_t)n});
+  const int rf = c->h2d_finish();
+  return rc ? rc : rf;
+}
+
+int psg_key_union_batch(psg_ctx* c, int chl, const uint64_t* const* keys, const size_t* n,
+                        int npush) {
+  if (!c || npush < 0 || (npush && (!keys || !n))) return fail(PSG_ERR_ARG, "null argument");
+  for (int p = 0; p < npush; ++p)
+    if (n[p] && !keys[p]) return fail(PSG_ERR_ARG, "push %d: null keys", p);
+  std::lock_guard<std::mutex> l(c->mu);
+  if (int rc = set_dev(c->device)) return rc;
+  std::vector<KeyRef> staged;
+  std::vector<const uint64_t*> dp;
+  std::vector<uint64_t> dn;
+  int rc = PSG_OK;
+  for (int p = 0; rc == PSG_OK && p < npush; ++p) {
+    if (!n[p]) continue;
+    KeyRef k;
+    rc = c->new_keys(n[p], &k);
+    if (rc == PSG_OK) rc = c->h2d(k->d, keys[p], 8 * n[p]);
+    if (rc == PSG_OK) {
+      staged.push_back(k);
+      dp.push_back(k->d);
+      dn.push_back(n[p]);
+    }
+  }
+  if (rc == PSG_OK && !dp.empty()) rc = key_union_impl(c, chl, dp, dn);
   const int rf = c->h2d_finish();
   return rc ? rc : rf;
 }
@@ -1332,7 +1418,7 @@ int psg_key_copy(psg_ctx* c, int chl, size_t off, size_t n, uint64_t* out) {
   auto it = c->ch.find(chl);
   const size_t have = it == c->ch.end() ? 0 : it->second.n;
   if (off + n > have) return fail(PSG_ERR_ARG, "key copy out of range");
-  if (n) memcpy(out, it->second.h_keys.data() + off, 8 * n);
+  if (n) memcpy(out, it->second.mirror() + off, 8 * n);
   return PSG_OK;
 }
 
@@ -1346,9 +1432,9 @@ int psg_find_range(psg_ctx* c, int chl, uint64_t kb, uint64_t ke, size_t* lo,
     *lo = *hi = 0;
     return PSG_OK;
   }
-  const auto& k = it->second.h_keys;
-  *lo = std::lower_bound(k.begin(), k.end(), kb) - k.begin();
-  *hi = std::lower_bound(k.begin(), k.end(), ke) - k.begin();
+  const uint64_t* k = it->second.mirror();
+  *lo = std::lower_bound(k, k + it->second.n, kb) - k;
+  *hi = std::lower_bound(k, k + it->second.n, ke) - k;
   return PSG_OK;
 }
 
@@ -1417,8 +1503,8 @@ int psg_push(psg_ctx* c, int chl, int time, uint64_t kb, uint64_t ke,
   size_t a = 0;
   bool dense = false;
   if (n >= kDenseMinKeys) {
-    const std::vector<uint64_t>& h = c->ch[chl].h_keys;
-    a = std::lower_bound(h.begin() + lo, h.begin() + hi, keys[0]) - h.begin();
+    const uint64_t* h = c->ch[chl].mirror();
+    a = std::lower_bound(h + lo, h + hi, keys[0]) - h;
     dense = a + n <= hi && h[a] == keys[0] && h[a + n - 1] == keys[n - 1] &&
             h[a + n - 1] - h[a] == n - 1;
   }
@@ -1535,7 +1621,6 @@ int push_cached_impl(psg_ctx* c, int sender, int chl, int time, uint64_t kb, uin
   if (int rc = set_dev(c->device)) return rc;
   const CacheKey ck{sender, chl, kb, ke};
   KeyRef k;  // the message's keys, resident
-  std::vector<uint64_t> hk;  // host keys when the message carried them
   if (!(kc & PSG_KC_SIG)) {
     // no signature: the cache entry of (channel, range) is dropped
     // (remote_node.cc:143-156) and the message's own keys are used
@@ -1578,17 +1663,9 @@ int push_cached_impl(psg_ctx* c, int sender, int chl, int time, uint64_t kb, uin
   if (kc & PSG_KC_ERASE) c->kcache.erase(ck);  // remote_node.cc:183
   const size_t n = k ? k->n : 0;
   if (n == 0) return PSG_OK;  // kv_vector.h:90,177: no keys, message ignored
-  if (m == 0 || nvals == 0) {
-    // key-only message: setUnion with the (possibly restored) keys
-    hk.resize(n);
-    if ((kc & PSG_KC_KEYS) && keys) {
-      memcpy(hk.data(), keys, 8 * n);
-    } else {
-      if (int rc = c->join_copy()) return rc;
-      HIP_TRY(hipMemcpyAsync(hk.data(), k->d, 8 * n, hipMemcpyDeviceToHost, c->stream));
-      HIP_TRY(hipStreamSynchronize(c->stream));
-    }
-    return key_union_impl(c, chl, hk.data(), n, k->d);
+  if (m == 0) {
+    // key-only message: setUnion with the (possibly restored) keys, on the device
+    return key_union_impl(c, chl, {k->d}, {(uint64_t)n});
   }
   if (nvals != n)  // CHECK_EQ(recv_data.size(), recv_key.size()) kv_vector.h:108,187
     return fail(PSG_ERR_SIZE, "%zu values for %zu keys", nvals, n);

@@ -68,6 +68,15 @@ class KVVector:
         _lib.check(self._L.psg_create(device, dtype, flags, C.byref(h)))
         self._h = h
 
+    def union_keys(self, channel: int, key_lists) -> None:
+        """Several key-only pushes at once (psg_key_union_batch): the key set
+        setUnion of each in turn gives (kv_vector.h:177-182), merged on the
+        device in one N-way pass."""
+        ks = [np.ascontiguousarray(k, np.uint64) for k in key_lists]
+        arr = _lib.ptr_array([_ptr(k) if k.size else 0 for k in ks])
+        ns = (C.c_size_t * max(1, len(ks)))(*[k.size for k in ks])
+        _lib.check(self._L.psg_key_union_batch(self._h, channel, arr, ns, len(ks)))
+
     def set_flush_pushes(self, n: int) -> None:
         """Pushes merged per launch (launch seams; psg_set_flush_pushes)."""
         _lib.check(self._L.psg_set_flush_pushes(self._h, n))
@@ -253,6 +262,54 @@ class MergePlan:
     def close(self):
         if getattr(self, "_h", None):
             self._L.psg_plan_destroy(self._h)
+            self._h = None
+
+    def __del__(self):  # pragma: no cover
+        try:
+            self.close()
+        except Exception:
+            pass
+
+
+class NWayMerge:
+    """A prepared N-way merge (psg_nway_*): the union of sorted device
+    pushes and, with values, their per-key sums in arrival order.
+
+    push_keys / push_n: device pointers / lengths; push_vals: [[ptr] * m]
+    per push (m = 0: keys only); out_keys / out_vals: device pointers of
+    sum(n) entries each."""
+
+    def __init__(self, device: int, dtype: int, push_keys, push_n, push_vals, out_keys,
+                 out_vals=(), parallel_match: bool = False):
+        self._L = _lib.lib()
+        m = len(out_vals)
+        P = len(push_keys)
+        pk = _lib.ptr_array(push_keys)
+        pn = (C.c_uint64 * max(1, P))(*push_n)
+        pv = _lib.ptr_array([v for vs in push_vals for v in vs]) if m else None
+        ov = _lib.ptr_array(list(out_vals)) if m else None
+        self._keep = [pk, pn, pv, ov]
+        h = C.c_void_p()
+        flags = PSG_PARALLEL_MATCH if parallel_match else PSG_SERIAL_MATCH
+        _lib.check(self._L.psg_nway_create(device, dtype, m, flags, P, pk, pn, pv, out_keys, ov,
+                                           C.byref(h)))
+        self._h = h
+        b, kv = C.c_uint64(), C.c_uint64()
+        _lib.check(self._L.psg_nway_bytes(h, C.byref(b), C.byref(kv)))
+        self.bytes_in, self.kv_pairs = b.value, kv.value
+
+    def run(self, stream: Optional[int] = None) -> None:
+        _lib.check(self._L.psg_nway_run(self._h, stream or None))
+
+    def result(self) -> int:
+        """Synchronises; the merged key count (PSGError if a push was unsorted)."""
+        n = C.c_uint64()
+        _lib.check(self._L.psg_nway_result(self._h, C.byref(n)))
+        return n.value
+
+    def close(self):
+        if getattr(self, "_h", None):
+            self._L.psg_nway_destroy(self._h)
             self._h = None
 
     def __del__(self):  # pragma: no cover
