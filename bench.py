@@ -46,7 +46,7 @@ METRIC = "aggregated kv-pairs/s (device-resident), N-way sparse push merge at 1/
 
 WORKLOADS = {
     "cfg2": dict(batch=64, desc=(
-        "cfg2: {a.npush} pushes x {a.n} sorted unique uint64 keys + f32 values, 10% shared "
+        "cfg2: {a.npush} pushes x {a.n} sorted unique uint64 keys + {a.dtype} values, 10% shared "
         "keys (U={U:,}); {batch} such (channel,time) aggregates per GPU per step")),
     "cfg3": dict(batch=2, desc=(
         "cfg3 (CTR shape): 64 pushes x 131072 unique murmur-shuffled Zipf(1.1) ranks in "
@@ -62,7 +62,7 @@ WORKLOADS = {
 
 # the aggregate kernel each workload's plan runs (the runtime picks the form:
 # dense slices, short pieces -> packed rounds, > 32 pushes -> 64-push groups)
-KERNEL = {"cfg2": "tile_kernel<float,1,32>", "cfg3": "tile_kernel<float,1,64>",
+KERNEL = {"cfg2": "tile_kernel<float,1,32>", "cfg2_f64": "tile_kernel<double,1,32>", "cfg3": "tile_kernel<float,1,64>",
           "cfg4": "dense_kernel<float,1>", "cfg5": "tile_packed_kernel<float,1>"}
 
 
@@ -77,6 +77,9 @@ def parse():
     ap.add_argument("--n", type=int, default=131072)
     ap.add_argument("--overlap", type=float, default=0.1)
     ap.add_argument("--workload", choices=sorted(WORKLOADS), default="cfg2")
+    ap.add_argument("--dtype", choices=["f32", "f64"], default="f32",
+                    help="value type of a side line (the reference's apps use double, "
+                         "batch_solver.h:32); the headline is f32 (north star)")
     ap.add_argument("--no-cfg5", action="store_true",
                     help="skip the cfg5 strong-scaling block of the default line")
     ap.add_argument("--cfg5-steps", type=int, default=10)
@@ -111,20 +114,22 @@ def make_plan(insts, dev, local):
     """MergePlan over [(D, pushes)] resident on `dev`; returns (plan, keep, jobs)."""
     import torch
     from parameter_server_amd.kv_vector import MergePlan
-    from parameter_server_amd._lib import PSG_F32
+    from parameter_server_amd._lib import PSG_F32, PSG_F64
     keep, jobs = [], []
+    f64 = bool(insts) and insts[0][1][0][1][0].dtype == np.float64
     for D, pushes in insts:
         dD = to_dev(D, dev)
         pk = [to_dev(k, dev) for k, _ in pushes]
         pv = [[to_dev(v, dev) for v in vs] for _, vs in pushes]
-        out = torch.empty(max(1, D.size), dtype=torch.float32, device=dev)
+        out = torch.empty(max(1, D.size), dtype=torch.float64 if f64 else torch.float32,
+                          device=dev)
         keep.append((dD, pk, pv, out))
         jobs.append({"keys": dD.data_ptr(), "nslots": int(D.size),
                      "push_keys": [t.data_ptr() for t in pk],
                      "push_vals": [[t.data_ptr() for t in vs] for vs in pv],
                      "push_n": [int(k.size) for k, _ in pushes],
                      "out": [out.data_ptr()]})
-    plan = MergePlan(local, PSG_F32, 1, jobs, flags=PLAN_FLAGS)
+    plan = MergePlan(local, PSG_F64 if f64 else PSG_F32, 1, jobs, flags=PLAN_FLAGS)
     return plan, keep, jobs
 
 
@@ -188,9 +193,13 @@ def main():
     if wl != "cfg2" and world > 1:
         raise SystemExit("--workload cfg3/cfg4/cfg5 are single-GPU side lines; the default "
                          "line carries cfg5's multi-GPU strong-scaling block")
+    vdt = np.float64 if args.dtype == "f64" else np.float32
+    if args.dtype == "f64" and wl != "cfg2":
+        raise SystemExit("--dtype f64 is a cfg2 side line")
     if wl == "cfg2":
         insts = [synth.shard_instance(seed=1 + j + 1000 * rank, lo=lo, hi=hi,
-                                      npush=args.npush, n=args.n, overlap=args.overlap)
+                                      npush=args.npush, n=args.n, overlap=args.overlap,
+                                      dtype=vdt)
                  for j in range(args.batch)]
     elif wl == "cfg3":
         insts = [synth.zipf_pushes(seed=3 + j) for j in range(args.batch)]
@@ -226,12 +235,14 @@ def main():
     # roofline of the aggregate kernel: ALGORITHMIC bytes per launch (SURVEY
     # 8d) / its mean HIP-event duration; cfg4 is priced in the dense form
     U = sum(int(jb["nslots"]) for jb in jobs)
+    sv = 8 if args.dtype == "f64" else 4
     if wl == "cfg4":
         nbytes = int(plan.kv_pairs) * 4 + U * 4
         formula = "dense form: sum_p n_p*4 [push values] + U*4 [sums] (keys implied, SURVEY 8d)"
     else:
         nbytes = int(plan.bytes)
-        formula = "sum_p n_p*(8+4) [pushes] + U*(8+4) [server keys + sums] (SURVEY 8d)"
+        formula = (f"sum_p n_p*(8+{sv}) [pushes] + U*(8+{sv}) [server keys + sums] "
+                   "(SURVEY 8d)")
     achieved = nbytes / (agg_ms * 1e-3) / 1e9
     step_gbps = nbytes / (ms_per_step * 1e-3) / 1e9
     copy_gbps = copy_bandwidth(dev, stream)
@@ -248,7 +259,7 @@ def main():
         "higher_is_better": True,
         "scaling": "weak",
         "vs_baseline": None,
-        "dtype": "f32",
+        "dtype": args.dtype,
         "data": "synthetic",
         "config": {
             "workload": WORKLOADS[wl]["desc"].format(a=args, U=jobs[0]["nslots"] if jobs else 0,
@@ -265,7 +276,7 @@ def main():
             "unit": "GB/s",
             "frac": achieved / HBM_PEAK_GBPS,
             "traffic": traffic.get("tile") if traffic else None,
-            "kernel": KERNEL[wl],
+            "kernel": KERNEL[wl + ("_f64" if args.dtype == "f64" else "")],
             "bytes_per_launch": nbytes,
             "bytes_formula": formula,
             "kernel_ms": agg_ms,
@@ -278,11 +289,12 @@ def main():
             "frac_of_measured_copy": achieved / copy_gbps if copy_gbps else None,
         },
     }
-    if wl == "cfg2" and not args.no_cfg5:
+    if wl == "cfg2" and not args.no_cfg5 and args.dtype == "f32":
         del plan, keep
         torch.cuda.empty_cache()
         result["cfg5"] = cfg5_block(args, rank, world, bounds, dist, dev, local, stream)
-    if rank == 0 and world == 1 and not args.no_cpu_baseline and wl == "cfg2":
+    if rank == 0 and world == 1 and not args.no_cpu_baseline and wl == "cfg2" and \
+            args.dtype == "f32":
         result["end_to_end"] = end_to_end(insts[0], local)
         result["rows"] = bench_rows(local)
         result["cpu_baseline"] = cpu_baseline(insts[0], args.cpu_seconds)
@@ -624,13 +636,18 @@ def end_to_end(inst, device, reps=7):
 
 def load_traffic(bytes_per_launch, workload):
     """HBM bytes per launch of the aggregate and partition kernels from the
-    committed rocprofv3 PMC summary (profiles/pmc_summary.json, written by
-    tools/pmc_traffic.py), when it was collected on this same workload; else
-    null."""
-    p = os.path.join(ROOT, "profiles", "pmc_summary.json")
-    try:
-        d = json.load(open(p))
-    except Exception:
+    committed rocprofv3 PMC summary of this workload
+    (profiles/pmc_summary_<workload>.json, or profiles/pmc_summary.json for
+    cfg2; written by tools/pmc_traffic.py), when it was collected on this
+    same workload and size; else null."""
+    d = None
+    for name in (f"pmc_summary_{workload}.json", "pmc_summary.json"):
+        try:
+            d = json.load(open(os.path.join(ROOT, "profiles", name)))
+            break
+        except Exception:
+            continue
+    if d is None:
         return None
     if d.get("bytes_per_launch") != bytes_per_launch or d.get("workload", "cfg2") != workload:
         return None

@@ -290,6 +290,58 @@ DEFINE_MATCH(f64, double)
 DEFINE_AGGREGATE(f32, float)
 DEFINE_AGGREGATE(f64, double)
 
+/* parallelSetValue (kv_vector.h:84-137) restated in O(sum n log |D|) for
+ * large checks: match() (message.h:134-226) sets (ASSIGN, first push, after
+ * zero-filling the range, :182) or adds (ADD) src_val at the dst position of
+ * every src key that equals a dst key and touches no other position, so one
+ * push's effect is a scatter of its matched values; the merge walk skips an
+ * unmatched src key (matched < n) -- here a key that lower_bound does not
+ * find, or a repeated key, which the walk never revisits.  For
+ * non-decreasing pushes (unsorted ones take orc_aggregate); cross-checked
+ * against orc_aggregate (parallel) in tests/test_oracle.py. */
+#define DEFINE_AGGREGATE_SCATTER(SUF, V)                                       \
+  int orc_aggregate_scatter_##SUF(const uint64_t* D, size_t nD, uint64_t kb,  \
+                                  uint64_t ke, int npush,                      \
+                                  const uint64_t* const* keys, const size_t* n,\
+                                  int m, const V* const* vals, V* const* out,  \
+                                  size_t* lo, size_t* hi, size_t* matched) {   \
+    *lo = *hi = 0;                                                             \
+    int have = 0;                                                              \
+    for (int p = 0; p < npush; ++p) {                                          \
+      matched[p] = 0;                                                          \
+      if (n[p] == 0) continue;                                                 \
+      if (nD == 0) return -1;                                                  \
+      size_t plo, phi;                                                         \
+      orc_find_range_u64(D, nD, kb, ke, &plo, &phi);                           \
+      if (have && (plo != *lo || phi != *hi)) return -2;                       \
+      if (!have)                                                               \
+        for (int i = 0; i < m; ++i) memset(out[i], 0, sizeof(V) * (phi - plo));\
+      size_t mt = 0, prev = (size_t)-1;                                        \
+      for (size_t k = 0; k < n[p]; ++k) {                                      \
+        const size_t pos = plo + lb_u64(D + plo, phi - plo, keys[p][k]);       \
+        if (pos >= phi || D[pos] != keys[p][k]) continue;                      \
+        if (prev != (size_t)-1 && pos <= prev) continue; /* walk never backs */\
+        prev = pos;                                                            \
+        ++mt;                                                                  \
+        for (int i = 0; i < m; ++i) {                                          \
+          V* o = out[i] + (pos - plo);                                         \
+          const V v = vals[(size_t)p * m + i][k];                              \
+          *o = have ? *o + v : v;                                              \
+        }                                                                      \
+      }                                                                        \
+      matched[p] = mt;                                                         \
+      if (!have) {                                                             \
+        *lo = plo;                                                             \
+        *hi = phi;                                                             \
+        have = 1;                                                              \
+      }                                                                        \
+    }                                                                          \
+    return 0;                                                                  \
+  }
+
+DEFINE_AGGREGATE_SCATTER(f32, float)
+DEFINE_AGGREGATE_SCATTER(f64, double)
+
 /* kv_vector.h:215-227: oldMatch(recv_key, key_[ch], val_[ch], union range)
  * -- a gather aligned to the request keys, zero where absent. */
 #define DEFINE_GATHER(SUF, V)                                                  \

@@ -92,6 +92,15 @@ int orc_aggregate_f64(const uint64_t* D, size_t nD, uint64_t kb, uint64_t ke,
                       int m, const double* const* vals, int parallel,
                       int nthreads, double* const* out, size_t* lo,
                       size_t* hi, size_t* matched);
+/* parallelSetValue in O(sum n log |D|) (large checks; see psg_oracle.c) */
+int orc_aggregate_scatter_f32(const uint64_t* D, size_t nD, uint64_t kb, uint64_t ke, int npush,
+                              const uint64_t* const* keys, const size_t* n, int m,
+                              const float* const* vals, float* const* out, size_t* lo, size_t* hi,
+                              size_t* matched);
+int orc_aggregate_scatter_f64(const uint64_t* D, size_t nD, uint64_t kb, uint64_t ke, int npush,
+                              const uint64_t* const* keys, const size_t* n, int m,
+                              const double* const* vals, double* const* out, size_t* lo,
+                              size_t* hi, size_t* matched);
 
 /* KVVector::serialGetValue (kv_vector.h:215-227): out[i] = W[pos(req[i])]
  * or 0 when req[i] is not a server key. */

@@ -598,6 +598,14 @@ struct Filter {
   uint32_t* d_table = nullptr;
   uint32_t n = 0;
   int k = 1;
+  // the caller's stream of the last psg_freq_*_dev call: the table is not
+  // recycled (clear / resize) before the kernels enqueued there finished
+  hipStream_t ext = nullptr;
+  bool ext_used = false;
+  void sync_ext() {
+    if (ext_used) (void)hipStreamSynchronize(ext);
+    ext_used = false;
+  }
 };
 
 }  // namespace
@@ -1146,7 +1154,10 @@ int psg_destroy(psg_ctx* c) {
     if (kv.second.hev) (void)hipEventDestroy(kv.second.hev);
   }
   c->ch.clear();
-  for (auto& kv : c->ff) c->dev_put(kv.second.d_table, 4 * (size_t)kv.second.n);
+  for (auto& kv : c->ff) {
+    kv.second.sync_ext();
+    c->dev_put(kv.second.d_table, 4 * (size_t)kv.second.n);
+  }
   c->ff.clear();
   if (c->stream) (void)hipStreamSynchronize(c->stream);
   for (auto& f : c->fly) c->free_ev.push_back(f.ev);
@@ -1858,6 +1869,7 @@ int psg_freq_resize(psg_ctx* c, int chl, int n, int k) {
   if (int rc = set_dev(c->device)) return rc;
   Filter& F = c->ff[chl];
   const uint32_t nn = (uint32_t)std::max(n, 64);  // countmin.h:15
+  F.sync_ext();
   if (nn != F.n) {
     c->dev_put(F.d_table, 4 * (size_t)F.n);
     F.d_table = nullptr;
@@ -1875,6 +1887,7 @@ int psg_freq_clear(psg_ctx* c, int chl) {
   std::lock_guard<std::mutex> l(c->mu);
   auto it = c->ff.find(chl);
   if (it != c->ff.end()) {
+    it->second.sync_ext();
     c->dev_put(it->second.d_table, 4 * (size_t)it->second.n);
     c->ff.erase(it);
   }
@@ -1906,6 +1919,8 @@ int psg_freq_insert_dev(psg_ctx* c, int chl, const uint64_t* keys, const uint32_
   Filter* F;
   if (int rc = filter_of(c, chl, &F)) return rc;
   HIP_TRY(psg::launch_cm_insert(keys, counts, n, F->d_table, F->n, F->k, (hipStream_t)stream));
+  F->ext = (hipStream_t)stream;
+  F->ext_used = true;
   return PSG_OK;
 }
 
@@ -1920,6 +1935,8 @@ int psg_freq_query_dev(psg_ctx* c, int chl, const uint64_t* keys, size_t n, int 
   if (int rc = filter_of(c, chl, &F)) return rc;
   HIP_TRY(psg::launch_cm_query(keys, n, F->d_table, F->n, F->k, freq, out, nout, scratch,
                                (hipStream_t)stream));
+  F->ext = (hipStream_t)stream;
+  F->ext_used = true;
   return PSG_OK;
 }
 

@@ -45,6 +45,10 @@ def orc() -> C.CDLL:
             "orc_aggregate_f64": (C.c_int, [_p, _sz, _u64, _u64, C.c_int, _p, _p,
                                             C.c_int, _p, C.c_int, C.c_int, _p,
                                             _psz, _psz, _p]),
+            "orc_aggregate_scatter_f32": (C.c_int, [_p, _sz, _u64, _u64, C.c_int, _p, _p,
+                                                    C.c_int, _p, _p, _psz, _psz, _p]),
+            "orc_aggregate_scatter_f64": (C.c_int, [_p, _sz, _u64, _u64, C.c_int, _p, _p,
+                                                    C.c_int, _p, _p, _psz, _psz, _p]),
             "orc_old_match_f32": (C.c_int, [_p, _sz, _p, _sz, _p, _u64, _u64, _p,
                                             _psz, _psz, _psz]),
             "orc_murmur3_x64_128": (None, [_p, C.c_int, C.c_uint32, _p]),
@@ -132,6 +136,30 @@ def aggregate(D, kb, ke, pushes, parallel=False, nthreads=1, dtype=np.float32):
     f = orc().orc_aggregate_f32 if dtype == np.float32 else orc().orc_aggregate_f64
     rc = f(_a(D), D.size, int(kb), int(ke), npush, kp, ns, m, vp, int(parallel),
            nthreads, op, C.byref(lo), C.byref(hi), _a(matched))
+    n = hi.value - lo.value
+    return rc, lo.value, hi.value, [o[:n] for o in outs], matched[:npush]
+
+
+def aggregate_scatter(D, kb, ke, pushes, dtype=np.float32):
+    """parallelSetValue in O(sum n log |D|) (orc_aggregate_scatter): the
+    parallel-mode result for checks too large for the merge-walk oracle."""
+    D = u64(D)
+    dtype = np.dtype(dtype)
+    npush = len(pushes)
+    m = len(pushes[0][1]) if npush else 1
+    keys = [u64(k) for k, _ in pushes]
+    vals = [np.ascontiguousarray(v, dtype=dtype) for _, vs in pushes for v in vs]
+    kp = (C.c_void_p * max(1, npush))(*[_a(k) for k in keys])
+    ns = (C.c_size_t * max(1, npush))(*[k.size for k in keys])
+    vp = (C.c_void_p * max(1, len(vals)))(*[_a(v) for v in vals])
+    lo0, hi0 = find_range(D, kb, ke)
+    outs = [np.zeros(max(1, hi0 - lo0), dtype) for _ in range(m)]
+    op = (C.c_void_p * m)(*[_a(o) for o in outs])
+    lo, hi = C.c_size_t(), C.c_size_t()
+    matched = np.zeros(max(1, npush), np.uint64)
+    f = orc().orc_aggregate_scatter_f32 if dtype == np.float32 else orc().orc_aggregate_scatter_f64
+    rc = f(_a(D), D.size, int(kb), int(ke), npush, kp, ns, m, vp, op, C.byref(lo), C.byref(hi),
+           _a(matched))
     n = hi.value - lo.value
     return rc, lo.value, hi.value, [o[:n] for o in outs], matched[:npush]
 

@@ -523,6 +523,30 @@ def test_plan_cfg5_shard(torch_cuda):
     assert_bitexact(keep[3][0].cpu().numpy()[: D.size], want[0])
 
 
+@pytest.mark.timeout(600)
+def test_plan_cfg5_whole_workload_parallel(torch_cuda):
+    """The whole 1-GPU cfg5 workload (the bench's cfg5 line): 256 pushes x
+    262,144 keys over U = 64.9 M server slots, packed-round kernel and stream
+    partition, parallel mode, bit-exact against the oracle's
+    parallelSetValue in scatter form (orc_aggregate_scatter, cross-checked
+    against the merge-walk restatement in test_oracle.py).  The serial
+    mode's sign-of-zero rule is covered at shard size
+    (test_plan_cfg5_shard)."""
+    torch = torch_cuda
+    from parameter_server_amd import synth
+    D, pushes = synth.uniform_pushes(seed=5)
+    assert len(pushes) == 256 and D.size > 64_000_000
+    plan, keep = plan_for(torch, [(D, pushes)], parallel=True)
+    plan.run()
+    assert plan.matched().tolist() == [k.size for k, _ in pushes]
+    got = keep[3][0].cpu().numpy()[: D.size]
+    del plan, keep
+    torch.cuda.empty_cache()
+    rc, lo, hi, want, matched = O.aggregate_scatter(D, *ALL, pushes)
+    assert rc == 0 and (lo, hi) == (0, D.size)
+    assert_bitexact(got, want[0])
+
+
 def test_rcv1_shape_blocks(torch_cuda):
     """cfg1 (rcv1 L1-LR via Darling) shape through the host API: 47,236
     server keys in [1, 47237), feature blocks as key ranges, 2 workers

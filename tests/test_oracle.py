@@ -170,3 +170,32 @@ def test_unmatched_and_duplicates_are_counted():
 def test_gather_repeated_request_reads_zero():
     out, mt = O.gather([5, 7], [1.0, 2.0], [5, 5, 7])
     assert out.tolist() == [1.0, 0.0, 2.0] and mt == 2
+
+
+@pytest.mark.parametrize("seed", range(4))
+def test_scatter_form_equals_parallel_merge_walk(seed):
+    """orc_aggregate_scatter (the O(sum n log U) parallelSetValue used for
+    the whole-cfg5 GPU check) equals the merge-walk restatement of match()
+    bit for bit: sub-ranges, keys outside the range or absent from D,
+    repeated keys, -0.0, empty pushes, f32 and f64, m = 1..2."""
+    rng = np.random.default_rng(100 + seed)
+    dtype = np.float32 if seed % 2 == 0 else np.float64
+    m = 1 + seed % 2
+    D = np.unique(rng.integers(0, 1 << 40, 3000, dtype=np.uint64))
+    pushes = []
+    for p in range(7):
+        k = np.sort(np.concatenate([rng.choice(D, int(rng.integers(0, 900)), replace=False),
+                                    rng.integers(0, 1 << 40, 20, dtype=np.uint64)]))
+        if p == 3 and k.size > 10:
+            k[5] = k[4]  # a repeated key
+        vs = [rng.standard_normal(k.size).astype(dtype) for _ in range(m)]
+        for v in vs:
+            v[rng.random(k.size) < 0.1] = -0.0
+        pushes.append((k, vs))
+    for kb, ke in [(0, (1 << 64) - 1), (int(D[100]), int(D[2500]))]:
+        a = O.aggregate(D, kb, ke, pushes, True, 3, dtype)
+        b = O.aggregate_scatter(D, kb, ke, pushes, dtype)
+        assert a[0] == b[0] == 0 and a[1:3] == b[1:3]
+        assert np.array_equal(a[4], b[4])
+        for x, y in zip(a[3], b[3]):
+            assert x.tobytes() == y.tobytes()
