@@ -83,6 +83,8 @@ def parse():
     ap.add_argument("--no-cfg5", action="store_true",
                     help="skip the cfg5 strong-scaling block of the default line")
     ap.add_argument("--cfg5-steps", type=int, default=10)
+    ap.add_argument("--cfg5-unsliced-child", action="store_true",
+                    help=argparse.SUPPRESS)  # internal: the unsliced leg in its own process
     ap.add_argument("--cpu-seconds", type=float, default=10.0)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--plan-flags", type=lambda x: int(x, 0), default=0,
@@ -168,6 +170,8 @@ def main():
     global PLAN_FLAGS
     args = parse()
     PLAN_FLAGS = args.plan_flags
+    if args.cfg5_unsliced_child:
+        return unsliced_child_main(args)
     import torch
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
@@ -394,13 +398,13 @@ def cfg5_block(args, rank, world, bounds, dist, dev, local, stream):
         "rank0": sliced["rank0"],
         "modes": {"sliced": sliced},
     }
-    # ---- unsliced ingress: whole pushes per rank, RCCL exchange in the step
-    try:
-        out["modes"]["unsliced"] = cfg5_unsliced(args, rank, world, bounds, dist, dev, local,
-                                                 stream, pushes, D, out_sliced, kv_total)
-    finally:
-        del out_sliced
-        torch.cuda.empty_cache()
+    log(f"rank {rank}: cfg5 sliced leg {sliced['ms_per_step']:.3f} ms/step")
+    # ---- unsliced ingress: whole pushes per rank, RCCL exchange in the step,
+    # run in a child process per rank (its own HIP context and RCCL world),
+    # so a failure of that leg cannot take this line down
+    del out_sliced
+    torch.cuda.empty_cache()
+    out["modes"]["unsliced"] = cfg5_unsliced_child(args, rank, world, dist)
     if world > 1:
         # the same whole workload on ONE GPU (rank 0), the others waiting
         t1 = None
@@ -421,6 +425,71 @@ def cfg5_block(args, rank, world, bounds, dist, dev, local, stream):
     return out
 
 
+def cfg5_unsliced_child(args, rank, world, dist):
+    """Runs `bench.py --cfg5-unsliced-child` as a child process of this rank
+    (rendezvous on MASTER_PORT + 1 for N > 1) and returns rank 0's result,
+    or an error record if the child failed."""
+    import subprocess
+    env = dict(os.environ)
+    if world > 1:
+        env["MASTER_PORT"] = str(int(os.environ.get("MASTER_PORT", "29500")) + 1)
+    cmd = [sys.executable, os.path.join(ROOT, "bench.py"), "--cfg5-unsliced-child",
+           "--cfg5-steps", str(args.cfg5_steps)] + (["--no-check"] if args.no_check else [])
+    res = {"error": "child did not report"}
+    try:
+        p = subprocess.run(cmd, env=env, stdout=subprocess.PIPE, stderr=None, timeout=400,
+                           text=True)
+        lines = [x for x in p.stdout.splitlines() if x.startswith("{")]
+        if p.returncode == 0 and lines:
+            res = json.loads(lines[-1])
+        elif rank == 0:
+            res = {"error": f"child exit {p.returncode}"}
+    except Exception as e:  # noqa: BLE001 - reported in the line
+        res = {"error": repr(e)}
+    if dist:
+        dist.barrier()
+    return res
+
+
+def unsliced_child_main(args):
+    """The unsliced cfg5 leg alone (bench.py --cfg5-unsliced-child): its own
+    torch.distributed world (gloo, for the RCCL id) when N > 1; prints rank
+    0's JSON result."""
+    import torch
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    torch.cuda.set_device(local)
+    dist = None
+    if world > 1:
+        import torch.distributed as dist
+        dist.init_process_group("gloo")
+    from parameter_server_amd import synth
+    from parameter_server_amd.kv_vector import shard_bounds
+    bounds = shard_bounds(world)
+    dev = torch.device("cuda", local)
+    stream = torch.cuda.current_stream()
+    _, pushes = synth.uniform_pushes(seed=5, union=False)
+    kv_total = sum(int(k.size) for k, _ in pushes)
+    pieces = synth.shard_pieces(pushes, bounds, rank)
+    D = np.unique(np.concatenate([k for k, _ in pieces]))
+    # the sliced merge of the same pieces, once (the bit-exactness reference)
+    ref = None
+    if not args.no_check:
+        plan, keep, _ = make_plan([(D, pieces)], dev, local)
+        plan.run(stream.cuda_stream)
+        torch.cuda.synchronize()
+        ref = keep[0][3].clone()
+        del plan, keep
+        torch.cuda.empty_cache()
+    r = cfg5_unsliced(args, rank, world, bounds, dist, dev, local, stream, pushes, D, ref,
+                      kv_total)
+    if rank == 0:
+        print(json.dumps(r), flush=True)
+    if dist:
+        dist.destroy_process_group()
+
+
 def cfg5_unsliced(args, rank, world, bounds, dist, dev, local, stream, pushes, D, out_sliced,
                   kv_total):
     """The cfg5 step with unsliced ingress (mode B): rank r holds pushes
@@ -434,8 +503,10 @@ def cfg5_unsliced(args, rank, world, bounds, dist, dev, local, stream, pushes, D
     a, b = rank * P // world, (rank + 1) * P // world
     sh = stream.cuda_stream
     dp = [(to_dev(k, dev), [to_dev(v, dev) for v in vs]) for k, vs in pushes[a:b]]
+    log(f"rank {rank}: unsliced cfg5 leg: {b - a} whole pushes, RCCL communicator")
     comm = shard.make_comm(local, rank, world, dist)
     x = shard.RcclExchange(comm, dp, world, PSG_F32)
+    log(f"rank {rank}: exchange set up: {x.nsent:,} keys sent, {x.nrecv:,} received")
     try:
         pcs = x.pieces()  # (offset, count) per (source, push), arrival order
         dD = to_dev(D, dev)
@@ -451,7 +522,8 @@ def cfg5_unsliced(args, rank, world, bounds, dist, dev, local, stream, pushes, D
             assert np.array_equal(plan.matched(), np.array([c for _, c in pcs], np.uint64))
             assert x.status() == 0
             # same pushes, same arrival order as the sliced leg: same bits
-            assert torch.equal(res.view(torch.int32), out_sliced.view(torch.int32)), \
+            assert out_sliced is None or torch.equal(res.view(torch.int32),
+                                                     out_sliced.view(torch.int32)), \
                 "unsliced cfg5 merge differs from the sliced one"
         K = args.cfg5_steps
         wall, (x_ms, part_ms, agg_ms) = timed_stages(
