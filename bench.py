@@ -87,6 +87,8 @@ def parse():
                     help=argparse.SUPPRESS)  # internal: the unsliced leg in its own process
     ap.add_argument("--cpu-seconds", type=float, default=10.0)
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--arena", action="store_true",
+                    help="stage each aggregate's pushes in one key / value arena (A/B)")
     ap.add_argument("--plan-flags", type=lambda x: int(x, 0), default=0,
                     help="kernel-form overrides of include/psg.h (A/B measurements only)")
     ap.add_argument("--no-check", action="store_true",
@@ -110,6 +112,7 @@ def to_dev(a, dev):
 
 
 PLAN_FLAGS = 0  # --plan-flags
+ARENA = False   # --arena
 
 
 def make_plan(insts, dev, local):
@@ -121,8 +124,20 @@ def make_plan(insts, dev, local):
     f64 = bool(insts) and insts[0][1][0][1][0].dtype == np.float64
     for D, pushes in insts:
         dD = to_dev(D, dev)
-        pk = [to_dev(k, dev) for k, _ in pushes]
-        pv = [[to_dev(v, dev) for v in vs] for _, vs in pushes]
+        if ARENA:
+            # the aggregate's pushes in one key arena and one value arena per
+            # value array, back to back (the layout of a server's ingest
+            # staging), as views
+            ka = to_dev(np.concatenate([k for k, _ in pushes]) if pushes else
+                        np.zeros(0, np.uint64), dev)
+            m = len(pushes[0][1]) if pushes else 0
+            va = [to_dev(np.concatenate([vs[i] for _, vs in pushes]), dev) for i in range(m)]
+            offs = np.concatenate([[0], np.cumsum([k.size for k, _ in pushes])]).astype(np.int64)
+            pk = [ka[offs[p]:offs[p + 1]] for p in range(len(pushes))]
+            pv = [[a[offs[p]:offs[p + 1]] for a in va] for p in range(len(pushes))]
+        else:
+            pk = [to_dev(k, dev) for k, _ in pushes]
+            pv = [[to_dev(v, dev) for v in vs] for _, vs in pushes]
         out = torch.empty(max(1, D.size), dtype=torch.float64 if f64 else torch.float32,
                           device=dev)
         keep.append((dD, pk, pv, out))
@@ -167,9 +182,10 @@ def timed_steps(plan, K, W, stream, dist):
 
 
 def main():
-    global PLAN_FLAGS
+    global PLAN_FLAGS, ARENA
     args = parse()
     PLAN_FLAGS = args.plan_flags
+    ARENA = args.arena
     if args.cfg5_unsliced_child:
         return unsliced_child_main(args)
     import torch

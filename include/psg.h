@@ -82,6 +82,7 @@ typedef enum psg_dtype { PSG_F32 = 0, PSG_F64 = 1 } psg_dtype;
 #define PSG_GROUP64 0x20000u      /* uniform rounds: groups of 64 pushes, 2048-slot tiles */
 #define PSG_NO_DENSE 0x40000u     /* never the dense (contiguous-slice) kernel */
 #define PSG_NO_ZERO_COPY 0x80000u /* context: DMA copies instead of GPU reads of pinned memory */
+#define PSG_NO_INDEX 0x100000u    /* plan: no resident bucket index (tables built per run) */
 
 int psg_abi_version(void);
 const char* psg_status_string(int status);

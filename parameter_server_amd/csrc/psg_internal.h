@@ -68,6 +68,9 @@ struct TileDesc {
   uint32_t flags;
   uint32_t segb;                  // the job's segb
   const uint64_t* dpos;           // dense jobs: job position of each push's first key
+  // tile kernel: the tile's bucket table built once with D (a plan's resident
+  // bucket index, launch_bucket_index), or null: built in the kernel
+  const uint32_t* bt;
 };
 
 // dense check of one push against the server keys (psg_tile_dense.hip):
@@ -90,8 +93,15 @@ hipError_t launch_partition(const JobDev* d_jobs, const uint32_t* d_split_item_j
 // aggregate: one workgroup per tile of kTileSlots slots.  psg_tile.hip:
 // every round holds one push (long pieces); psg_tile_packed.hip: rounds may
 // hold several pushes (many short pieces)
+// form: 0 = groups of 32 pushes (1024-slot tiles), 1 = groups of 64 (2048-slot
+// tiles)
 hipError_t launch_aggregate_tile(int dtype, int m, const TileDesc* d_tiles, uint32_t ntiles,
-                                 bool wide, hipStream_t stream);
+                                 int form, hipStream_t stream);
+// the bucket tables of the tile kernel's tiles (psg_tile.hip), built from D
+// alone: bucket_index_words(wide) u32 per tile at out + tile * words
+uint32_t bucket_index_words(bool wide);
+hipError_t launch_bucket_index(const TileDesc* d_tiles, uint32_t ntiles, bool wide, uint32_t* out,
+                               hipStream_t stream);
 hipError_t launch_aggregate_tile_packed(int dtype, int m, const TileDesc* d_tiles,
                                         uint32_t ntiles, hipStream_t stream);
 // psg_tile_dense.hip: every push of every job a contiguous slice of D

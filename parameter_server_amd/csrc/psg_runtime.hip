@@ -211,8 +211,10 @@ struct JobTable {
   // job: pkeys, pvals, pn, out, fail, seg, split.  The image is copied on
   // stream `strm`, without a host wait when `async`; work enqueued on
   // `strm` afterwards sees it.
+  // `index`: give the tile kernel's tiles a resident bucket table (built
+  // here, once, from D: plans, whose D is fixed for their lifetime)
   int build(int dev, int dt, int mm, const std::vector<JobSpec>& jobs, hipStream_t strm = nullptr,
-            bool async = false) {
+            bool async = false, bool index = false) {
     device = dev;
     dtype = dt;
     m = mm;
@@ -298,6 +300,10 @@ struct JobTable {
     size_t off = align_up(sizeof(JobDev) * jobs.size(), 256);
     const size_t tiles_off = off;
     off = align_up(off + sizeof(psg::TileDesc) * tiles, 256);
+    const bool use_index = index && !dense && !pack;
+    const uint32_t iw = psg::bucket_index_words(wide);
+    const size_t index_off = off;
+    if (use_index) off = align_up(off + 4 * (size_t)iw * tiles, 256);
     const size_t sitems_off = off;
     off = align_up(off + 4 * sitems, 256);
     const size_t items_off = off;
@@ -414,6 +420,7 @@ struct JobTable {
         T.segb = d.segb;
         T.flags = s.flags;
         T.dpos = s.dense ? (const uint64_t*)(base + o.dpos) : nullptr;
+        T.bt = use_index ? (const uint32_t*)(base + index_off) + (size_t)(tcur - 1) * iw : nullptr;
       }
     }
     // the fill must match the sizing pass exactly (the image regions are
@@ -437,6 +444,9 @@ struct JobTable {
     else
       HIP_TRY(hipMemcpyAsync(blob, img, off, hipMemcpyHostToDevice, strm));
     HIP_TRY(hipEventRecord(himg_ev[ib], strm));
+    if (use_index)
+      HIP_TRY(psg::launch_bucket_index(d_tiles, ntiles, wide,
+                                       (uint32_t*)((char*)blob + index_off), strm));
     if (!async) HIP_TRY(hipStreamSynchronize(strm));
     return PSG_OK;
   }
@@ -450,7 +460,7 @@ struct JobTable {
     else if (pack)
       HIP_TRY(psg::launch_aggregate_tile_packed(dtype, m, d_tiles, ntiles, s));
     else
-      HIP_TRY(psg::launch_aggregate_tile(dtype, m, d_tiles, ntiles, wide, s));
+      HIP_TRY(psg::launch_aggregate_tile(dtype, m, d_tiles, ntiles, wide ? 1 : 0, s));
     return PSG_OK;
   }
 
@@ -977,7 +987,7 @@ int psg_plan_create(int device, int dtype, int m, unsigned flags,
     if (int rc = detect_dense(specs)) return rc;
   psg_plan* p = new psg_plan();
   p->table.read_knobs(flags);
-  int rc = p->table.build(device, dtype, m, specs);
+  int rc = p->table.build(device, dtype, m, specs, nullptr, false, !(flags & PSG_NO_INDEX));
   if (rc) {
     p->table.release();
     delete p;

@@ -51,12 +51,12 @@ namespace psg {
 
 #ifdef PSG_PHASES
 // diagnostic build only (tools/phases.py): shader clocks between the phase
-// marks of thread 0 of every workgroup, one row per tile (plain stores, no
-// contention), rows of the last launch
+// marks of thread 0 of every workgroup, summed in registers and stored once
+// per tile (one row per tile of the last launch)
 constexpr int kPhTiles = 1 << 17;
 __device__ uint32_t g_phase[kPhTiles][8];
-#define PH(i) do { if (tid == 0 && ti < (uint32_t)kPhTiles) { const unsigned long long _t = clock64(); \
-    g_phase[ti][i] += (uint32_t)(_t - ph_t); ph_t = _t; } } while (0)
+#define PH(i) do { const unsigned long long _t = clock64(); \
+    ph_acc[i] += (uint32_t)(_t - ph_t); ph_t = _t; } while (0)
 #else
 #define PH(i) do { } while (0)
 #endif
@@ -134,6 +134,10 @@ __global__ __launch_bounds__(nt_of(kGroup), (occupancy<V, M, kGroup>())) void ti
   constexpr int kBPT = kNB / kNT;      // bucket-table entries per thread in the scan
   constexpr int kCB = cb_of(kGroup);   // bits of a round's chunk index
   static_assert(kTS / kNT == 4 && (kBPT == 8 || kBPT == 4), "layout");
+  // rounds a wave holds per pass: 6 at 8 workgroups per CU (64 VGPRs); the
+  // 64-push form runs 7 per CU and affords 8 (4 waves x 8 = 32 rounds: a
+  // group of 64 one-round pieces in 2 passes)
+  constexpr int kCap = kGroup == 64 ? KCAP64 : 6;
   __shared__ __attribute__((aligned(16))) uint64_t dk[kTS + 8];
   // bucket starts (u16); the histogram counts in it as packed pairs by 32-bit atomics
   __shared__ __attribute__((aligned(16))) uint32_t bt32[(kNB + 8) / 2];
@@ -152,10 +156,6 @@ __global__ __launch_bounds__(nt_of(kGroup), (occupancy<V, M, kGroup>())) void ti
   __shared__ int pcarry;
   __shared__ uint32_t wsum[kNW];
 
-  // rounds a wave holds per pass: 6 at 8 workgroups per CU (64 VGPRs); the
-  // 64-push form runs 7 per CU and affords 8 (4 waves x 8 = 32 rounds: a
-  // group of 64 one-round pieces in 2 passes)
-  constexpr int kCap = kGroup == 64 ? KCAP64 : 6;
   const uint32_t w = uni((uint32_t)threadIdx.x >> 6);
   const int tid = threadIdx.x;
   const int lane = tid & 63;
@@ -163,8 +163,7 @@ __global__ __launch_bounds__(nt_of(kGroup), (occupancy<V, M, kGroup>())) void ti
   if (ti >= ntiles) return;
 #ifdef PSG_PHASES
   unsigned long long ph_t = clock64();
-  if (tid == 0 && ti < (uint32_t)kPhTiles)
-    for (int i = 0; i < 8; ++i) g_phase[ti][i] = 0;
+  uint32_t ph_acc[8] = {0, 0, 0, 0, 0, 0, 0, 0};
 #endif
   const TileDesc& T = tiles[ti];
   const uint32_t np = T.np;
@@ -232,6 +231,18 @@ __global__ __launch_bounds__(nt_of(kGroup), (occupancy<V, M, kGroup>())) void ti
 #pragma unroll
     for (int j = 0; j < 4; ++j) d[j] = s0 + j < nt ? G(Dg)[s0 + j] : ~0ull;
   }
+  // the resident bucket table (plans): kBPT u16 entries per thread
+  const uint32_t* Bg = T.bt;
+  u32x4 btw = {0u, 0u, 0u, 0u};
+  if (Bg) {
+    if constexpr (kBPT == 8) {
+      btw = __builtin_nontemporal_load((const AS1 u32x4*)Bg + tid);
+    } else {
+      const u32x2 h = __builtin_nontemporal_load((const AS1 u32x2*)Bg + tid);
+      btw.x = h.x;
+      btw.y = h.y;
+    }
+  }
   V a0[M][4];
 #pragma unroll
   for (int mi = 0; mi < M; ++mi)
@@ -264,13 +275,21 @@ __global__ __launch_bounds__(nt_of(kGroup), (occupancy<V, M, kGroup>())) void ti
   cnt32[2 * tid] = 0u;
   cnt32[2 * tid + 1] = 0u;
   if (tid < 8) dk[kTS + tid] = ~0ull;
-  {
+  if (Bg) {  // resident table: installed as loaded
+    bt32[tid * (kBPT / 2)] = btw.x;
+    bt32[tid * (kBPT / 2) + 1] = btw.y;
+    if constexpr (kBPT == 8) {
+      bt32[tid * (kBPT / 2) + 2] = btw.z;
+      bt32[tid * (kBPT / 2) + 3] = btw.w;
+    }
+    if (tid == 0) bt[kNB] = (uint16_t)nt;
+  } else {
     uint32_t z = 0;  // zero
 #pragma unroll
     for (int i = 0; i < kBPT / 2; ++i) bt32[tid * (kBPT / 2) + i] = z;
   }
   if (tid == 0) pcarry = -1;
-  __syncthreads();  // (1) tables, D, cleared histogram
+  __syncthreads();  // (1) tables, D, cleared histogram (or the resident bucket table)
   PH(0);
 
   // ---- a pass: this wave's run of rounds, loaded into registers
@@ -311,8 +330,10 @@ __global__ __launch_bounds__(nt_of(kGroup), (occupancy<V, M, kGroup>())) void ti
   PH(1);
 
   // ---- bucket table: histogram, exclusive scan -> bt[b] = first slot of bucket b
-  // D keys back from LDS: the registers that held them are free during the
-  // pass's element loads (8 waves/SIMD leave 64 VGPRs)
+  // (skipped when the plan's resident index supplied it).  D keys back from
+  // LDS: the registers that held them are free during the pass's element
+  // loads (8 waves/SIMD leave 64 VGPRs)
+  if (!Bg) {
   const u64x2 y0 = *(const u64x2*)&dk[s0];
   const u64x2 y1 = *(const u64x2*)&dk[s0 + 2];
   const uint64_t dd[4] = {y0.x, y0.y, y1.x, y1.y};
@@ -352,6 +373,7 @@ __global__ __launch_bounds__(nt_of(kGroup), (occupancy<V, M, kGroup>())) void ti
     if (tid == 0) bt[kNB] = (uint16_t)nt;
   }
   __syncthreads();  // (4)
+  }
   PH(2);
 
   for (;;) {
@@ -497,11 +519,81 @@ __global__ __launch_bounds__(nt_of(kGroup), (occupancy<V, M, kGroup>())) void ti
     }
   }
   PH(6);
+#ifdef PSG_PHASES
+  if (tid == 0 && ti < (uint32_t)kPhTiles)
+    for (int i = 0; i < 8; ++i) g_phase[ti][i] = ph_acc[i];
+#endif
+}
+
+// The bucket table of every tile, from D alone (a plan's resident index,
+// built once at plan creation: the plan contract fixes D for its
+// lifetime).  Exactly the tile kernel's histogram + scan with the same
+// bucket map, written out as the kNB u16 bucket starts of each tile.
+template <int kGroup>
+__global__ __launch_bounds__(nt_of(kGroup)) void bucket_index_kernel(
+    const TileDesc* __restrict__ tiles, uint32_t ntiles, uint32_t* __restrict__ out) {
+  constexpr int kNT = nt_of(kGroup);
+  constexpr int kNW = kNT / 64;
+  constexpr int kNB = nb_of(kGroup);
+  constexpr int kBPT = kNB / kNT;
+  __shared__ __attribute__((aligned(16))) uint32_t bt32[(kNB + 8) / 2];
+  __shared__ uint32_t wsum[kNW];
+  const uint32_t ti = blockIdx.x;
+  if (ti >= ntiles) return;
+  const TileDesc& T = tiles[ti];
+  const uint32_t nt = T.nt;
+  const uint64_t* Dg = T.dk;
+  const int tid = threadIdx.x, lane = tid & 63;
+  const uint32_t w = uni((uint32_t)tid >> 6);
+  const uint32_t s0 = 4u * (uint32_t)tid;
+  const uint64_t klo = G(Dg)[0];
+  const uint64_t khi = G(Dg)[nt - 1];
+  const uint64_t range = khi - klo;
+  const int bits = range ? 64 - __builtin_clzll(range) : 0;
+  const int s2 = bits > 32 ? bits - 32 : 0;
+  const uint64_t r32 = range >> s2;
+  const uint32_t mul = dev::bucket_scale(r32, kNB);
+#pragma unroll
+  for (int i = 0; i < kBPT / 2; ++i) bt32[tid * (kBPT / 2) + i] = 0u;
+  __syncthreads();
+#pragma unroll
+  for (int j = 0; j < 4; ++j)
+    if (s0 + j < nt) {
+      const uint64_t x = (G(Dg)[s0 + j] - klo) >> s2;
+      const uint32_t b = x > r32 ? (uint32_t)(kNB - 1) : __umulhi((uint32_t)x, mul);
+      __hip_atomic_fetch_add(&bt32[b >> 1], 1u << (16 * (b & 1u)), __ATOMIC_RELAXED,
+                             __HIP_MEMORY_SCOPE_WORKGROUP);
+    }
+  __syncthreads();
+  uint32_t e[kBPT];
+#pragma unroll
+  for (int i = 0; i < kBPT / 2; ++i) {
+    const uint32_t h = bt32[tid * (kBPT / 2) + i];
+    e[2 * i] = h & 0xffffu;
+    e[2 * i + 1] = h >> 16;
+  }
+  uint32_t tot = 0;
+#pragma unroll
+  for (int j = 0; j < kBPT; ++j) {
+    const uint32_t c = e[j];
+    e[j] = tot;
+    tot += c;
+  }
+  const uint32_t x = wave_scan_incl(tot);
+  if (lane == 63) wsum[w] = x;
+  __syncthreads();
+  uint32_t off = x - tot;
+#pragma unroll
+  for (uint32_t v = 0; v < (uint32_t)kNW - 1u; ++v) off += v < w ? wsum[v] : 0u;
+  uint32_t* o = out + (size_t)ti * (kNB / 2);
+#pragma unroll
+  for (int i = 0; i < kBPT / 2; ++i)
+    o[tid * (kBPT / 2) + i] = (e[2 * i] + off) | (e[2 * i + 1] + off) << 16;
 }
 
 template <typename V, int M>
-hipError_t go(const TileDesc* t, uint32_t n, bool wide, hipStream_t s) {
-  if (wide)
+hipError_t go(const TileDesc* t, uint32_t n, int form, hipStream_t s) {
+  if (form == 1)
     hipLaunchKernelGGL((tile_kernel<V, M, 64>), dim3(n), dim3(nt_of(64)), 0, s, t, n);
   else
     hipLaunchKernelGGL((tile_kernel<V, M, 32>), dim3(n), dim3(nt_of(32)), 0, s, t, n);
@@ -509,12 +601,12 @@ hipError_t go(const TileDesc* t, uint32_t n, bool wide, hipStream_t s) {
 }
 
 template <typename V>
-hipError_t launch_m(int m, const TileDesc* t, uint32_t n, bool wide, hipStream_t s) {
+hipError_t launch_m(int m, const TileDesc* t, uint32_t n, int form, hipStream_t s) {
   switch (m) {
-    case 1: return go<V, 1>(t, n, wide, s);
-    case 2: return go<V, 2>(t, n, wide, s);
-    case 3: return go<V, 3>(t, n, wide, s);
-    case 4: return go<V, 4>(t, n, wide, s);
+    case 1: return go<V, 1>(t, n, form, s);
+    case 2: return go<V, 2>(t, n, form, s);
+    case 3: return go<V, 3>(t, n, form, s);
+    case 4: return go<V, 4>(t, n, form, s);
     default: return hipErrorInvalidValue;
   }
 }
@@ -529,11 +621,25 @@ extern "C" int psg_debug_phases(uint32_t* out, uint32_t ntiles) {
 }
 #endif
 
-hipError_t launch_aggregate_tile(int dtype, int m, const TileDesc* d_tiles, uint32_t ntiles,
-                                 bool wide, hipStream_t stream) {
+uint32_t bucket_index_words(bool wide) { return (uint32_t)(wide ? nb_of(64) : nb_of(32)) / 2u; }
+
+hipError_t launch_bucket_index(const TileDesc* d_tiles, uint32_t ntiles, bool wide, uint32_t* out,
+                               hipStream_t stream) {
   if (ntiles == 0) return hipSuccess;
-  return dtype == 0 ? launch_m<float>(m, d_tiles, ntiles, wide, stream)
-                    : launch_m<double>(m, d_tiles, ntiles, wide, stream);
+  if (wide)
+    hipLaunchKernelGGL(bucket_index_kernel<64>, dim3(ntiles), dim3(nt_of(64)), 0, stream, d_tiles,
+                       ntiles, out);
+  else
+    hipLaunchKernelGGL(bucket_index_kernel<32>, dim3(ntiles), dim3(nt_of(32)), 0, stream, d_tiles,
+                       ntiles, out);
+  return hipGetLastError();
+}
+
+hipError_t launch_aggregate_tile(int dtype, int m, const TileDesc* d_tiles, uint32_t ntiles,
+                                 int form, hipStream_t stream) {
+  if (ntiles == 0) return hipSuccess;
+  return dtype == 0 ? launch_m<float>(m, d_tiles, ntiles, form, stream)
+                    : launch_m<double>(m, d_tiles, ntiles, form, stream);
 }
 
 }  // namespace psg

@@ -757,3 +757,4 @@ def test_nan_payloads(torch_cuda, dtype, parallel):
     cand = np.stack([pa[idx % len(pays)], pa[(idx + 2) % len(pays)]]) | ut(quiet)
     assert np.all((gb[idx] == cand[0]) | (gb[idx] == cand[1]))
 
+
