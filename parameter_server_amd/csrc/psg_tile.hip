@@ -49,6 +49,9 @@
 
 namespace psg {
 
+#ifndef PSG_SKELETON
+#define PSG_SKELETON 0  // diagnostic A/B builds (profiles/r03_ab_fold.txt): 1, 2 skip phases
+#endif
 #ifdef PSG_PHASES
 // diagnostic build only (tools/phases.py): shader clocks between the phase
 // marks of thread 0 of every workgroup, summed in registers and stored once
@@ -387,6 +390,24 @@ __global__ __launch_bounds__(nt_of(kGroup), (occupancy<V, M, kGroup>())) void ti
       if (U) load_pass();
       continue;
     }
+#if PSG_SKELETON == 1
+    // diagnostic (A/B builds only): the loads and stores of the kernel, no
+    // search and no fold -- the memory side's own time
+    {
+      V t = V(0);
+#pragma unroll
+      for (int r = 0; r < kCap; ++r)
+        if ((uint32_t)r < nrw && ((fl >> r) & 1u)) t += ev[r][0] + (V)(uint32_t)(ek[r] & 1u);
+      acc[0][s0] += t;
+      done += kNW * Rw;
+      if (done < U) {
+        load_pass();
+        continue;
+      }
+      U = 0;
+      continue;
+    }
+#endif
     // ---- search every held round
     uint32_t pos[kCap];
     fl &= 0xffu;
@@ -419,6 +440,23 @@ __global__ __launch_bounds__(nt_of(kGroup), (occupancy<V, M, kGroup>())) void ti
     if (nrw && lane == 63) lastpos[w] = mylast;
     __syncthreads();  // (5) lastpos of every wave
     PH(3);
+#if PSG_SKELETON == 2
+    // diagnostic: loads, stores and the search, no order check and no fold
+    {
+      V t = V(0);
+#pragma unroll
+      for (int r = 0; r < kCap; ++r)
+        if ((uint32_t)r < nrw && ((fl >> (8 + r)) & 1u)) t += ev[r][0] + (V)pos[r];
+      acc[0][s0] += t;
+      done += kNW * Rw;
+      if (done < U) {
+        load_pass();
+        continue;
+      }
+      U = 0;
+      continue;
+    }
+#endif
 
     // ---- order check
 #pragma unroll

@@ -758,3 +758,61 @@ def test_nan_payloads(torch_cuda, dtype, parallel):
     assert np.all((gb[idx] == cand[0]) | (gb[idx] == cand[1]))
 
 
+
+
+def _corner_pushes(dtype, seed, npush=8, nkeys=6000, m=2):
+    """Pushes whose values mix IEEE corner cases (denormals of both signs,
+    +-0, +inf, the largest finite, round-to-even ties around 1.0 and 2^24 /
+    2^53, values whose sums go denormal or overflow to +inf) with ordinary
+    values.  No -inf and no large negatives: +inf + -inf makes the default
+    NaN, whose sign differs between x86 (the oracle) and the GPU."""
+    rng = np.random.default_rng(seed)
+    if dtype == np.float32:
+        ut, tiny = np.uint32, 2.0 ** -140
+        pool = [0x00000001, 0x80000001, 0x007fffff, 0x807fffff, 0x00800000, 0x80800000,
+                0x7f7fffff, 0x7f800000, 0x00000000, 0x80000000, 0x3f800000, 0x33800000,
+                0x33800001, 0xb3800000, 0x4b800000, 0x3f800001, 0x00400000, 0x80400001]
+    else:
+        ut, tiny = np.uint64, 2.0 ** -1060
+        pool = [0x1, 0x8000000000000001, 0x000fffffffffffff, 0x800fffffffffffff,
+                0x0010000000000000, 0x8010000000000000, 0x7fefffffffffffff,
+                0x7ff0000000000000, 0x0, 0x8000000000000000, 0x3ff0000000000000,
+                0x3ca0000000000000, 0x3ca0000000000001, 0xbca0000000000000,
+                0x4340000000000000, 0x3ff0000000000001, 0x0008000000000000]
+    pool = np.array(pool, ut)
+    D = np.unique(rng.integers(0, 1 << 40, nkeys).astype(np.uint64))
+    pushes = []
+    for _ in range(npush):
+        keep = rng.random(D.size) < 0.7
+        k = D[keep]
+        vs = []
+        for _ in range(m):
+            v = rng.standard_normal(k.size).astype(dtype)
+            sel = rng.random(k.size)
+            v[sel < 0.4] = pool[rng.integers(0, pool.size, int((sel < 0.4).sum()))].view(dtype)
+            small = (sel >= 0.4) & (sel < 0.6)
+            v[small] = (rng.standard_normal(int(small.sum())) * tiny).astype(dtype)
+            vs.append(v)
+        pushes.append((k, vs))
+    return D, pushes
+
+
+@pytest.mark.parametrize("dtype", [np.float32, np.float64])
+@pytest.mark.parametrize("parallel", [False, True])
+def test_fold_ieee_corner_values(torch_cuda, dtype, parallel):
+    """The tile kernel's fold adds by LDS float atomics (ds_add_f32 /
+    ds_add_f64): bit-identical to the reference's `+=` on denormals,
+    signed zeros, overflow and ties, through a plan (m = 2) and through the
+    server context."""
+    torch = torch_cuda
+    D, pushes = _corner_pushes(dtype, 21)
+    plan, keep = plan_for(torch, [(D, pushes)], dtype, parallel)
+    plan.run()
+    torch.cuda.synchronize()
+    _, _, _, want, _ = O.aggregate(D, *ALL, pushes, parallel, 2, dtype)
+    for i in range(2):
+        assert_bitexact(keep[3][i].cpu().numpy()[:D.size], np.asarray(want[i], dtype))
+    plan.close()
+    out = run_ctx(D, [(k, vs) for k, vs in pushes], dtype=dtype, parallel=parallel)
+    for i in range(2):
+        assert_bitexact(np.asarray(out[i][1]), np.asarray(want[i], dtype))
