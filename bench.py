@@ -91,6 +91,8 @@ def parse():
                     help="stage each aggregate's pushes in one key / value arena (A/B)")
     ap.add_argument("--plan-flags", type=lambda x: int(x, 0), default=0,
                     help="kernel-form overrides of include/psg.h (A/B measurements only)")
+    ap.add_argument("--no-server-api", action="store_true",
+                    help="cfg4: skip the server-API (psg_push + psg_received) leg")
     ap.add_argument("--no-check", action="store_true",
                     help="skip the matched-count guard (ablation builds via PSG_LIB_PATH only)")
     ap.add_argument("--profile-steps", type=int, default=0,
@@ -309,6 +311,11 @@ def main():
             "frac_of_measured_copy": achieved / copy_gbps if copy_gbps else None,
         },
     }
+    if wl == "cfg4" and rank == 0 and not args.no_server_api:
+        del plan, keep
+        torch.cuda.empty_cache()
+        result["server_api"] = {"pinned_out": cfg4_server_api(insts[0], local),
+                                "pageable_out": cfg4_server_api(insts[0], local, pinned_out=False)}
     if wl == "cfg2" and not args.no_cfg5 and args.dtype == "f32":
         del plan, keep
         torch.cuda.empty_cache()
@@ -722,6 +729,44 @@ def end_to_end(inst, device, reps=7):
                       f"{reps}; value = the pinned_hold mode")}
 
 
+def cfg4_server_api(inst, device, reps=5, pinned_out=True):
+    """cfg4 through the server API, the reference's call pattern
+    (KVVector::setValue per push, then received(t)): 8 x psg_push of pinned
+    keys + values (PSG_HOLD_BUFFERS) + psg_received into pinned memory.
+    psg_push's O(1) dense test routes every push to the dense kernel; the
+    keys are order-checked where they lie (zero-copy, never staged).  Wall
+    time per aggregate, PCIe included; the merge's device time is in the
+    committed kernel trace (tools/run_cfg4_server.py under rocprofv3)."""
+    import torch
+    from parameter_server_amd import _lib
+    from parameter_server_amd.kv_vector import KVVector, Message
+    D, pushes = inst
+    kv = sum(int(k.size) for k, _ in pushes)
+    hk = [torch.from_numpy(k.view(np.int64)).pin_memory() for k, _ in pushes]
+    hv = [torch.from_numpy(vs[0]).pin_memory() for _, vs in pushes]
+    # pinned out: the merge kernel writes the sums straight into host memory
+    # (its stores are the D2H); pageable out: sums in HBM, then a DMA copy
+    res = (torch.empty(D.size, dtype=torch.float32, pin_memory=True).numpy() if pinned_out
+           else np.empty(D.size, np.float32))
+    v = KVVector(device, _lib.PSG_F32, flags=_lib.PSG_HOLD_BUFFERS)
+    v.setValue(Message(key=D))
+    times = []
+    for r in range(reps + 1):
+        t0 = time.perf_counter()
+        for k, x in zip(hk, hv):
+            v.setValue(Message(time=r, key=k.numpy().view(np.uint64), value=[x.numpy()]))
+        v.received(r, out=[res])
+        if r:
+            times.append(time.perf_counter() - t0)
+    v.close()
+    t = float(np.median(times))
+    link = kv * (4 + 8) + D.size * 4
+    return {"value": kv / t, "unit": "kv-pairs/s", "ms_per_aggregate": t * 1e3,
+            "link_bytes": link, "link_GBps": link / t / 1e9,
+            "scope": ("8 x psg_push (pinned, held) + psg_received of one cfg4 aggregate "
+                      f"(8 x 16,777,216 kv), median of {reps}: PCIe-inclusive, never `value`")}
+
+
 def load_traffic(bytes_per_launch, workload):
     """HBM bytes per launch of the aggregate and partition kernels from the
     committed rocprofv3 PMC summary of this workload
@@ -804,17 +849,6 @@ def bench_rows(device, reps=5):
                               (" + f32 sums" if m else ""))
     assert np.array_equal(ok[:D.size].cpu().numpy().view(np.uint64), D)
     del dk, dv, ok, ov
-    # the reference's way: setUnion push after push on one CPU core (oracle)
-    sys.path.insert(0, os.path.join(ROOT, "tests"))
-    import oracle_py as O
-    t0, reps = time.perf_counter(), 0
-    while time.perf_counter() - t0 < 1.0:
-        acc = np.zeros(0, np.uint64)
-        for k, _ in pushes:
-            acc = O.set_union(acc, k)
-        reps += 1
-    el = time.perf_counter() - t0
-    out["key_union"]["cpu_setUnion_keys_per_s"] = reps * tot / el
     # pull gather (getValue) of 1 M sorted request keys from a cfg2 shard
     req = np.sort(np.concatenate([k for k, _ in pushes[:8]]))[::1]
     dD = torch.from_numpy(D.view(np.int64)).to(dev)
@@ -927,6 +961,7 @@ def cpu_baseline(inst, seconds):
     repeated for ~`seconds` on this host; plus the threaded match path."""
     sys.path.insert(0, os.path.join(ROOT, "tests"))
     import oracle_py as O
+    from parameter_server_amd import synth
     D, pushes = inst
     kv = sum(int(k.size) for k, _ in pushes)
     ALL = (0, (1 << 64) - 1)
@@ -960,8 +995,20 @@ def cpu_baseline(inst, seconds):
                 break
     except Exception:
         pass
+    # the key union the reference's way: setUnion push after push
+    # (shared_array_inl.h:155-162) on one core, beside rows.key_union
+    _, kpushes = synth.overlap_pushes(1)
+    ktot = sum(int(k.size) for k, _ in kpushes)
+    t0, ureps = time.perf_counter(), 0
+    while time.perf_counter() - t0 < 1.0:
+        acc = np.zeros(0, np.uint64)
+        for k, _ in kpushes:
+            acc = O.set_union(acc, k)
+        ureps += 1
+    union_rate = ureps * ktot / (time.perf_counter() - t0)
     return {
         "value": v, "unit": "kv-pairs/s", "cores": 1, "kind": "port",
+        "setUnion_keys_per_s": union_rate,
         "sample": (f"{reps} x one cfg2 aggregate (8 x 131072 kv, U={D.size}) through the "
                    f"oracle's serialSetValue restatement in {el:.1f}s on 1 thread of {model} "
                    f"(host: nproc {os.cpu_count()}, this job's affinity {share} CPUs); the "

@@ -132,6 +132,10 @@ hipError_t launch_host_copy_batch(const HostCopyBatch& b, hipStream_t stream);
 hipError_t launch_check_sorted(const uint64_t* keys, uint64_t n,
                                unsigned long long* bad, hipStream_t stream,
                                bool strict = true);
+// strictly increasing, keys in pinned host memory (device-visible address,
+// 16-B aligned), read by the GPU over the link
+hipError_t launch_check_sorted_host(const uint64_t* keys, uint64_t n,
+                                    unsigned long long* bad, hipStream_t stream);
 // keys-only N-way union of K (<= 64) non-empty sorted device arrays into
 // out_keys (psg_nway.hip); scratch >= nway_scratch_bytes(K, n).  Uploads its
 // tables with a synchronous copy on `stream`, then enqueues the merge;

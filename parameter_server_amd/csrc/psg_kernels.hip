@@ -135,6 +135,33 @@ __global__ __launch_bounds__(256) void check_sorted_kernel(
   if ((threadIdx.x & 63) == 0 && m) atomicAdd(bad, (unsigned long long)__popcll(m));
 }
 
+// Strictly-increasing check of keys in pinned HOST memory, read by the GPU
+// itself (zero-copy, 16 B per lane per load) -- a dense push's keys are
+// needed for nothing else, so they are never staged in HBM.  Lane l of a
+// wave holds keys 2u, 2u+1 (u = unit index); key 2u-1 comes from lane l-1,
+// or, for lane 0, from one 8-B load.  Keys 16-B aligned (the runtime checks).
+__global__ __launch_bounds__(256) void check_sorted_host_kernel(
+    const uint64_t* __restrict__ k, uint64_t n, unsigned long long* bad) {
+  typedef unsigned long long u64x2_t __attribute__((ext_vector_type(2)));
+  const uint64_t n2 = n / 2;  // whole units
+  const uint64_t stride = (uint64_t)gridDim.x * 256u;
+  const int lane = threadIdx.x & 63;
+  uint32_t cnt = 0;
+  // every lane of a wave runs the same iterations (u0 is wave-uniform)
+  for (uint64_t u0 = (uint64_t)blockIdx.x * 256u + (threadIdx.x & ~63u); u0 < n2; u0 += stride) {
+    const uint64_t u = u0 + (uint64_t)lane;
+    u64x2_t v = {0ull, 0ull};
+    if (u < n2) v = __builtin_nontemporal_load((const u64x2_t*)k + u);
+    uint64_t prev = (uint64_t)__shfl_up((long long)v.y, 1, 64);
+    if (lane == 0 && u > 0) prev = k[2 * u - 1];
+    if (u < n2) cnt += (v.x < v.y ? 0u : 1u) + ((u > 0 && !(prev < v.x)) ? 1u : 0u);
+  }
+  if (blockIdx.x == 0 && threadIdx.x == 0 && (n & 1u) && n > 1)
+    cnt += k[n - 2] < k[n - 1] ? 0u : 1u;
+  for (int o = 32; o > 0; o >>= 1) cnt += (uint32_t)__shfl_down((int)cnt, o, 64);
+  if (lane == 0 && cnt) atomicAdd(bad, (unsigned long long)cnt);
+}
+
 // sliceKeyOrderedMsg positions: one wave per separator (message.h:96-99)
 __global__ __launch_bounds__(256) void slice_kernel(
     const uint64_t* __restrict__ keys, uint64_t n, uint64_t kb, uint64_t ke,
@@ -221,6 +248,16 @@ hipError_t launch_check_sorted(const uint64_t* keys, uint64_t n,
   if (n < 2) return hipSuccess;
   hipLaunchKernelGGL(check_sorted_kernel, dim3((uint32_t)((n + 255) / 256)),
                      dim3(256), 0, stream, keys, n, bad, strict);
+  return hipGetLastError();
+}
+
+hipError_t launch_check_sorted_host(const uint64_t* keys, uint64_t n,
+                                    unsigned long long* bad, hipStream_t stream) {
+  if (n < 2) return hipSuccess;
+  uint64_t blocks = (n / 2 + 255) / 256;
+  blocks = blocks < 1 ? 1 : (blocks > 512 ? 512 : blocks);
+  hipLaunchKernelGGL(check_sorted_host_kernel, dim3((uint32_t)blocks), dim3(256), 0, stream,
+                     keys, n, bad);
   return hipGetLastError();
 }
 

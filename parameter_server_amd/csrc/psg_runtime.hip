@@ -519,6 +519,9 @@ namespace {
 struct KeyBuf {
   uint64_t* d = nullptr;
   size_t n = 0, bytes = 0;
+  // a dense push's keys left in the caller's pinned memory (d null): the
+  // device-visible address its order check reads
+  const uint64_t* host = nullptr;
 };
 using KeyRef = std::shared_ptr<KeyBuf>;
 
@@ -1377,7 +1380,12 @@ int psg_ctx::push_values(int chl, int time, uint64_t kb, uint64_t ke, const KeyR
     pp.dense = true;
     pp.dpos = *slice - lo;
     pp.kd = ch[chl].d_keys + *slice;
-    HIP_TRY(psg::launch_check_sorted(keys->d, n, A.d_bad, copy, true));
+    if (keys->d) {
+      HIP_TRY(psg::launch_check_sorted(keys->d, n, A.d_bad, copy, true));
+    } else {
+      HIP_TRY(psg::launch_check_sorted_host(keys->host, n, A.d_bad, copy));
+      pinned_wait = pinned_wait || !(flags & PSG_HOLD_BUFFERS);
+    }
   }
   A.pending.push_back(pp);
   A.expected_total += n;
@@ -1530,9 +1538,19 @@ int psg_push(psg_ctx* c, int chl, int time, uint64_t kb, uint64_t ke,
             h[a + n - 1] - h[a] == n - 1;
   }
   KeyRef k;
-  int rc = c->new_keys(n, &k);
-  // a dense push's keys are read by its check right away: not deferred
-  if (rc == PSG_OK) rc = c->h2d(k->d, keys, 8 * n, !dense);
+  int rc = PSG_OK;
+  const void* kdev = nullptr;
+  if (dense && c->zero_copy && host_pinned(keys, &kdev) && kdev && ((uintptr_t)kdev & 15u) == 0) {
+    // pinned keys of a dense push: its order check reads them where they
+    // are; nothing else needs them on the device (no HBM copy)
+    k = std::make_shared<KeyBuf>();
+    k->n = n;
+    k->host = (const uint64_t*)kdev;
+  } else {
+    rc = c->new_keys(n, &k);
+    // a dense push's keys are read by its check right away: not deferred
+    if (rc == PSG_OK) rc = c->h2d(k->d, keys, 8 * n, !dense);
+  }
   if (rc == PSG_OK) rc = c->push_values(chl, time, kb, ke, k, m, vals, nullptr, dense ? &a : nullptr);
   const int rf = c->h2d_finish();
   return rc ? rc : rf;

@@ -709,6 +709,61 @@ def test_push_dense_slice_order_violation_is_unmatched(torch_cuda):
     v.close()
 
 
+@pytest.mark.parametrize("hold", [False, True])
+def test_push_dense_pinned_keys_checked_in_place(torch_cuda, hold):
+    """Pinned keys of a dense push are never staged: the order check reads
+    them from host memory (16 B per lane, neighbour keys across lanes and
+    waves).  Every kind of violation is reported -- swaps inside a lane's
+    pair, across lanes, across a wave boundary, in an odd tail, and a
+    duplicate -- and a clean push still merges bit-exact.  A pinned buffer
+    that is not 16-B aligned takes the staged path."""
+    torch = torch_cuda
+    from parameter_server_amd._lib import PSGError, PSG_ERR_UNMATCHED, PSG_HOLD_BUFFERS
+    n = 50001  # odd: a tail key past the last whole pair
+    D = np.arange(7, 7 + n, dtype=np.uint64)
+
+    def pinned(a, shift=0):
+        t = torch.empty(a.size + 2, dtype=torch.int64).pin_memory()
+        h = t.numpy().view(np.uint64)[shift:shift + a.size]
+        h[:] = a
+        return t, h
+
+    def swap(i, j):
+        k = D.copy()
+        k[i], k[j] = k[j], k[i]
+        return k
+    dup = D.copy()
+    dup[1001:20000] = D[1000:19999]  # keys 1000 twice, ends and count unchanged
+    dup[20000:] = D[20000:]
+    cases = [swap(100, 101), swap(101, 102), swap(127, 128), swap(255, 256),
+             swap(n - 2, n - 1), dup]
+    flags = PSG_HOLD_BUFFERS if hold else 0
+    for shift in (0, 1):
+        for k in cases:
+            keep, hk = pinned(k, shift)
+            v = kvv(flags=flags)
+            v.setValue(msg(D))
+            vals = np.ones(n, np.float32)
+            v.setValue(msg(hk, [vals], t=3))
+            with pytest.raises(PSGError) as e:
+                v.received(3)
+            assert e.value.status == PSG_ERR_UNMATCHED
+            v.close()
+            del keep
+        keep, hk = pinned(D, shift)
+        vals = np.random.default_rng(2).standard_normal(n).astype(np.float32)
+        v = kvv(flags=flags)
+        v.setValue(msg(D))
+        v.setValue(msg(hk, [vals], t=4))
+        v.setValue(msg(hk, [vals], t=4))
+        (rng, got), = v.received(4)
+        _, lo, hi, want, _ = O.aggregate(D, *ALL, [(D, [vals])] * 2, False, 1, np.float32)
+        assert tuple(rng) == (lo, hi)
+        assert_bitexact(got, want[0])
+        v.close()
+        del keep
+
+
 @pytest.mark.parametrize("dtype", [np.float32, np.float64])
 @pytest.mark.parametrize("parallel", [False, True])
 def test_nan_payloads(torch_cuda, dtype, parallel):
