@@ -622,7 +622,7 @@ def copy_bandwidth(dev, stream):
     return gbps
 
 
-def end_to_end(inst, device, reps=7):
+def end_to_end(inst, device, reps=7, only=None):
     """PCIe-inclusive rate of one cfg2 aggregate through the host C ABI, the
     reference's own call pattern (setValue per push, then received(t) with
     the D2H of the merged shard), driven from C++ (tools/e2e/libe2e.so, no
@@ -661,6 +661,8 @@ def end_to_end(inst, device, reps=7):
     del keys, doff, dsig
     out = {}
     for mode in ("pageable", "pinned", "pinned_hold", "pinned_cached"):
+        if only and mode not in only:
+            continue
         pin = mode != "pageable"
         if pin:
             src = [(torch.from_numpy(k.view(np.int64)).pin_memory().numpy().view(np.uint64),
@@ -683,23 +685,55 @@ def end_to_end(inst, device, reps=7):
         _lib.check(rc)
         t = float(np.median(ms[1:])) * 1e-3
         out[mode] = {"value": kv / t, "ms_per_aggregate": t * 1e3}
-    # the Darling server step on the same keys (f64 G and U from pinned
-    # memory, keys from the key cache, fused updateWeight: nothing D2H)
-    rng = np.random.default_rng(77)
-    GU = [(torch.from_numpy(rng.standard_normal(k.size)).pin_memory().numpy(),
-           torch.from_numpy(rng.random(k.size)).pin_memory().numpy()) for k, _ in pushes]
-    kp = (C.c_void_p * npush)(*[k.ctypes.data for k, _ in pushes])
-    ns = (C.c_size_t * npush)(*[k.size for k, _ in pushes])
-    gp = (C.c_void_p * npush)(*[g.ctypes.data for g, _ in GU])
-    up = (C.c_void_p * npush)(*[u.ctypes.data for _, u in GU])
-    ms = np.zeros(reps + 1, np.float64)
-    vio = C.c_double()
-    _lib.check(E.psg_e2e_darling(C.c_int(device), C.c_uint(_lib.PSG_HOLD_BUFFERS),
-                                 C.c_void_p(D.ctypes.data), C.c_size_t(D.size), C.c_int(npush),
-                                 kp, ns, gp, up, C.c_void_p(sigs.ctypes.data), C.c_int(reps + 1),
-                                 C.c_void_p(ms.ctypes.data), C.byref(vio)))
-    t = float(np.median(ms[1:])) * 1e-3
-    out["darling_fused"] = {"value": kv / t, "ms_per_aggregate": t * 1e3, "dtype": "f64", "m": 2}
+    if not only or "compressed" in only:
+        # compressed messages (the worker's compressTo, van.cc:204-214): each
+        # push's key and value parts snappy-compressed by the harness, pinned,
+        # through psg_push_compressed (decoded on the device), then received
+        E.psg_e2e_compress.restype = C.c_size_t
+        cparts = []
+        for k, vs in pushes:
+            pair = []
+            for raw in (np.ascontiguousarray(k).view(np.uint8), np.ascontiguousarray(vs[0]).view(np.uint8)):
+                buf = np.empty(32 + raw.size + raw.size // 6, np.uint8)
+                nb = E.psg_e2e_compress(C.c_void_p(raw.ctypes.data), C.c_size_t(raw.size),
+                                        C.c_void_p(buf.ctypes.data))
+                pin = torch.empty(nb, dtype=torch.uint8, pin_memory=True).numpy()
+                pin[:] = buf[:nb]
+                pair.append(pin)
+            cparts.append(pair)
+        ck = (C.c_void_p * npush)(*[a.ctypes.data for a, _ in cparts])
+        ckn = (C.c_size_t * npush)(*[a.size for a, _ in cparts])
+        cv = (C.c_void_p * npush)(*[b.ctypes.data for _, b in cparts])
+        cvn = (C.c_size_t * npush)(*[b.size for _, b in cparts])
+        res = torch.empty(D.size, dtype=torch.float32, pin_memory=True).numpy()
+        ms = np.zeros(reps + 1, np.float64)
+        _lib.check(E.psg_e2e_compressed(C.c_int(device), C.c_int(_lib.PSG_F32),
+                                        C.c_uint(_lib.PSG_SERIAL_MATCH), C.c_void_p(D.ctypes.data),
+                                        C.c_size_t(D.size), C.c_int(npush), ck, ckn, cv, cvn,
+                                        C.c_void_p(res.ctypes.data), C.c_int(reps + 1),
+                                        C.c_void_p(ms.ctypes.data)))
+        t = float(np.median(ms[1:])) * 1e-3
+        cbytes = sum(a.size + b.size for a, b in cparts)
+        out["compressed"] = {"value": kv / t, "ms_per_aggregate": t * 1e3,
+                             "compressed_bytes": cbytes, "ratio": cbytes / (12 * kv)}
+    if not only or "darling_fused" in only:
+        # the Darling server step on the same keys (f64 G and U from pinned
+        # memory, keys from the key cache, fused updateWeight: nothing D2H)
+        rng = np.random.default_rng(77)
+        GU = [(torch.from_numpy(rng.standard_normal(k.size)).pin_memory().numpy(),
+               torch.from_numpy(rng.random(k.size)).pin_memory().numpy()) for k, _ in pushes]
+        kp = (C.c_void_p * npush)(*[k.ctypes.data for k, _ in pushes])
+        ns = (C.c_size_t * npush)(*[k.size for k, _ in pushes])
+        gp = (C.c_void_p * npush)(*[g.ctypes.data for g, _ in GU])
+        up = (C.c_void_p * npush)(*[u.ctypes.data for _, u in GU])
+        ms = np.zeros(reps + 1, np.float64)
+        vio = C.c_double()
+        _lib.check(E.psg_e2e_darling(C.c_int(device), C.c_uint(_lib.PSG_HOLD_BUFFERS),
+                                     C.c_void_p(D.ctypes.data), C.c_size_t(D.size), C.c_int(npush),
+                                     kp, ns, gp, up, C.c_void_p(sigs.ctypes.data), C.c_int(reps + 1),
+                                     C.c_void_p(ms.ctypes.data), C.byref(vio)))
+        t = float(np.median(ms[1:])) * 1e-3
+        out["darling_fused"] = {"value": kv / t, "ms_per_aggregate": t * 1e3, "dtype": "f64", "m": 2}
     # the link itself: pinned <-> device copies of 64 MB (torch, same streams)
     link = {}
     hbuf = torch.empty(64 << 20, dtype=torch.uint8, pin_memory=True)
@@ -719,11 +753,16 @@ def end_to_end(inst, device, reps=7):
     vb, kb, ob = 4 * kv, 8 * kv, 4 * D.size
     for mode, b, ob in (("pageable", kb + vb + ob, ob), ("pinned", kb + vb + ob, ob),
                         ("pinned_hold", kb + vb + ob, ob), ("pinned_cached", vb + ob, ob),
+                        ("compressed", out.get("compressed", {}).get("compressed_bytes", 0) + ob,
+                         ob),
                         ("darling_fused", 16 * kv, 0)):
+        if mode not in out:
+            continue
         bound = (b - ob) / (link["h2d_GBps"] * 1e9) + ob / (link["d2h_GBps"] * 1e9)
         out[mode]["link_bytes"] = b
         out[mode]["frac_of_link"] = bound * 1e3 / out[mode]["ms_per_aggregate"]
-    return {"value": out["pinned_hold"]["value"], "unit": "kv-pairs/s", "modes": out, "link": link,
+    return {"value": out.get("pinned_hold", {}).get("value"), "unit": "kv-pairs/s", "modes": out,
+            "link": link,
             "scope": ("one cfg2 aggregate (8 pushes x 131,072 keys): 8 x psg_push (H2D, merge) "
                       "+ psg_received (D2H of the 956,827-slot shard), C++ caller, median of "
                       f"{reps}; value = the pinned_hold mode")}
@@ -906,6 +945,32 @@ def bench_rows(device, reps=5):
         dst_.data_ptr(), None)))
     assert int(dst_.abs().sum().item()) == 0, "snappy row: a part failed to decode"
     row("snappy_uncompress", ms, int(soff[-1]) + nparts * plen, nparts * plen,
+        "uncompressed bytes/s")
+    del dsrc, ddst
+    # snappy, incompressible 1 MB parts (a cfg2 push's key part: what snappy
+    # emits for random data is one 65,536-byte literal per block), 16 parts:
+    # the parse defers the literals, the copy kernel moves them chip-wide
+    nbig, blen = 16, 1 << 20
+
+    def lit_part(seed):
+        r = np.random.default_rng(seed)
+        b = bytearray([0x80, 0x80, 0x40])  # varint 1 MiB
+        for _ in range(blen // 65536):
+            b += bytes([61 << 2, 0xff, 0xff]) + r.integers(0, 256, 65536, dtype=np.uint8).tobytes()
+        return bytes(b)
+
+    parts = [lit_part(i) for i in range(nbig)]
+    soff = np.concatenate([[0], np.cumsum([len(x) for x in parts])]).astype(np.uint64)
+    dsrc = torch.from_numpy(np.frombuffer(b"".join(parts), np.uint8).copy()).to(dev)
+    dso = torch.from_numpy(soff.view(np.int64)).to(dev)
+    ddo = torch.arange(0, nbig + 1, dtype=torch.int64, device=dev) * blen
+    ddst = torch.empty(nbig * blen, dtype=torch.uint8, device=dev)
+    dst_ = torch.empty(nbig, dtype=torch.int32, device=dev)
+    ms = timed(lambda: _lib.check(L.psg_snappy_uncompress_dev(
+        dsrc.data_ptr(), dso.data_ptr(), nbig, ddst.data_ptr(), ddo.data_ptr(),
+        dst_.data_ptr(), None)))
+    assert int(dst_.abs().sum().item()) == 0, "snappy row: a large part failed to decode"
+    row("snappy_uncompress_1MB_parts", ms, int(soff[-1]) + nbig * blen, nbig * blen,
         "uncompressed bytes/s")
     del dsrc, ddst
     # CountMin: insertKeys / queryKeys of 16.8 M keys, 2^26 counters, k = 4

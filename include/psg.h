@@ -142,8 +142,10 @@ int psg_push(psg_ctx* ctx, int chl, int time, uint64_t kb, uint64_t ke,
  * (Van::recv with task.uncompressed_size set, van.cc:204-214): the key part
  * (uint64 keys) and m value parts are DMA'd compressed and decompressed on
  * the device (psg_snappy_uncompress_dev), then pushed like psg_push.
- * Waits for its own decompression; a corrupt part is PSG_ERR_ARG, parts of
- * inconsistent sizes PSG_ERR_SIZE (the reference's CHECKs). */
+ * Parts of inconsistent declared sizes are PSG_ERR_SIZE here (the
+ * reference's CHECKs).  The decode runs asynchronously (the caller's
+ * buffers are free on return, as for psg_push): a part that fails to decode
+ * is reported by psg_received(time) as PSG_ERR_ARG, for the whole aggregate. */
 int psg_push_compressed(psg_ctx* ctx, int chl, int time, uint64_t kb, uint64_t ke,
                         const void* ckeys, size_t ckeys_bytes, int m,
                         const void* const* cvals, const size_t* cvals_bytes);

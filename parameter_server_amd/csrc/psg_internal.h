@@ -177,10 +177,22 @@ hipError_t launch_cm_query(const uint64_t* keys, uint64_t nk, const uint32_t* ta
                            void* scratch, hipStream_t stream);
 
 // snappy raw-format decompression (psg_snappy.hip), one wave per message:
-// part i -> dst + doff[i], of dcap[i] bytes (dcap NULL: doff[i+1] - doff[i])
+// part i -> dst + doff[i], of dcap[i] bytes (dcap NULL: doff[i+1] - doff[i]).
+// scratch (snappy_scratch_bytes(nmsg), device; NULL: no deferral) holds the
+// long literals the parse defers to the chip-wide copy kernel.
+struct SnappyLit {
+  const uint8_t* src;
+  uint8_t* dst;
+  uint64_t len;
+};
+size_t snappy_scratch_bytes(uint64_t nmsg);
+// nbad (nullable): incremented once per part that fails.  pairs: soff holds
+// each part's (begin, end) device addresses (src unused), so the parts of
+// several staging blocks decode in one launch.
 hipError_t launch_snappy(const uint8_t* src, const uint64_t* soff, uint64_t nmsg, uint8_t* dst,
                          const uint64_t* doff, const uint64_t* dcap, int32_t* status,
-                         hipStream_t stream);
+                         void* scratch, hipStream_t stream, unsigned long long* nbad,
+                         bool pairs = false);
 
 // CRC-32C (psg_crc32c.hip): out[i] = crc32c::Extend(init ? init[i] : 0,
 // data + off[i], min(off[i+1] - off[i], max_len)); all pointers device

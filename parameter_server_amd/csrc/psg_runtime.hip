@@ -561,6 +561,16 @@ struct PendingPush {
   bool dense = false;
   uint64_t dpos = 0;           // position of the first key in [lo, hi)
   const uint64_t* kd = nullptr;  // D + lo + dpos
+  // a compressed push's staging block (its parts, decoded on `copy`): held
+  // until the merge that follows the decode
+  void* sblock = nullptr;
+  size_t sbytes = 0;
+  // its parts still to decode (device addresses): input [cbeg, cend),
+  // output cdst of ccap bytes -- decoded together with the other pending
+  // compressed pushes right before the merge that needs them
+  int cparts = 0;
+  uint64_t cbeg[psg::kMaxM + 1] = {}, cend[psg::kMaxM + 1] = {};
+  uint64_t cdst[psg::kMaxM + 1] = {}, ccap[psg::kMaxM + 1] = {};
 };
 
 struct Aggregate {
@@ -570,7 +580,9 @@ struct Aggregate {
   std::vector<PendingPush> pending;
   uint64_t folded = 0;               // pushes already merged into d_out
   uint64_t expected_total = 0;
-  unsigned long long* d_bad = nullptr;  // device: pushed keys not matched so far
+  // device: [0] pushed keys not matched so far, [1] compressed parts that
+  // failed to decode (psg_push_compressed reports them here, asynchronously)
+  unsigned long long* d_bad = nullptr;
 };
 
 // key_cache_ of remote node `sender`, index (key_channel, key_range)
@@ -630,6 +642,7 @@ struct psg_ctx {
   hipStream_t stream = nullptr;  // kernels, D2H
   hipStream_t copy = nullptr;    // H2D of pushes / keys / values
   hipEvent_t copy_ev = nullptr;
+
   std::mutex mu;
   std::unordered_map<int, Channel> ch;
   std::map<int, Aggregate> agg;
@@ -852,6 +865,11 @@ struct psg_ctx {
     pp.keys.reset();
     dev_put(pp.vblock, pp.vbytes);
     pp.vblock = nullptr;
+    // its decode (on `copy`) must be ordered before the release event
+    // dev_put records on `stream`
+    if (pp.sblock) (void)join_copy();
+    dev_put(pp.sblock, pp.sbytes);
+    pp.sblock = nullptr;
   }
 
   // Enqueue the merge of every pending push of `a` into its device output;
@@ -862,9 +880,14 @@ struct psg_ctx {
   // of the host-side release work (psg_received waits for it)
   int flush(Aggregate& a, void* const* outs = nullptr, void* bad_host = nullptr) {
     if (a.pending.empty()) return PSG_OK;
-    if (int rc = join_copy()) return rc;
     while (!a.pending.empty()) {
       const size_t take = std::min(a.pending.size(), flush_pushes);
+      // compressed pushes of this launch: all their parts decode in one
+      // launch on `copy` (one wave per part, side by side), then the join
+      void* dblk = nullptr;
+      size_t dbytes = 0;
+      if (int rc = decode_pending(a, take, &dblk, &dbytes)) return rc;
+      if (int rc = join_copy()) return rc;
       JobSpec js;
       js.keys = ch[a.chl].d_keys + a.lo;
       js.nslots = a.hi - a.lo;
@@ -888,10 +911,11 @@ struct psg_ctx {
       if (int rc = table.run(stream)) return rc;
       HIP_TRY(psg::launch_unmatched(table.d_jobs, 0, table.info[0].np, a.d_bad, stream));
       if (bad_host && take == a.pending.size())
-        if (int rc = d2h(bad_host, a.d_bad, 8)) return rc;
+        if (int rc = d2h(bad_host, a.d_bad, 16)) return rc;
       for (size_t p = 0; p < take; ++p) release_push(a.pending[p]);
       a.pending.erase(a.pending.begin(), a.pending.begin() + take);
       a.folded += take;
+      dev_put(dblk, dbytes);  // after the join: `stream` is past the decode
     }
     return PSG_OK;
   }
@@ -901,7 +925,7 @@ struct psg_ctx {
     for (auto& pp : a.pending) release_push(pp);
     a.pending.clear();
     for (int i = 0; i < a.m; ++i) dev_put(a.d_out[i], (a.hi - a.lo) * sv);
-    dev_put(a.d_bad, 8);
+    dev_put(a.d_bad, 16);
   }
 
   // the value push behind psg_push / psg_push_cached / psg_push_compressed:
@@ -913,7 +937,11 @@ struct psg_ctx {
   // aggregate's unmatched counter
   int push_values(int chl, int time, uint64_t kb, uint64_t ke, const KeyRef& keys, int m,
                   const void* const* vals, void* vblock = nullptr,
-                  const size_t* slice = nullptr);
+                  const size_t* slice = nullptr, void* sblock = nullptr, size_t sbytes = 0,
+                  const PendingPush* comp = nullptr);
+  int decode_pending(Aggregate& a, size_t take, void** blk, size_t* bytes);
+  // the aggregate of `time` (created on first use) over [kb, ke) of chl
+  int aggregate_for(int chl, int time, uint64_t kb, uint64_t ke, int m, Aggregate** out);
 };
 
 namespace {
@@ -1104,7 +1132,14 @@ int psg_snappy_uncompress_dev(const uint8_t* src, const uint64_t* soff, uint64_t
                               void* stream) {
   if (nmsg == 0) return PSG_OK;
   if (!src || !soff || !dst || !doff || !status) return fail(PSG_ERR_ARG, "null argument");
-  HIP_TRY(psg::launch_snappy(src, soff, nmsg, dst, doff, nullptr, status, (hipStream_t)stream));
+  // the deferred-literal list, stream-ordered (freed behind the kernels)
+  hipStream_t st = (hipStream_t)stream;
+  void* scratch = nullptr;
+  HIP_TRY(hipMallocAsync(&scratch, psg::snappy_scratch_bytes(nmsg), st));
+  const hipError_t e =
+      psg::launch_snappy(src, soff, nmsg, dst, doff, nullptr, status, scratch, st, nullptr);
+  HIP_TRY(hipFreeAsync(scratch, st));
+  HIP_TRY(e);
   return PSG_OK;
 }
 
@@ -1329,23 +1364,88 @@ int check_push(psg_ctx* c, int chl, int time, uint64_t kb, uint64_t ke, size_t n
 
 }  // namespace
 
-int psg_ctx::push_values(int chl, int time, uint64_t kb, uint64_t ke, const KeyRef& keys, int m,
-                         const void* const* vals, void* vblock, const size_t* slice) {
-  (void)kb;
-  (void)ke;
-  size_t lo = 0, hi = 0;
+int psg_ctx::decode_pending(Aggregate& a, size_t take, void** blk, size_t* bytes) {
+  *blk = nullptr;
+  *bytes = 0;
+  std::vector<uint64_t> pr, dst, cap;
+  for (size_t p = 0; p < take; ++p) {
+    PendingPush& pp = a.pending[p];
+    for (int i = 0; i < pp.cparts; ++i) {
+      pr.push_back(pp.cbeg[i]);
+      pr.push_back(pp.cend[i]);
+      dst.push_back(pp.cdst[i]);
+      cap.push_back(pp.ccap[i]);
+    }
+    pp.cparts = 0;
+  }
+  const size_t n = dst.size();
+  if (n == 0) return PSG_OK;
+  // held pushes' parts may still sit in the zero-copy batch: issue it first
+  if (int rc = zc_flush()) return rc;
+  // [pairs 16n][dst 8n][cap 8n] | [status 4n] | decoder scratch
+  const size_t hb = 32 * n, sb = align_up(hb + 4 * n, 256);
+  const size_t total = sb + psg::snappy_scratch_bytes(n);
+  void* b = nullptr;
+  if (int rc = dev_get(total, &b, copy)) return rc;
+  std::vector<uint64_t> img(4 * n);
+  std::copy(pr.begin(), pr.end(), img.begin());
+  std::copy(dst.begin(), dst.end(), img.begin() + 2 * n);
+  std::copy(cap.begin(), cap.end(), img.begin() + 3 * n);
+  int rc = h2d(b, img.data(), hb);
+  if (rc == PSG_OK) {
+    const uint64_t* d = (const uint64_t*)b;
+    const hipError_t e = psg::launch_snappy(nullptr, d, n, nullptr, d + 2 * n, d + 3 * n,
+                                            (int32_t*)(d + 4 * n), (char*)b + sb, copy,
+                                            a.d_bad + 1, true);
+    if (e != hipSuccess) rc = fail(PSG_ERR_DEVICE, "snappy: %s", hipGetErrorString(e));
+  }
+  if (rc != PSG_OK) {
+    (void)hipStreamSynchronize(copy);
+    dev_put(b, total);
+    return rc;
+  }
+  *blk = b;
+  *bytes = total;
+  return PSG_OK;
+}
+
+int psg_ctx::aggregate_for(int chl, int time, uint64_t kb, uint64_t ke, int m,
+                           Aggregate** out) {
   auto ait = agg.find(time);
-  {
-    // (re-derived: the caller checked before staging the keys)
+  if (ait == agg.end()) {
+    // (re-derived: the caller checked the push against the range)
     Channel& C = ch[chl];
     const uint64_t* h = C.mirror();
-    lo = std::lower_bound(h, h + C.n, kb) - h;
-    hi = std::lower_bound(h, h + C.n, ke) - h;
+    const size_t lo = std::lower_bound(h, h + C.n, kb) - h;
+    const size_t hi = std::lower_bound(h, h + C.n, ke) - h;
+    Aggregate A;
+    A.chl = chl;
+    A.m = m;
+    A.lo = lo;
+    A.hi = hi;
+    for (int i = 0; i < m; ++i)
+      if (int rc = dev_get((hi - lo) * vsize(dtype), &A.d_out[i], stream)) return rc;
+    // zeroed on `copy`: the dense pushes' order checks and the compressed
+    // pushes' decodes add to it there; every reader on `stream` runs after
+    // a join_copy
+    if (int rc = dev_get(16, (void**)&A.d_bad, copy)) return rc;
+    HIP_TRY(hipMemsetAsync(A.d_bad, 0, 16, copy));
+    ait = agg.emplace(time, A).first;
   }
+  *out = &ait->second;
+  return PSG_OK;
+}
+
+int psg_ctx::push_values(int chl, int time, uint64_t kb, uint64_t ke, const KeyRef& keys, int m,
+                         const void* const* vals, void* vblock, const size_t* slice,
+                         void* sblock, size_t sbytes, const PendingPush* comp) {
   const size_t sv = vsize(dtype), n = keys->n;
   PendingPush pp;
+  if (comp) pp = *comp;  // the compressed parts to decode
   pp.n = n;
   pp.keys = keys;
+  pp.sblock = sblock;
+  pp.sbytes = sbytes;
   const size_t vb = align_up(sv * n, 256);
   pp.vbytes = m * vb;
   if (vblock) {
@@ -1361,24 +1461,15 @@ int psg_ctx::push_values(int chl, int time, uint64_t kb, uint64_t ke, const KeyR
       }
     }
   }
-  if (ait == agg.end()) {
-    Aggregate A;
-    A.chl = chl;
-    A.m = m;
-    A.lo = lo;
-    A.hi = hi;
-    for (int i = 0; i < m; ++i)
-      if (int rc = dev_get((hi - lo) * sv, &A.d_out[i], stream)) return rc;
-    // zeroed on `copy`: the dense pushes' order checks add to it there;
-    // every reader on `stream` runs after a join_copy
-    if (int rc = dev_get(8, (void**)&A.d_bad, copy)) return rc;
-    HIP_TRY(hipMemsetAsync(A.d_bad, 0, 8, copy));
-    ait = agg.emplace(time, A).first;
+  Aggregate* Ap = nullptr;
+  if (int rc = aggregate_for(chl, time, kb, ke, m, &Ap)) {
+    release_push(pp);
+    return rc;
   }
-  Aggregate& A = ait->second;
+  Aggregate& A = *Ap;
   if (slice) {
     pp.dense = true;
-    pp.dpos = *slice - lo;
+    pp.dpos = *slice - A.lo;
     pp.kd = ch[chl].d_keys + *slice;
     if (keys->d) {
       HIP_TRY(psg::launch_check_sorted(keys->d, n, A.d_bad, copy, true));
@@ -1587,55 +1678,41 @@ int psg_push_compressed(psg_ctx* c, int chl, int time, uint64_t kb, uint64_t ke,
   if (int rc = set_dev(c->device)) return rc;
   size_t lo, hi;
   if (int rc = check_push(c, chl, time, kb, ke, n, m, &lo, &hi)) return rc;
-  // staging block: compressed parts, then source offsets, destinations,
-  // capacities and statuses of the m + 1 parts
+  // staging block: the m + 1 compressed parts back to back; they are
+  // decoded right before the merge that needs them (psg_ctx::flush), with
+  // every other compressed push pending then, in one launch
   const int np = m + 1;
   std::vector<uint64_t> soff(np + 1, 0);
   soff[1] = ckeys_bytes;
   for (int i = 0; i < m; ++i) soff[i + 2] = soff[i + 1] + cvals_bytes[i];
-  const size_t tb = align_up(soff[np], 256), meta = 8 * (size_t)(np + 1) + 16 * np + 4 * np;
+  const size_t tb = align_up(soff[np], 256);
   void* blk = nullptr;
-  if (int rc = c->dev_get(tb + meta, &blk, c->copy)) return rc;
+  if (int rc = c->dev_get(tb, &blk, c->copy)) return rc;
   KeyRef k;
   void* vblock = nullptr;
   const size_t vb = align_up(sv * n, 256);
   int rc = c->new_keys(n, &k);
   if (rc == PSG_OK) rc = c->dev_get(m * vb, &vblock, c->copy);
   char* b = (char*)blk;
-  uint64_t* d_soff = (uint64_t*)(b + tb);
-  uint64_t* d_dst = d_soff + (np + 1);
-  uint64_t* d_cap = d_dst + np;
-  int32_t* d_st = (int32_t*)(d_cap + np);
-  std::vector<uint64_t> hm(np + 1 + 2 * np);
-  if (rc == PSG_OK) {
-    std::copy(soff.begin(), soff.end(), hm.begin());
-    hm[np + 1] = (uint64_t)k->d;
-    hm[np + 1 + np] = klen;
-    for (int i = 0; i < m; ++i) {
-      hm[np + 2 + i] = (uint64_t)((char*)vblock + i * vb);
-      hm[np + 1 + np + 1 + i] = n * sv;
-    }
-    rc = c->h2d(b, ckeys, ckeys_bytes);
-    for (int i = 0; rc == PSG_OK && i < m; ++i) rc = c->h2d(b + soff[i + 1], cvals[i], cvals_bytes[i]);
-    if (rc == PSG_OK) rc = c->h2d(d_soff, hm.data(), 8 * hm.size());
-  }
-  std::vector<int32_t> st(np, 0);
-  if (rc == PSG_OK) {
-    hipError_t e = psg::launch_snappy((const uint8_t*)b, d_soff, np, nullptr, d_dst, d_cap, d_st,
-                                      c->copy);
-    if (e == hipSuccess) e = hipMemcpyAsync(st.data(), d_st, 4 * np, hipMemcpyDeviceToHost, c->copy);
-    if (e == hipSuccess) e = hipStreamSynchronize(c->copy);
-    if (e != hipSuccess) rc = fail(PSG_ERR_DEVICE, "snappy: %s", hipGetErrorString(e));
-  }
-  c->pinned_wait = false;  // the copy stream is idle
-  c->dev_put(blk, tb + meta);
-  for (int i = 0; rc == PSG_OK && i < np; ++i)
-    if (st[i]) rc = fail(st[i], "compressed part %d: %s", i, psg_status_string(st[i]));
+  if (rc == PSG_OK) rc = c->h2d(b, ckeys, ckeys_bytes, true);
+  for (int i = 0; rc == PSG_OK && i < m; ++i) rc = c->h2d(b + soff[i + 1], cvals[i], cvals_bytes[i], true);
+  // the caller's buffers are free once their copies land (unless held)
+  if (rc == PSG_OK) rc = c->h2d_finish();
   if (rc != PSG_OK) {
+    (void)hipStreamSynchronize(c->copy);
+    c->dev_put(blk, tb);
     c->dev_put(vblock, m * vb);
     return rc;
   }
-  return c->push_values(chl, time, kb, ke, k, m, nullptr, vblock);
+  PendingPush cp;
+  cp.cparts = np;
+  for (int i = 0; i < np; ++i) {
+    cp.cbeg[i] = (uint64_t)(b + soff[i]);
+    cp.cend[i] = (uint64_t)(b + soff[i + 1]);
+    cp.cdst[i] = i == 0 ? (uint64_t)k->d : (uint64_t)((char*)vblock + (i - 1) * vb);
+    cp.ccap[i] = i == 0 ? (uint64_t)klen : (uint64_t)(n * sv);
+  }
+  return c->push_values(chl, time, kb, ke, k, m, nullptr, vblock, nullptr, blk, tb, &cp);
 }
 
 int psg_push_cached(psg_ctx* c, int sender, int chl, int time, uint64_t kb, uint64_t ke,
@@ -1768,16 +1845,20 @@ int psg_received(psg_ctx* c, int time, int m, void* const* out) {
   for (int i = 0; !direct && rc == PSG_OK && i < A.m && len; ++i)
     rc = c->d2h(out[i], A.d_out[i], len * sv);
   unsigned long long bad = 0;
-  if (rc == PSG_OK && !(direct && pend)) rc = c->d2h(c->h_small, A.d_bad, 8);
+  unsigned long long corrupt = 0;
+  if (rc == PSG_OK && !(direct && pend)) rc = c->d2h(c->h_small, A.d_bad, 16);
   if (rc == PSG_OK) {
     hipError_t e = hipStreamSynchronize(c->stream);
     if (e != hipSuccess) rc = fail(PSG_ERR_DEVICE, "received: %s", hipGetErrorString(e));
     bad = c->h_small[0];
+    corrupt = c->h_small[1];
   }
   const unsigned long long want = A.expected_total;
   c->drop(A);
   c->agg.erase(it);
   if (rc) return rc;
+  if (corrupt)  // Van::recv's CHECK on uncompressFrom (shared_array_inl.h:236)
+    return fail(PSG_ERR_ARG, "time %d: %llu compressed parts failed to decode", time, corrupt);
   if (bad)
     return fail(PSG_ERR_UNMATCHED, "time %d: matched %llu of %llu pushed keys", time,
                 want - bad, want);

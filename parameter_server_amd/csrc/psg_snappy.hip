@@ -20,6 +20,15 @@
 // Offsets beyond the ring (possible only for 4-byte-offset copies, which
 // snappy's own compressor never emits across its 64 KB blocks) read the
 // output in global memory after a fence.
+//
+// Long literals (>= kBigLit bytes: what incompressible data becomes -- the
+// cfg2 key and value parts are one 64 KB literal per snappy block) are not
+// moved by the parsing wave: it records (source, destination, length) and
+// skips them, and a second, chip-wide kernel copies every recorded piece
+// 16 B per lane.  The part's deferred pieces are listed in LDS by output
+// position; a copy element whose source lies wholly inside one of them is
+// itself deferred as a piece of the compressed input (no bytes move in the
+// parse), and one that straddles reads the deferred bytes from the input.
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
@@ -30,22 +39,47 @@ namespace psg {
 
 namespace {
 
+#ifdef PSG_SNAPPY_PROF
+// diagnostic build only (tools/snappy_prof.py): per part, shader clocks in
+// [0] window refills, [1] copies' piece lookups, [2] the whole part, and
+// counts [3] refills, [4] deferred pieces, [5] copies resolved per lane,
+// [6] elements
+__device__ unsigned long long g_sprof[4096][8];
+#define SP_T0() const unsigned long long _sp0 = clock64()
+#define SP_ADD(i) (sp[i] += clock64() - _sp0)
+#else
+#define SP_T0() do { } while (0)
+#define SP_ADD(i) do { } while (0)
+#endif
+
 constexpr uint32_t kRing = 65536;
 constexpr uint32_t kWin = 4096;
-constexpr uint32_t kFlush = 4096;  // output burst size  // LDS window over the compressed stream (tags, offsets)
+
+constexpr uint32_t kBigLit = 2048;   // literals deferred to the copy kernel
+constexpr uint32_t kMaxDef = 768;    // deferred pieces per part (LDS list)
+constexpr uint32_t kLitUnits = 256;  // 16-B units per copy-kernel chunk (4 KB)
 
 __global__ __launch_bounds__(64) void snappy_kernel(const uint8_t* __restrict__ src,
                                                     const uint64_t* __restrict__ soff,
                                                     uint8_t* __restrict__ dst,
                                                     const uint64_t* __restrict__ doff,
                                                     const uint64_t* __restrict__ dcap,
-                                                    uint64_t nmsg, int32_t* __restrict__ status) {
+                                                    uint64_t nmsg, int32_t* __restrict__ status,
+                                                    SnappyLit* __restrict__ lits,
+                                                    uint32_t* __restrict__ nlits,
+                                                    uint32_t lit_cap,
+                                                    unsigned long long* __restrict__ nbad,
+                                                    int pairs) {
   __shared__ uint8_t ring[kRing];
   __shared__ __attribute__((aligned(4))) uint8_t win[kWin];
+  // deferred pieces of the current part, in output order: output start,
+  // input start, length
+  __shared__ uint32_t tdst[kMaxDef], tsrc[kMaxDef], tlen[kMaxDef];
   const uint32_t lane = threadIdx.x;
   for (uint64_t msg = blockIdx.x; msg < nmsg; msg += gridDim.x) {
-    const uint8_t* const s0 = src + soff[msg];
-    const uint64_t slen = soff[msg + 1] - soff[msg];
+    // pairs: soff holds (begin, end) device addresses per part
+    const uint8_t* const s0 = pairs ? (const uint8_t*)soff[2 * msg] : src + soff[msg];
+    const uint64_t slen = pairs ? soff[2 * msg + 1] - soff[2 * msg] : soff[msg + 1] - soff[msg];
     uint8_t* const out = dst + doff[msg];
     const uint64_t cap = dcap ? dcap[msg] : doff[msg + 1] - doff[msg];
     // an empty part is an empty array (uncompressFrom of 0 bytes clears, :233)
@@ -68,20 +102,38 @@ __global__ __launch_bounds__(64) void snappy_kernel(const uint8_t* __restrict__ 
     // a scalar readlane: one LDS read serves several tags
     const uintptr_t mis = (uintptr_t)s0 & 3u;
     int32_t wb = -(int32_t)kWin - 64;  // part offset of win[0]; nothing loaded
+#ifdef PSG_SNAPPY_PROF
+    unsigned long long sp[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+    const unsigned long long sp_part = clock64();
+#endif
     auto refill = [&](uint32_t q) {
+      SP_T0();
+#ifdef PSG_SNAPPY_PROF
+      sp[3] += 1;
+#endif
       wb = (int32_t)((q + mis) & ~3u) - (int32_t)mis;  // 4-byte aligned in memory
-      for (uint32_t o4 = lane * 4u; o4 < kWin; o4 += 256u) {
-        const int64_t g = (int64_t)wb + o4;
-        uint32_t v = 0;
+      // all 16 loads in flight before the first LDS store (one HBM round
+      // trip per refill, not 16: a refill follows every skipped literal)
+      constexpr int kR = (int)(kWin / 256u);
+      uint32_t v[kR];
+#pragma unroll
+      for (int r = 0; r < kR; ++r) {
+        const int64_t g = (int64_t)wb + lane * 4u + 256u * r;
+        v[r] = 0;
         if (g >= 0 && g + 4 <= (int64_t)e) {
-          v = *(const uint32_t*)(s0 + g);
+          v[r] = *(const uint32_t*)(s0 + g);
         } else {
           for (uint32_t b = 0; b < 4; ++b)
-            if (g + b >= 0 && g + b < (int64_t)e) v |= (uint32_t)s0[g + b] << (8 * b);
+            if (g + b >= 0 && g + b < (int64_t)e) v[r] |= (uint32_t)s0[g + b] << (8 * b);
         }
-        *(uint32_t*)&win[o4] = v;
       }
+#pragma unroll
+      for (int r = 0; r < kR; ++r) *(uint32_t*)&win[lane * 4u + 256u * r] = v[r];
       __builtin_amdgcn_wave_barrier();
+#ifdef PSG_SNAPPY_PROF
+      (void)__builtin_amdgcn_readfirstlane((int)win[lane]);  // wait for the window
+#endif
+      SP_ADD(0);
     };
     uint32_t lp = 0xffffffffu - 64u, la = 0;
     auto ub = [&](uint32_t q) -> uint32_t {
@@ -106,16 +158,69 @@ __global__ __launch_bounds__(64) void snappy_kernel(const uint8_t* __restrict__ 
     if (!st && ulen != cap) st = PSG_ERR_SIZE;
     const uint32_t ucap = (uint32_t)ulen;
     uint32_t o = 0;
-    // output bytes [fl, o) live only in the ring; they reach global memory
-    // in kFlush-sized bursts, so the element loop issues no global stores
-    // (on gfx9 a store holds vmcnt, which the next dependent wait drains)
-    uint32_t fl = 0;
+    // this part's deferred pieces (LDS list); [dlo, dhi) spans them all
+    uint32_t nd = 0, dlo = 0xffffffffu, dhi = 0;
+    // Output bytes below fl are in memory or in deferred pieces; the rest
+    // live only in the ring until a flush, which happens only when a ring
+    // write would overwrite an unflushed byte (ofs: the first ring position
+    // written since the last flush), before a read of memory, and at the
+    // end -- so the element loop issues almost no global stores (on gfx9 a
+    // store holds vmcnt, which the next window refill would wait for).
+    // A flush skips the deferred pieces (the copy kernel writes them).
+    uint32_t fl = 0, ofs = 0xffffffffu, fk = 0;
     auto flush = [&](uint32_t to) {
       __builtin_amdgcn_wave_barrier();
-      for (uint32_t x = fl + lane; x < to; x += 64) out[x] = ring[x & (kRing - 1)];
+      uint32_t x = fl;
+      while (x < to) {
+        while (fk < nd && tdst[fk] + tlen[fk] <= x) ++fk;
+        if (fk < nd && tdst[fk] <= x) {  // x inside a deferred piece
+          x = tdst[fk] + tlen[fk];
+          ++fk;
+          continue;
+        }
+        const uint32_t end = fk < nd && tdst[fk] < to ? tdst[fk] : to;
+        for (uint32_t y = x + lane; y < end; y += 64) out[y] = ring[y & (kRing - 1)];
+        x = end;
+      }
       fl = to;
+      ofs = 0xffffffffu;
+    };
+    // before ring writes of [o, o + n): keep every unflushed byte's slot
+    auto room = [&](uint32_t n) {
+      if (ofs != 0xffffffffu && o + n > ofs + kRing) flush(o);
+      if (ofs == 0xffffffffu) ofs = o;
+    };
+    // last piece starting at or before output position x (-1: none)
+    auto find = [&](uint32_t x) -> int {
+      int lo = -1, hi = (int)nd;
+      while (hi - lo > 1) {
+        const int mid = (lo + hi) >> 1;
+        if (tdst[mid] <= x) lo = mid; else hi = mid;
+      }
+      return lo;
+    };
+    // append a piece of input bytes [in, in + len) at output o (the caller
+    // checked nd < kMaxDef); the list goes to the copy kernel when the part
+    // ends (one reservation per part: no global round trip per piece)
+    auto defer = [&](uint32_t len, uint32_t in) {
+#ifdef PSG_SNAPPY_PROF
+      sp[4] += 1;
+#endif
+      if (lane == 0) {
+        tdst[nd] = o;
+        tsrc[nd] = in;
+        tlen[nd] = len;
+      }
+      __builtin_amdgcn_wave_barrier();
+      ++nd;
+      dlo = dlo < o ? dlo : o;
+      o += len;
+      dhi = o;  // its bytes never enter the ring
     };
     while (!st && p < e) {
+#ifdef PSG_SNAPPY_PROF
+      sp[6] += 1;
+#endif
       const uint32_t tag = ub(p++);
       uint32_t len, off;
       if ((tag & 3u) == 0u) {  // literal
@@ -130,18 +235,24 @@ __global__ __launch_bounds__(64) void snappy_kernel(const uint8_t* __restrict__ 
           len += 1u;
         }
         if (e - p < len || ucap - o < len) { st = PSG_ERR_ARG; break; }
+        if (lits && len >= kBigLit && nd < kMaxDef) {
+          defer(len, p);
+          p += len;
+          continue;
+        }
         if ((int32_t)p >= wb && (int64_t)p + len <= (int64_t)wb + kWin) {
+          room(len);  // len <= kWin < kRing
           const uint32_t w0 = (uint32_t)((int32_t)p - wb);
           for (uint32_t l = lane; l < len; l += 64) ring[(o + l) & (kRing - 1)] = win[w0 + l];
+          o += len;
         } else {
           for (uint32_t c = 0; c < len; c += 64) {  // wave-uniform steps
-            if (o + c - fl >= kRing - kFlush) flush(o + c);  // a long literal
-            if (c + lane < len) ring[(o + c + lane) & (kRing - 1)] = s0[p + c + lane];
+            room(64);
+            if (c + lane < len) ring[(o + lane) & (kRing - 1)] = s0[p + c + lane];
+            o += len - c < 64u ? len - c : 64u;
           }
         }
         p += len;
-        o += len;
-        if (o - fl >= kFlush) flush(o);
         continue;
       }
       if ((tag & 3u) == 1u) {
@@ -163,33 +274,190 @@ __global__ __launch_bounds__(64) void snappy_kernel(const uint8_t* __restrict__ 
       if (off == 0 || off > o || ucap - o < len) { st = PSG_ERR_ARG; break; }
       // len <= 64: one step; every source byte precedes o
       const uint32_t li = off >= 64u ? lane : lane % off;  // uniform branch on off
-      if (off <= kRing) {
+      const uint32_t slo = o - off, shi = slo + (len < off ? len : off);
+      if (nd && slo < dhi && shi > dlo) {
+        // wholly inside one deferred piece (and clear of its own output):
+        // deferred too, as that piece's input bytes
+        SP_T0();
+        const int j = find(slo);
+        SP_ADD(1);
+        if (j >= 0 && off >= len && slo - tdst[j] + len <= tlen[j] && nd < kMaxDef) {
+          defer(len, tsrc[j] + (slo - tdst[j]));
+          continue;
+        }
+        // else: bytes in deferred pieces come from the compressed input,
+        // the rest from the ring (or, past it, memory)
+#ifdef PSG_SNAPPY_PROF
+        sp[5] += 1;
+#endif
+        const uint32_t pos = slo + li;
+        uint32_t from = 0xffffffffu;
+        const int jj = find(pos);
+        if (jj >= 0 && pos - tdst[jj] < tlen[jj]) from = tsrc[jj] + (pos - tdst[jj]);
+        if (off > kRing) {
+          flush(o);
+          __threadfence();
+        }
+        const uint8_t b = lane < len ? (from != 0xffffffffu ? s0[from]
+                                        : off <= kRing ? ring[pos & (kRing - 1)] : out[pos])
+                                     : 0;
+        room(len);
+        if (lane < len) ring[(o + lane) & (kRing - 1)] = b;
+      } else if (off <= kRing) {
+        room(len);
         if (lane < len) ring[(o + lane) & (kRing - 1)] = ring[(o - off + li) & (kRing - 1)];
       } else {
         // the source was flushed: read it back after this wave's stores land
         flush(o);
         __threadfence();
+        room(len);
         if (lane < len) ring[(o + lane) & (kRing - 1)] = out[o - off + li];
       }
       o += len;
-      if (o - fl >= kFlush) flush(o);
     }
     if (!st && o != ucap) st = PSG_ERR_ARG;
     if (!st) flush(o);
-    if (lane == 0) status[msg] = st;
+    if (!st && nd) {
+      // hand the part's pieces to the copy kernel; past the launch's room,
+      // move them here (reads of them took the input bytes, so late is fine)
+      uint32_t base = 0;
+      if (lane == 0) base = atomicAdd(nlits, nd);
+      base = (uint32_t)__builtin_amdgcn_readfirstlane((int)base);
+      for (uint32_t i = lane; i < nd; i += 64)
+        if (base + i < lit_cap) lits[base + i] = SnappyLit{s0 + tsrc[i], out + tdst[i], tlen[i]};
+      for (uint32_t i = (base < lit_cap ? lit_cap - base : 0u); i < nd; ++i)
+        for (uint32_t b = lane; b < tlen[i]; b += 64) out[tdst[i] + b] = s0[tsrc[i] + b];
+    }
+    if (lane == 0) {
+      status[msg] = st;
+      if (st && nbad) atomicAdd(nbad, 1ull);
+    }
+#ifdef PSG_SNAPPY_PROF
+    sp[2] = clock64() - sp_part;
+    if (lane == 0 && msg < 4096)
+      for (int i = 0; i < 8; ++i) g_sprof[msg][i] = sp[i];
+#endif
+    __builtin_amdgcn_wave_barrier();  // the next part rewrites the piece list
+  }
+}
+
+// The deferred literals, chip-wide: a literal is cut into 16-B units
+// aligned to its destination; a workgroup moves 256 units (4 KB) per chunk,
+// chunks numbered across literals and dealt round-robin to the grid (the
+// literals' chunk counts are scanned in LDS, 256 literals at a time, and a
+// chunk finds its literal by binary search there).  Each lane loads the 5
+// aligned source dwords around its unit and shifts them into place
+// (v_alignbyte): aligned 16-B stores whatever the source offset.  Units at
+// a literal's ends, and ones whose source window would pass the dword
+// holding the literal's last byte, move byte by byte.
+__global__ __launch_bounds__(256) void snappy_lit_kernel(const SnappyLit* __restrict__ lits,
+                                                         const uint32_t* __restrict__ nlits,
+                                                         uint32_t lit_cap) {
+  __shared__ uint32_t pre[257];  // chunks before literal i of the batch
+  __shared__ uint32_t wsum[4];
+  const uint32_t n = *nlits < lit_cap ? *nlits : lit_cap;
+  const uint32_t t = threadIdx.x, lane = t & 63, w = t >> 6;
+  uint64_t base = 0;  // chunks of the batches before
+  for (uint32_t b0 = 0; b0 < n; b0 += 256) {
+    uint32_t nch = 0;
+    if (b0 + t < n) {
+      const SnappyLit L = lits[b0 + t];
+      const uintptr_t A = (uintptr_t)L.dst & ~(uintptr_t)15;
+      const uint64_t units = ((uintptr_t)L.dst + L.len - A + 15) / 16;
+      nch = (uint32_t)((units + kLitUnits - 1) / kLitUnits);
+    }
+    // block exclusive scan of nch
+    uint32_t x = nch;
+    for (int o = 1; o < 64; o <<= 1) {
+      const uint32_t y = (uint32_t)__shfl_up((int)x, o, 64);
+      if (lane >= (uint32_t)o) x += y;
+    }
+    if (lane == 63) wsum[w] = x;
+    __syncthreads();
+    uint32_t off = 0;
+    for (uint32_t v = 0; v < w; ++v) off += wsum[v];
+    pre[t + 1] = off + x;
+    if (t == 0) pre[0] = 0;
+    __syncthreads();
+    const uint32_t nb = n - b0 < 256u ? n - b0 : 256u;
+    const uint32_t tot = pre[nb];
+    // this block's chunks g = base + c, c = 0..tot-1, g = blockIdx.x mod grid
+    for (uint32_t c = (uint32_t)((blockIdx.x + gridDim.x - base % gridDim.x) % gridDim.x); c < tot;
+         c += gridDim.x) {
+      uint32_t lo = 0, hi = nb;  // last literal with pre[i] <= c
+      while (hi - lo > 1) {
+        const uint32_t mid = (lo + hi) >> 1;
+        if (pre[mid] <= c) lo = mid; else hi = mid;
+      }
+      const SnappyLit L = lits[b0 + lo];
+      const uintptr_t A = (uintptr_t)L.dst & ~(uintptr_t)15;
+      const uint64_t units = ((uintptr_t)L.dst + L.len - A + 15) / 16;
+      const uint64_t u = (uint64_t)(c - pre[lo]) * kLitUnits + t;
+      if (u >= units) continue;
+      const uintptr_t ua = A + 16 * u;
+      const uintptr_t b0b = ua > (uintptr_t)L.dst ? ua : (uintptr_t)L.dst;
+      const uintptr_t b1 = ua + 16 < (uintptr_t)L.dst + L.len ? ua + 16 : (uintptr_t)L.dst + L.len;
+      const uintptr_t sa = (uintptr_t)L.src + (ua - (uintptr_t)L.dst);  // source of byte ua
+      const uintptr_t a0 = sa & ~(uintptr_t)3;
+      const uintptr_t slast = ((uintptr_t)L.src + L.len - 1) & ~(uintptr_t)3;
+      if (b0b == ua && b1 == ua + 16 && a0 + 16 <= slast) {
+        const uint32_t* wp = (const uint32_t*)a0;
+        const uint32_t sh = (uint32_t)(sa & 3u);
+        uint32_t xw[5];
+#pragma unroll
+        for (int i = 0; i < 5; ++i) xw[i] = wp[i];
+        typedef uint32_t u4 __attribute__((ext_vector_type(4)));
+        u4 v;
+        v.x = __builtin_amdgcn_alignbyte(xw[1], xw[0], sh);
+        v.y = __builtin_amdgcn_alignbyte(xw[2], xw[1], sh);
+        v.z = __builtin_amdgcn_alignbyte(xw[3], xw[2], sh);
+        v.w = __builtin_amdgcn_alignbyte(xw[4], xw[3], sh);
+        *(u4*)ua = v;
+      } else {
+        for (uintptr_t b = b0b; b < b1; ++b) *(uint8_t*)b = L.src[b - (uintptr_t)L.dst];
+      }
+    }
+    base += tot;
+    __syncthreads();  // pre[] is rewritten by the next batch
   }
 }
 
 }  // namespace
 
+// room for 256 deferred pieces per part on average (shared by the launch;
+// past it pieces move in the parse)
+constexpr uint32_t kAvgDef = 256;
+#ifdef PSG_SNAPPY_PROF
+extern "C" int psg_debug_snappy_prof(unsigned long long* out, uint32_t nmsg) {
+  if (nmsg > 4096) nmsg = 4096;
+  return hipMemcpyFromSymbol(out, HIP_SYMBOL(g_sprof), (size_t)nmsg * 64) == hipSuccess ? 0 : -1;
+}
+#endif
+
+size_t snappy_scratch_bytes(uint64_t nmsg) {
+  return 256 + (size_t)nmsg * kAvgDef * sizeof(SnappyLit);
+}
+
 hipError_t launch_snappy(const uint8_t* src, const uint64_t* soff, uint64_t nmsg, uint8_t* dst,
                          const uint64_t* doff, const uint64_t* dcap, int32_t* status,
-                         hipStream_t stream) {
+                         void* scratch, hipStream_t stream, unsigned long long* nbad,
+                         bool pairs) {
   if (nmsg == 0) return hipSuccess;
+  uint32_t* nlits = (uint32_t*)scratch;
+  SnappyLit* lits = (SnappyLit*)((char*)scratch + 256);
+  const uint64_t cap64 = nmsg * kAvgDef;
+  const uint32_t cap = cap64 < 0xffffffffull ? (uint32_t)cap64 : 0xffffffffu;
+  if (nlits) {
+    const hipError_t e = hipMemsetAsync(nlits, 0, 4, stream);
+    if (e != hipSuccess) return e;
+  }
   // 64 KB of LDS per workgroup: two resident per CU
   const uint64_t blocks = nmsg < 512 ? nmsg : 512;
   hipLaunchKernelGGL(snappy_kernel, dim3((uint32_t)blocks), dim3(64), 0, stream, src, soff, dst,
-                     doff, dcap, nmsg, status);
+                     doff, dcap, nmsg, status, nlits ? lits : nullptr, nlits, cap, nbad,
+                     pairs ? 1 : 0);
+  if (!nlits) return hipGetLastError();
+  hipLaunchKernelGGL(snappy_lit_kernel, dim3(1024), dim3(256), 0, stream, lits, nlits, cap);
   return hipGetLastError();
 }
 

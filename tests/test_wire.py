@@ -512,11 +512,90 @@ def test_gpu_snappy_batched_parts_vs_oracle():
     assert st == [_lib.PSG_ERR_SIZE]
 
 
+def _snappy_stream(elems):
+    """A raw snappy stream from ("lit", bytes) / ("copy", offset, length)
+    elements (length <= 64; 2-byte offsets below 65536, else 4-byte), and
+    the bytes it decodes to."""
+    out = bytearray()
+    body = bytearray()
+    for e in elems:
+        if e[0] == "lit":
+            d = e[1]
+            x = len(d) - 1
+            if x < 60:
+                body.append(x << 2)
+            else:
+                nb = 1 if x < 256 else 2 if x < 65536 else 3
+                body.append((59 + nb) << 2)
+                body += x.to_bytes(nb, "little")
+            body += d
+            out += d
+        else:
+            _, off, ln = e
+            if off < 65536:
+                body += bytes([(ln - 1) << 2 | 2]) + off.to_bytes(2, "little")
+            else:
+                body += bytes([(ln - 1) << 2 | 3]) + off.to_bytes(4, "little")
+            for _ in range(ln):
+                out.append(out[len(out) - off])
+    ulen, pre = len(out), bytearray()
+    while True:
+        pre.append((ulen & 0x7F) | (0x80 if ulen > 0x7F else 0))
+        ulen >>= 7
+        if not ulen:
+            break
+    return bytes(pre + body), bytes(out)
+
+
+@pytest.mark.gpu
+def test_gpu_snappy_deferred_literals():
+    """The parse defers literals of >= 2048 bytes to the chip-wide copy
+    kernel: copies that read back into them (wholly, straddling a deferred
+    literal and ring bytes, run-length, past the 64 KB ring), more deferred
+    literals than a part keeps (> 64: the rest move in the parse), literals
+    just under the threshold, and destinations at every alignment."""
+    rng = np.random.default_rng(8)
+    parts, datas = [], []
+    for variant in range(4):
+        el = []
+        nlit = 80 if variant == 0 else 12
+        for i in range(nlit):
+            ln = int(rng.choice([2047, 2048, 2049, 3000, 4096 + 13, 65536]))
+            el.append(("lit", rng.integers(0, 256, ln, dtype=np.uint8).tobytes()))
+            if i:
+                # back into the previous literal, straddling into this one,
+                # run-length, short literal between
+                el.append(("copy", ln + 5, 64))
+                el.append(("copy", 40, 64))
+                el.append(("copy", 1, 17))
+                el.append(("lit", rng.integers(0, 256, 9, dtype=np.uint8).tobytes()))
+                el.append(("copy", 3000, 33))
+        if variant == 1:
+            el.append(("copy", 70000, 64))  # past the ring, into a deferred literal
+        comp, want = _snappy_stream(el)
+        assert O.snappy_uncompress(comp) == want
+        parts.append(comp)
+        datas.append(want)
+    # an odd-sized lead part shifts every later destination's alignment
+    lead = _snappy_stream([("lit", b"xyz")])
+    parts.insert(0, lead[0])
+    datas.insert(0, lead[1])
+    got, st = _gpu_snappy(parts, [len(d) for d in datas])
+    assert st == [0] * len(parts)
+    for g, d in zip(got, datas):
+        assert g == d
+    # the large cfg2-shaped part: incompressible keys, one literal per block
+    big = np.sort(rng.integers(0, 1 << 63, 131072, dtype=np.uint64)).tobytes()
+    got, st = _gpu_snappy([O.snappy_compress(big)] * 3, [len(big)] * 3)
+    assert st == [0, 0, 0] and all(g == big for g in got)
+
+
 @pytest.mark.gpu
 def test_gpu_push_compressed_matches_plain_push():
     """psg_push_compressed: snappy parts off the wire (keys + m value parts),
     decompressed on the device and merged -- the same bits as plain pushes;
-    a corrupt part and inconsistent part sizes are refused."""
+    a corrupt part (reported by received) and inconsistent part sizes (at
+    the push) are refused."""
     import ctypes as C
     import torch
     assert torch.cuda.is_available()
@@ -544,6 +623,19 @@ def test_gpu_push_compressed_matches_plain_push():
     _, _, _, want, _ = O.aggregate(D, 0, (1 << 64) - 1, pushes)
     assert np.array_equal(got.view(np.uint32), want[0].view(np.uint32))
     k, vals = pushes[0]
-    assert cpush(4, k, vals, corrupt=True) == _lib.PSG_ERR_ARG
-    assert cpush(4, k, [vals[0][:-1]]) == _lib.PSG_ERR_SIZE
+    # a corrupt part decodes asynchronously: psg_received of its time
+    # reports it (PSG_ERR_ARG), beside good pushes of the same time
+    _lib.check(cpush(4, pushes[1][0], pushes[1][1]))
+    assert cpush(4, k, vals, corrupt=True) == _lib.PSG_OK
+    with pytest.raises(_lib.PSGError) as e:
+        v.received(4)
+    assert e.value.status == _lib.PSG_ERR_ARG
+    # declared sizes are checked on the host, at the push
+    assert cpush(5, k, [vals[0][:-1]]) == _lib.PSG_ERR_SIZE
+    # the context goes on: a later time merges as before
+    for kk, vv in pushes[:2]:
+        _lib.check(cpush(6, kk, vv))
+    (_, got), = v.received(6)
+    _, _, _, want, _ = O.aggregate(D, 0, (1 << 64) - 1, pushes[:2])
+    assert np.array_equal(got.view(np.uint32), want[0].view(np.uint32))
     v.close()

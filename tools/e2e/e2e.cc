@@ -7,6 +7,7 @@
 #include <chrono>
 #include <cstdint>
 #include <cstdio>
+#include <cstring>
 #include <vector>
 
 #include "../../include/psg.h"
@@ -75,6 +76,91 @@ extern "C" int psg_e2e_darling(int device, unsigned flags, const uint64_t* D, si
                 .count();
   }
   if (rc) fprintf(stderr, "psg_e2e_darling: %s\n", psg_last_error());
+  psg_destroy(c);
+  return rc;
+}
+
+// The worker's side of a compressed message (SArray::compressTo,
+// shared_array_inl.h:222-230, as Van::send applies it): a raw snappy stream
+// -- varint length, then per 64 KB block greedy 4-byte hash matches as
+// 2-byte-offset copies (<= 64 bytes) and literals between them.  Harness
+// code: it only has to produce valid streams of the usual shape.
+extern "C" size_t psg_e2e_compress(const uint8_t* src, size_t n, uint8_t* dst) {
+  size_t o = 0;
+  for (size_t v = n;;) {
+    const uint8_t b = v & 0x7f;
+    v >>= 7;
+    dst[o++] = (uint8_t)(b | (v ? 0x80 : 0));
+    if (!v) break;
+  }
+  std::vector<int32_t> h(1 << 14);
+  auto lit = [&](size_t a, size_t b) {
+    if (a == b) return;
+    const size_t x = b - a - 1;
+    if (x < 60) {
+      dst[o++] = (uint8_t)(x << 2);
+    } else {
+      const int nb = x < 256 ? 1 : x < 65536 ? 2 : x < (1u << 24) ? 3 : 4;
+      dst[o++] = (uint8_t)((59 + nb) << 2);
+      for (int i = 0; i < nb; ++i) dst[o++] = (uint8_t)(x >> (8 * i));
+    }
+    memcpy(dst + o, src + a, b - a);
+    o += b - a;
+  };
+  for (size_t blk = 0; blk < n; blk += 65536) {
+    const size_t end = blk + 65536 < n ? blk + 65536 : n;
+    std::fill(h.begin(), h.end(), -1);
+    size_t i = blk, pend = blk;
+    while (i + 4 <= end) {
+      uint32_t w;
+      memcpy(&w, src + i, 4);
+      const uint32_t k = (w * 0x1e35a7bdu) >> 18;
+      const int32_t c = h[k];
+      h[k] = (int32_t)(i - blk);
+      if (c >= 0 && memcmp(src + blk + c, src + i, 4) == 0) {
+        size_t m = 4;
+        while (i + m < end && m < 64 && src[blk + c + m] == src[i + m]) ++m;
+        lit(pend, i);
+        const size_t off = i - blk - (size_t)c;
+        dst[o++] = (uint8_t)(2 | ((m - 1) << 2));
+        dst[o++] = (uint8_t)off;
+        dst[o++] = (uint8_t)(off >> 8);
+        i += m;
+        pend = i;
+      } else {
+        ++i;
+      }
+    }
+    lit(pend, end);
+  }
+  return o;
+}
+
+// The aggregate from compressed messages (Van::recv's uncompressFrom,
+// van.cc:204-214, then setValue): each push's key part and value part,
+// pinned, through psg_push_compressed, then received(t).
+extern "C" int psg_e2e_compressed(int device, int dtype, unsigned flags, const uint64_t* D,
+                                  size_t nd, int npush, const void* const* ckeys,
+                                  const size_t* ckn, const void* const* cvals, const size_t* cvn,
+                                  void* out, int reps, double* ms) {
+  psg_ctx* c = nullptr;
+  int rc = psg_create(device, dtype, flags, &c);
+  if (rc) return rc;
+  rc = psg_key_union(c, 0, D, nd);
+  const uint64_t all = ~0ull;
+  for (int r = 0; rc == 0 && r < reps; ++r) {
+    const auto t0 = std::chrono::steady_clock::now();
+    for (int p = 0; rc == 0 && p < npush; ++p) {
+      const void* v[1] = {cvals[p]};
+      const size_t vn[1] = {cvn[p]};
+      rc = psg_push_compressed(c, 0, r, 0, all, ckeys[p], ckn[p], 1, v, vn);
+    }
+    void* o[1] = {out};
+    if (rc == 0) rc = psg_received(c, r, 1, o);
+    ms[r] = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0)
+                .count();
+  }
+  if (rc) fprintf(stderr, "psg_e2e_compressed: %s\n", psg_last_error());
   psg_destroy(c);
   return rc;
 }

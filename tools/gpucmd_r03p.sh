@@ -1,0 +1,12 @@
+# snappy copy kernel with scanned chunks; profile of the compressed e2e mode
+set -o pipefail
+export TMPDIR=/tmp
+O=gpurun_out/r03p; mkdir -p $O
+timeout -k 10 600 python3 -u -m pytest tests/test_wire.py -x -q -m gpu --timeout 300 --timeout-method thread > $O/tests.log 2>&1 || { echo TESTFAIL; tail -40 $O/tests.log; exit 1; }
+tail -2 $O/tests.log
+timeout -k 10 300 rocprofv3 --kernel-trace --hip-runtime-trace --memory-copy-trace --stats --output-format csv -d $O/prof -o run -- python3 tools/e2e/run_e2e.py 5 compressed,pinned > $O/e2e.json 2> $O/e2e.err || { echo "e2e failed"; tail -5 $O/e2e.err; exit 1; }
+python3 -c "import json;d=json.load(open('$O/e2e.json'));[print(k,'%.3g'%v['value'],'%.3f ms'%v['ms_per_aggregate']) for k,v in d['modes'].items()]"
+head -12 $O/prof/run_kernel_stats.csv
+true
+timeout -k 10 300 python3 tools/run_rows.py > $O/rows.json 2> $O/rows.err || { echo "rows failed"; tail -5 $O/rows.err; exit 1; }
+python3 -c "import json;d=json.load(open('$O/rows.json'));[print(k,'%.4f ms'%v['ms'],'%.1f GB/s'%v['GBps']) for k,v in d.items() if 'snappy' in k]"
