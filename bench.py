@@ -87,8 +87,11 @@ def parse():
                     help=argparse.SUPPRESS)  # internal: the unsliced leg in its own process
     ap.add_argument("--cpu-seconds", type=float, default=10.0)
     ap.add_argument("--no-cpu-baseline", action="store_true")
-    ap.add_argument("--arena", action="store_true",
-                    help="stage each aggregate's pushes in one key / value arena (A/B)")
+    ap.add_argument("--layout", choices=["arena", "separate"], default="arena",
+                    help="where the pushes sit in HBM: 'arena' = each aggregate's push keys "
+                         "back to back in one allocation and each value array likewise (a "
+                         "server's receive buffer; the layout psg_exchange delivers), "
+                         "'separate' = one allocation per push array")
     ap.add_argument("--plan-flags", type=lambda x: int(x, 0), default=0,
                     help="kernel-form overrides of include/psg.h (A/B measurements only)")
     ap.add_argument("--no-server-api", action="store_true",
@@ -114,7 +117,7 @@ def to_dev(a, dev):
 
 
 PLAN_FLAGS = 0  # --plan-flags
-ARENA = False   # --arena
+ARENA = True    # --layout arena
 
 
 def make_plan(insts, dev, local):
@@ -128,8 +131,11 @@ def make_plan(insts, dev, local):
         dD = to_dev(D, dev)
         if ARENA:
             # the aggregate's pushes in one key arena and one value arena per
-            # value array, back to back (the layout of a server's ingest
-            # staging), as views
+            # value array, back to back, as views: a server receives an
+            # aggregate's pushes into one buffer (psg_exchange's receive
+            # buffer has exactly this layout).  Same bytes and kernels as
+            # --layout separate; sparse many-push tiles (cfg5) touch far fewer
+            # translation entries this way
             ka = to_dev(np.concatenate([k for k, _ in pushes]) if pushes else
                         np.zeros(0, np.uint64), dev)
             m = len(pushes[0][1]) if pushes else 0
@@ -187,7 +193,7 @@ def main():
     global PLAN_FLAGS, ARENA
     args = parse()
     PLAN_FLAGS = args.plan_flags
-    ARENA = args.arena
+    ARENA = args.layout == "arena"
     if args.cfg5_unsliced_child:
         return unsliced_child_main(args)
     import torch
@@ -231,6 +237,11 @@ def main():
         insts = [synth.uniform_pushes(seed=5 + j) for j in range(args.batch)]
     log(f"rank {rank}: generated {args.batch} {wl} aggregates in {time.time() - t0:.1f}s")
 
+    if wl == "cfg4":
+        # the bench's pushes are fixed for the plan's lifetime: the dense
+        # kernel (no key reads) is allowed (include/psg.h PSG_STATIC_KEYS)
+        from parameter_server_amd._lib import PSG_STATIC_KEYS
+        PLAN_FLAGS |= PSG_STATIC_KEYS
     plan, keep, jobs = make_plan(insts, dev, local)
     stream = torch.cuda.current_stream()
 
@@ -288,6 +299,7 @@ def main():
                                                      batch=args.batch),
             "global_batch": args.batch * world,
             "kv_per_step": kv_all,
+            "input_layout": args.layout,
             "parallelism": (f"key-range shards evenDivide({world}); worker-sliced ingress, "
                             "no data-path collective"),
         },

@@ -83,6 +83,15 @@ typedef enum psg_dtype { PSG_F32 = 0, PSG_F64 = 1 } psg_dtype;
 #define PSG_NO_DENSE 0x40000u     /* never the dense (contiguous-slice) kernel */
 #define PSG_NO_ZERO_COPY 0x80000u /* context: DMA copies instead of GPU reads of pinned memory */
 #define PSG_NO_INDEX 0x100000u    /* plan: no resident bucket index (tables built per run) */
+/* Plan option (psg_plan_create): the caller promises that the push KEYS at
+ * the job's device pointers stay as they were at creation for the plan's
+ * lifetime (values may change between runs).  Only then may the plan take
+ * the dense kernel for pushes that are contiguous slices of D: that kernel
+ * reads no push keys, so it cannot see a key that changed.  Without this
+ * flag every run partitions and order-checks the keys it merges, and a
+ * changed key is reported through psg_plan_matched.  (D itself is always
+ * fixed for a plan's lifetime: its bucket index is built at creation.) */
+#define PSG_STATIC_KEYS 0x200000u
 
 int psg_abi_version(void);
 const char* psg_status_string(int status);

@@ -51,6 +51,8 @@ PSG_GROUP64 = 0x20000
 PSG_NO_DENSE = 0x40000
 PSG_NO_ZERO_COPY = 0x80000
 PSG_NO_INDEX = 0x100000
+# plan option: push keys fixed for the plan's lifetime (enables the dense kernel)
+PSG_STATIC_KEYS = 0x200000
 MAX_VALUE_ARRAYS = 4
 
 # Every symbol include/psg.h declares, with its ctypes signature.

@@ -155,12 +155,15 @@ __device__ __forceinline__ void stream_item(const JobDev& J, uint32_t p, uint32_
   const uint64_t i0 = (uint64_t)c * kStreamChunk;
   const uint32_t cl = (uint32_t)(n - i0 < kStreamChunk ? n - i0 : kStreamChunk);
   const bool last = i0 + cl == n;
-  // the chunk's keys into LDS (4 per lane); +inf past the push's end
+  // the chunk's keys (kKPL per lane, element j*64 + lane: every load is one
+  // coalesced 512-B wave access), then into LDS in order; +inf past the end
   uint64_t k[kKPL];
+  const __attribute__((address_space(1))) uint64_t* Sg =
+      (const __attribute__((address_space(1))) uint64_t*)(S + i0);
 #pragma unroll
   for (int j = 0; j < kKPL; ++j) {
-    const uint32_t x = kKPL * (uint32_t)lane + j;
-    k[j] = x < cl ? S[i0 + x] : ~0ull;
+    const uint32_t x = 64u * j + (uint32_t)lane;
+    k[j] = x < cl ? Sg[x] : ~0ull;
   }
   // T0 = (splitters <= S[i0-1]) - 1: an interpolated guess checked against a
   // window of 64 splitters around it (murmur-hashed keys and D are near-
@@ -200,7 +203,7 @@ __device__ __forceinline__ void stream_item(const JobDev& J, uint32_t p, uint32_
   // stores before the wave's reads of them: LDS accesses of one wave are
   // ordered; the fences keep the compiler from moving the reads up
 #pragma unroll
-  for (int j = 0; j < kKPL; ++j) ck[kKPL * lane + j] = k[j];
+  for (int j = 0; j < kKPL; ++j) ck[64 * j + lane] = k[j];
   __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
   __builtin_amdgcn_wave_barrier();
   __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
@@ -229,18 +232,19 @@ __device__ __forceinline__ void stream_item(const JobDev& J, uint32_t p, uint32_
     if (!last && uni64((uint64_t)__shfl((long long)sv, 63, 64)) > klast) break;
   }
   // order check: a key not above its predecessor cannot match
+  // (element j*64 + lane follows lane - 1's element j, or lane 63's
+  // element j - 1, or the previous chunk's last key)
   uint32_t bad = 0;
   {
-    const uint64_t kprev_l = (uint64_t)__shfl_up((long long)k[kKPL - 1], 1, 64);
-    uint64_t prev = lane == 0 ? (i0 > 0 ? S[i0 - 1] : 0ull) : kprev_l;
-    bool has = lane > 0 || i0 > 0;
+    const uint64_t before = i0 > 0 ? uni64(S[i0 - 1]) : 0ull;
 #pragma unroll
     for (int j = 0; j < kKPL; ++j) {
-      if (kKPL * (uint32_t)lane + j < cl) {
-        if (has && !(prev < k[j])) ++bad;
-        prev = k[j];
-        has = true;
-      }
+      const uint64_t up = (uint64_t)__shfl_up((long long)k[j], 1, 64);
+      const uint64_t l63 = j > 0 ? (uint64_t)__shfl((long long)k[j > 0 ? j - 1 : 0], 63, 64)
+                                 : before;
+      const uint64_t prev = lane == 0 ? l63 : up;
+      const bool has = lane > 0 || j > 0 || i0 > 0;
+      if (64u * j + (uint32_t)lane < cl && has && !(prev < k[j])) ++bad;
     }
   }
   if (__ballot(bad != 0) && bad)

@@ -555,6 +555,7 @@ struct PendingPush {
   void* vblock = nullptr;  // the m value arrays
   size_t vbytes = 0;
   void* d_vals[psg::kMaxM] = {};
+  int m = 0;  // value arrays of this push (the aggregate's list grows to the largest)
   uint64_t n = 0;
   // a contiguous slice of the server keys (psg_push's dense test): the merge
   // reads D[dpos, dpos + n) of the aggregate's range in place of the keys
@@ -573,12 +574,17 @@ struct PendingPush {
   uint64_t cdst[psg::kMaxM + 1] = {}, ccap[psg::kMaxM + 1] = {};
 };
 
+// recved_val_[t] (kv_vector.h:189-196, 110-129): a list of value arrays that
+// grows when a push brings more arrays than the earlier ones; array i is
+// assigned by the first push holding an i-th array and added to by the later
+// ones that hold one (a push without it leaves it alone)
 struct Aggregate {
-  int chl = 0, m = 0;
+  int chl = 0, m = 0;                // m: arrays so far (the largest push's)
   size_t lo = 0, hi = 0;
   void* d_out[psg::kMaxM] = {};
   std::vector<PendingPush> pending;
   uint64_t folded = 0;               // pushes already merged into d_out
+  uint64_t folded_arr[psg::kMaxM] = {};  // of them, those holding array i
   uint64_t expected_total = 0;
   // device: [0] pushed keys not matched so far, [1] compressed parts that
   // failed to decode (psg_push_compressed reports them here, asynchronously)
@@ -888,31 +894,49 @@ struct psg_ctx {
       size_t dbytes = 0;
       if (int rc = decode_pending(a, take, &dblk, &dbytes)) return rc;
       if (int rc = join_copy()) return rc;
-      JobSpec js;
-      js.keys = ch[a.chl].d_keys + a.lo;
-      js.nslots = a.hi - a.lo;
-      js.flags = (flags & PSG_PARALLEL_MATCH ? psg::kFlagParallel : 0u) |
-                 (a.folded > 0 ? psg::kFlagCont : 0u);
-      bool dense = true;
-      for (size_t p = 0; p < take; ++p) {
-        const PendingPush& pp = a.pending[p];
-        js.pkeys.push_back(pp.kd ? pp.kd : pp.keys->d);
-        for (int i = 0; i < a.m; ++i) js.pvals.push_back(pp.d_vals[i]);
-        js.pn.push_back(pp.n);
-        dense = dense && pp.dense;
+      // one job over every push and all arrays when each push holds all of
+      // them and every array has the same history (the reference's apps:
+      // always); otherwise one single-array job per array over the pushes
+      // holding it (kv_vector.h:189-196).  Job 0 holds every push either way
+      // (each has array 0): its unmatched count is the launch's
+      bool uniform = true;
+      for (size_t p = 0; p < take; ++p) uniform = uniform && a.pending[p].m == a.m;
+      for (int i = 1; i < a.m; ++i)
+        uniform = uniform && (a.folded_arr[i] > 0) == (a.folded_arr[0] > 0);
+      const int jm = uniform ? a.m : 1;
+      std::vector<JobSpec> jobs;
+      for (int i = 0; i < (uniform ? 1 : a.m); ++i) {
+        JobSpec js;
+        js.keys = ch[a.chl].d_keys + a.lo;
+        js.nslots = a.hi - a.lo;
+        js.flags = (flags & PSG_PARALLEL_MATCH ? psg::kFlagParallel : 0u) |
+                   (a.folded_arr[i] > 0 ? psg::kFlagCont : 0u);
+        bool dense = true;
+        for (size_t p = 0; p < take; ++p) {
+          const PendingPush& pp = a.pending[p];
+          if (pp.m <= i) continue;
+          js.pkeys.push_back(pp.kd ? pp.kd : pp.keys->d);
+          for (int k = 0; k < jm; ++k) js.pvals.push_back(pp.d_vals[i + k]);
+          js.pn.push_back(pp.n);
+          js.dpos.push_back(pp.dpos);
+          dense = dense && pp.dense;
+        }
+        if (js.pn.empty()) continue;  // no push of this launch holds array i
+        // every push a contiguous slice: the dense kernel (no key reads)
+        js.dense = dense;
+        if (!dense) js.dpos.clear();
+        for (int k = 0; k < jm; ++k) js.out.push_back(outs ? outs[i + k] : a.d_out[i + k]);
+        jobs.push_back(std::move(js));
       }
-      // every push a contiguous slice: the dense kernel (no key reads)
-      if (dense) {
-        js.dense = true;
-        for (size_t p = 0; p < take; ++p) js.dpos.push_back(a.pending[p].dpos);
-      }
-      for (int i = 0; i < a.m; ++i) js.out.push_back(outs ? outs[i] : a.d_out[i]);
-      if (int rc = table.build(device, dtype, a.m, {js}, stream, true)) return rc;
+      if (int rc = table.build(device, dtype, jm, jobs, stream, true)) return rc;
       if (int rc = table.run(stream)) return rc;
       HIP_TRY(psg::launch_unmatched(table.d_jobs, 0, table.info[0].np, a.d_bad, stream));
       if (bad_host && take == a.pending.size())
         if (int rc = d2h(bad_host, a.d_bad, 16)) return rc;
-      for (size_t p = 0; p < take; ++p) release_push(a.pending[p]);
+      for (size_t p = 0; p < take; ++p) {
+        for (int i = 0; i < a.pending[p].m; ++i) ++a.folded_arr[i];
+        release_push(a.pending[p]);
+      }
       a.pending.erase(a.pending.begin(), a.pending.begin() + take);
       a.folded += take;
       dev_put(dblk, dbytes);  // after the join: `stream` is past the decode
@@ -1014,7 +1038,9 @@ int psg_plan_create(int device, int dtype, int m, unsigned flags,
     for (int i = 0; i < m; ++i) s.out.push_back(J.out[i]);
     bytes += J.nslots * (8 + m * sv);
   }
-  if (!(flags & PSG_NO_DENSE))
+  // the dense kernel reads no push keys: only for keys the caller fixed
+  // (PSG_STATIC_KEYS, psg.h); otherwise every run re-checks them
+  if ((flags & PSG_STATIC_KEYS) && !(flags & PSG_NO_DENSE))
     if (int rc = detect_dense(specs)) return rc;
   psg_plan* p = new psg_plan();
   p->table.read_knobs(flags);
@@ -1357,7 +1383,6 @@ int check_push(psg_ctx* c, int chl, int time, uint64_t kb, uint64_t ke, size_t n
     if (A.lo != *lo || A.hi != *hi)  // CHECK_EQ(aligned.first, stored) kv_vector.h:199
       return fail(PSG_ERR_RANGE, "time %d: range [%zu,%zu) != [%zu,%zu)", time, *lo, *hi,
                   A.lo, A.hi);
-    if (A.m != m) return fail(PSG_ERR_ARG, "time %d: %d value arrays != %d", time, m, A.m);
   }
   return PSG_OK;
 }
@@ -1420,11 +1445,8 @@ int psg_ctx::aggregate_for(int chl, int time, uint64_t kb, uint64_t ke, int m,
     const size_t hi = std::lower_bound(h, h + C.n, ke) - h;
     Aggregate A;
     A.chl = chl;
-    A.m = m;
     A.lo = lo;
     A.hi = hi;
-    for (int i = 0; i < m; ++i)
-      if (int rc = dev_get((hi - lo) * vsize(dtype), &A.d_out[i], stream)) return rc;
     // zeroed on `copy`: the dense pushes' order checks and the compressed
     // pushes' decodes add to it there; every reader on `stream` runs after
     // a join_copy
@@ -1432,7 +1454,12 @@ int psg_ctx::aggregate_for(int chl, int time, uint64_t kb, uint64_t ke, int m,
     HIP_TRY(hipMemsetAsync(A.d_bad, 0, 16, copy));
     ait = agg.emplace(time, A).first;
   }
-  *out = &ait->second;
+  Aggregate& A = ait->second;
+  // a push with more value arrays than the earlier ones extends the list
+  // (recved_val_[t].push_back, kv_vector.h:118-125,193-194)
+  for (; A.m < m; ++A.m)
+    if (int rc = dev_get((A.hi - A.lo) * vsize(dtype), &A.d_out[A.m], stream)) return rc;
+  *out = &A;
   return PSG_OK;
 }
 
@@ -1443,6 +1470,7 @@ int psg_ctx::push_values(int chl, int time, uint64_t kb, uint64_t ke, const KeyR
   PendingPush pp;
   if (comp) pp = *comp;  // the compressed parts to decode
   pp.n = n;
+  pp.m = m;
   pp.keys = keys;
   pp.sblock = sblock;
   pp.sbytes = sbytes;

@@ -2,8 +2,8 @@
 
 Integer/key outputs and float sums are compared bit for bit (the kernels
 fold in the reference's push order with IEEE adds, so the tolerance the
-north star allows, 1e-6 relative, is not needed); NaNs are compared as NaN
-masks because payload propagation is not part of the contract.
+north star allows, 1e-6 relative, is not needed); NaN payloads are
+compared bit for bit too (assert_bitexact).
 """
 import json
 import os
@@ -373,22 +373,44 @@ def test_plan_batched_jobs_and_dense(torch_cuda):
              synth.dense_pushes(npush=8, n=1 << 20),
              synth.overlap_pushes(4, npush=40, n=3000, overlap=0.5),
              synth.zipf_pushes(3, npush=16, n=8192)]
-    plan, keep = plan_for(torch, cases)
+    from parameter_server_amd._lib import PSG_STATIC_KEYS
+    for flags in (PSG_STATIC_KEYS, 0):  # dense job allowed / never
+        plan, keep = plan_for(torch, cases, flags=flags)
+        plan.run()
+        mt = plan.matched()
+        assert mt.tolist() == [k.size for _, ps in cases for k, _ in ps]
+        outs = keep[3::4]
+        for (D, pushes), out in zip(cases, outs):
+            _, _, _, want, _ = O.aggregate(D, *ALL, pushes)
+            assert_bitexact(out[0].cpu().numpy()[: D.size], want[0])
+        plan.close()
+
+
+def test_plan_changed_slice_keys_are_reported(torch_cuda):
+    """a plan over contiguous-slice pushes created WITHOUT
+    PSG_STATIC_KEYS re-checks the keys every run, so a push key changed
+    after creation (here: one key of a slice moved off D) is reported
+    unmatched by the next run instead of being folded silently."""
+    torch = torch_cuda
+    from parameter_server_amd import synth
+    D, pushes = synth.dense_pushes(npush=4, n=1 << 16)
+    plan, keep = plan_for(torch, [(D, pushes)])
     plan.run()
-    mt = plan.matched()
-    assert mt.tolist() == [k.size for _, ps in cases for k, _ in ps]
-    outs = keep[3::4]
-    for (D, pushes), out in zip(cases, outs):
-        _, _, _, want, _ = O.aggregate(D, *ALL, pushes)
-        assert_bitexact(out[0].cpu().numpy()[: D.size], want[0])
+    assert plan.matched().tolist() == [1 << 16] * 4
+    keep[1][2][777] = int(D[777]) * 1000 + 3  # not a server key any more
+    plan.run()
+    mt = plan.matched().tolist()
+    assert mt[2] < (1 << 16) and mt[:2] == [1 << 16] * 2 and mt[3] == 1 << 16
+    plan.close()
 
 
 def test_plan_cfg4_full_dense(torch_cuda):
     """cfg4 at its full size: 8 pushes x 16 M contiguous keys."""
     torch = torch_cuda
     from parameter_server_amd import synth
+    from parameter_server_amd._lib import PSG_STATIC_KEYS
     D, pushes = synth.dense_pushes()
-    plan, keep = plan_for(torch, [(D, pushes)])
+    plan, keep = plan_for(torch, [(D, pushes)], flags=PSG_STATIC_KEYS)
     plan.run()
     assert plan.matched().tolist() == [1 << 24] * 8
     _, _, _, want, _ = O.aggregate(D, *ALL, pushes)
@@ -416,8 +438,9 @@ def test_plan_dense_slices(torch_cuda, dtype, parallel):
     dense = (D, [(D[a:b], vals(b - a)) for a, b in sl])
     near_k = np.delete(D[200:5200], 77)
     near = (D, [(D[0:3000], vals(3000)), (near_k, vals(near_k.size))])
+    from parameter_server_amd._lib import PSG_STATIC_KEYS
     for cases in ([dense], [dense, near]):
-        plan, keep = plan_for(torch, cases, dtype=dtype, parallel=parallel)
+        plan, keep = plan_for(torch, cases, dtype=dtype, parallel=parallel, flags=PSG_STATIC_KEYS)
         for rep in range(2):
             plan.run()
             mt = plan.matched().tolist()
@@ -871,3 +894,28 @@ def test_fold_ieee_corner_values(torch_cuda, dtype, parallel):
     out = run_ctx(D, [(k, vs) for k, vs in pushes], dtype=dtype, parallel=parallel)
     for i in range(2):
         assert_bitexact(np.asarray(out[i][1]), np.asarray(want[i], dtype))
+
+
+# ------------------------------- a value-array list that grows within a time
+@pytest.mark.parametrize("parallel", [False, True])
+@pytest.mark.parametrize("flush", [None, 2])
+def test_growing_value_array_list(torch_cuda, parallel, flush):
+    """recved_val_[t] grows when a later push of the same time brings more
+    value arrays (kv_vector.h:110-129 / 189-196): array i is assigned by the
+    first push holding an i-th array and added to only by later pushes that
+    hold one (serial: with the dense += over the range, so a push without
+    the key adds +0.0; a push without array i adds nothing to it).  So array
+    i is exactly the aggregate of the pushes holding it: checked bit for bit
+    against the oracle run over that subset, with single-launch and
+    continued (2 pushes per launch) flushes."""
+    mseq = [1, 2, 1, 3, 2, 1, 3]
+    dtype = np.float64 if parallel else np.float32
+    D, full = random_case(77, dtype, 3, len(mseq), 0.3, 4000)
+    pushes = [(k, vs[:mp]) for (k, vs), mp in zip(full, mseq)]
+    out = run_ctx(D, pushes, dtype=dtype, parallel=parallel, flush=flush)
+    assert len(out) == max(mseq)
+    for i in range(max(mseq)):
+        sub = [(k, [vs[i]]) for k, vs in pushes if len(vs) > i]
+        rc, lo, hi, want, _ = O.aggregate(D, *ALL, sub, parallel, 1, dtype)
+        assert rc == 0 and list(out[i][0]) == [lo, hi]
+        assert_bitexact(out[i][1], want[0])
