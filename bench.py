@@ -92,6 +92,8 @@ def parse():
                          "back to back in one allocation and each value array likewise (a "
                          "server's receive buffer; the layout psg_exchange delivers), "
                          "'separate' = one allocation per push array")
+    ap.add_argument("--arena-pushes", type=int, default=0,
+                    help=argparse.SUPPRESS)  # A/B: pushes per arena allocation (0 = all)
     ap.add_argument("--plan-flags", type=lambda x: int(x, 0), default=0,
                     help="kernel-form overrides of include/psg.h (A/B measurements only)")
     ap.add_argument("--no-server-api", action="store_true",
@@ -118,6 +120,7 @@ def to_dev(a, dev):
 
 PLAN_FLAGS = 0  # --plan-flags
 ARENA = True    # --layout arena
+ARENA_PUSHES = 0  # --arena-pushes
 
 
 def make_plan(insts, dev, local):
@@ -136,13 +139,16 @@ def make_plan(insts, dev, local):
             # buffer has exactly this layout).  Same bytes and kernels as
             # --layout separate; sparse many-push tiles (cfg5) touch far fewer
             # translation entries this way
-            ka = to_dev(np.concatenate([k for k, _ in pushes]) if pushes else
-                        np.zeros(0, np.uint64), dev)
             m = len(pushes[0][1]) if pushes else 0
-            va = [to_dev(np.concatenate([vs[i] for _, vs in pushes]), dev) for i in range(m)]
-            offs = np.concatenate([[0], np.cumsum([k.size for k, _ in pushes])]).astype(np.int64)
-            pk = [ka[offs[p]:offs[p + 1]] for p in range(len(pushes))]
-            pv = [[a[offs[p]:offs[p + 1]] for a in va] for p in range(len(pushes))]
+            step = ARENA_PUSHES or max(1, len(pushes))
+            pk, pv = [], []
+            for c0 in range(0, len(pushes), step):
+                part = pushes[c0:c0 + step]
+                ka = to_dev(np.concatenate([k for k, _ in part]), dev)
+                va = [to_dev(np.concatenate([vs[i] for _, vs in part]), dev) for i in range(m)]
+                offs = np.concatenate([[0], np.cumsum([k.size for k, _ in part])]).astype(np.int64)
+                pk += [ka[offs[p]:offs[p + 1]] for p in range(len(part))]
+                pv += [[a[offs[p]:offs[p + 1]] for a in va] for p in range(len(part))]
         else:
             pk = [to_dev(k, dev) for k, _ in pushes]
             pv = [[to_dev(v, dev) for v in vs] for _, vs in pushes]
@@ -190,10 +196,11 @@ def timed_steps(plan, K, W, stream, dist):
 
 
 def main():
-    global PLAN_FLAGS, ARENA
+    global PLAN_FLAGS, ARENA, ARENA_PUSHES
     args = parse()
     PLAN_FLAGS = args.plan_flags
     ARENA = args.layout == "arena"
+    ARENA_PUSHES = args.arena_pushes
     if args.cfg5_unsliced_child:
         return unsliced_child_main(args)
     import torch

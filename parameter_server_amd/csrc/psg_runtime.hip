@@ -674,6 +674,26 @@ struct psg_ctx {
   size_t pool_bytes = 0;
   std::vector<hipEvent_t> free_ev;
   static constexpr size_t kPoolCap = size_t(8) << 30;
+  // ---- slabs: blocks up to kSlabBlock bytes (staged pushes, cached keys,
+  // aggregates of a shard's range) are carved from kSlab-byte allocations
+  // by a bump pointer and then cycle through the pool (never freed on their
+  // own), so an aggregate's pushes sit back to back in a few large mappings
+  // instead of one allocation each: the sparse kernel's tiles, which read a
+  // few keys of each of hundreds of pushes, then touch far fewer address
+  // translations (cfg5: 0.99 -> 0.74 ms for the same kernel, DESIGN.md 4.3;
+  // bench.py --layout arena is this layout for the plan API)
+#ifndef PSG_SLAB_BLOCK
+#define PSG_SLAB_BLOCK (size_t(16) << 20)  // A/B builds: 0 = no slabs
+#endif
+  static constexpr size_t kSlab = size_t(256) << 20, kSlabBlock = PSG_SLAB_BLOCK;
+  std::vector<std::pair<char*, size_t>> slabs;
+  char* slab_cur = nullptr;
+  size_t slab_left = 0;
+  bool in_slab(const void* p) const {
+    for (const auto& s : slabs)
+      if ((const char*)p >= s.first && (const char*)p < s.first + s.second) return true;
+    return false;
+  }
 
   int event(hipEvent_t* e) {
     if (!free_ev.empty()) {
@@ -692,9 +712,27 @@ struct psg_ctx {
       *p = it->second.p;
       if (writer != stream) HIP_TRY(hipStreamWaitEvent(writer, it->second.ev, 0));
       free_ev.push_back(it->second.ev);
-      pool_bytes -= it->first;
+      if (!in_slab(*p)) pool_bytes -= it->first;
       pool.erase(it);
       return PSG_OK;
+    }
+    if (b <= kSlabBlock) {
+      if (slab_left < b) {
+        char* sp = nullptr;
+        if (hipMalloc((void**)&sp, kSlab) == hipSuccess) {
+          slabs.emplace_back(sp, kSlab);
+          slab_cur = sp;
+          slab_left = kSlab;
+        } else {
+          (void)hipGetLastError();  // no room for a slab: an allocation of its own
+        }
+      }
+      if (slab_left >= b) {
+        *p = slab_cur;
+        slab_cur += b;
+        slab_left -= b;
+        return PSG_OK;
+      }
     }
     HIP_TRY(hipMalloc(p, b));
     return PSG_OK;
@@ -705,24 +743,29 @@ struct psg_ctx {
     // the block's release event on `stream`
     if (zc.n) (void)join_copy();
     b = align_up(b ? b : 1, 4096);
+    const bool carved = in_slab(p);  // always pooled: its slab stays allocated anyway
     hipEvent_t e = nullptr;
-    if (pool_bytes + b > kPoolCap || event(&e) != PSG_OK ||
+    if ((!carved && pool_bytes + b > kPoolCap) || event(&e) != PSG_OK ||
         hipEventRecord(e, stream) != hipSuccess) {
       if (e) free_ev.push_back(e);
       (void)hipStreamSynchronize(stream);
-      (void)hipFree(p);
+      if (!carved) (void)hipFree(p);  // a carved block is lost until the slab goes
       return;
     }
     pool.emplace(b, Pooled{p, e});
-    pool_bytes += b;
+    if (!carved) pool_bytes += b;
   }
   void pool_release() {
     for (auto& kv : pool) {
-      (void)hipFree(kv.second.p);
+      if (!in_slab(kv.second.p)) (void)hipFree(kv.second.p);
       (void)hipEventDestroy(kv.second.ev);
     }
     pool.clear();
     pool_bytes = 0;
+    for (auto& sl : slabs) (void)hipFree(sl.first);
+    slabs.clear();
+    slab_cur = nullptr;
+    slab_left = 0;
     for (hipEvent_t e : free_ev) (void)hipEventDestroy(e);
     free_ev.clear();
   }

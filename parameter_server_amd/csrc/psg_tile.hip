@@ -22,9 +22,10 @@
 //     is a coalesced 512 B (keys) / 256 B (f32 values) wave access;
 //   * all of a wave's element loads are issued before the tile's bucket
 //     table is built, so they overlap it;
-//   * D goes to LDS; a bucket table (histogram + scan, 2 buckets per slot,
-//     the tile's key range scaled by one high multiply) turns a search into
-//     one table read and one paired key read;
+//   * D goes to LDS; a bucket table (1 bucket per slot, the tile's key range
+//     scaled by one high multiply; a plan's resident index, or built here by
+//     histogram + scan) turns a search into one table read and one paired
+//     key read;
 //   * the fold runs wave by wave (4 barrier steps): rounds are push-major
 //     and waves hold contiguous runs of them, so every slot sees its
 //     contributions in arrival order with no atomics; sums and per-slot
@@ -76,18 +77,20 @@ __device__ __forceinline__ AS1 T* GW(T* p) {
 }
 
 // Two forms, by pushes per group (one lane of wave 0 each):
-//   32 pushes: 1024-slot tiles, 256 threads, 2 buckets per slot;
+//   32 pushes: 1024-slot tiles, 256 threads;
 //   64 pushes (jobs of more than 32 pushes): 2048-slot tiles (kWideSlots),
-//      512 threads, 1 bucket per slot -- each push's piece per tile doubles,
+//      512 threads -- each push's piece per tile doubles,
 //      so its push-uniform rounds are fuller (cfg3: ~30 -> ~60 of 64 lanes).
 constexpr int ts_of(int g) { return g == 64 ? kWideSlots : kTileSlots; }
 constexpr int nt_of(int g) { return ts_of(g) / 4; }
-constexpr int nb_of(int g) { return g == 64 ? ts_of(g) : 2 * ts_of(g); }
+// one bucket per slot in both forms: a plan's resident index is then 2 B per
+// slot of HBM reads per run (2 per slot measured 2.5 % slower on cfg2,
+// profiles/r03_ab_index.txt)
+constexpr int nb_of(int g) { return ts_of(g); }
 constexpr int cb_of(int g) { return ts_of(g) / 64 > 16 ? 5 : 4; }  // round-chunk bits
 static_assert(ts_of(64) <= 0x7ffe, "u16 positions");
 
 typedef unsigned long long u64x2 __attribute__((ext_vector_type(2)));
-typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
 typedef uint32_t u32x2 __attribute__((ext_vector_type(2)));
 
 __device__ __forceinline__ uint32_t uni(uint32_t v) { return __builtin_amdgcn_readfirstlane(v); }
@@ -136,7 +139,7 @@ __global__ __launch_bounds__(nt_of(kGroup), (occupancy<V, M, kGroup>())) void ti
   constexpr int kNB = nb_of(kGroup);   // buckets
   constexpr int kBPT = kNB / kNT;      // bucket-table entries per thread in the scan
   constexpr int kCB = cb_of(kGroup);   // bits of a round's chunk index
-  static_assert(kTS / kNT == 4 && (kBPT == 8 || kBPT == 4), "layout");
+  static_assert(kTS / kNT == 4 && kBPT == 4, "layout");
   // rounds a wave holds per pass: 6 at 8 workgroups per CU (64 VGPRs); the
   // 64-push form runs 7 per CU and affords 8 (4 waves x 8 = 32 rounds: a
   // group of 64 one-round pieces in 2 passes)
@@ -236,16 +239,8 @@ __global__ __launch_bounds__(nt_of(kGroup), (occupancy<V, M, kGroup>())) void ti
   }
   // the resident bucket table (plans): kBPT u16 entries per thread
   const uint32_t* Bg = T.bt;
-  u32x4 btw = {0u, 0u, 0u, 0u};
-  if (Bg) {
-    if constexpr (kBPT == 8) {
-      btw = __builtin_nontemporal_load((const AS1 u32x4*)Bg + tid);
-    } else {
-      const u32x2 h = __builtin_nontemporal_load((const AS1 u32x2*)Bg + tid);
-      btw.x = h.x;
-      btw.y = h.y;
-    }
-  }
+  u32x2 btw = {0u, 0u};
+  if (Bg) btw = __builtin_nontemporal_load((const AS1 u32x2*)Bg + tid);
   V a0[M][4];
 #pragma unroll
   for (int mi = 0; mi < M; ++mi)
@@ -281,10 +276,6 @@ __global__ __launch_bounds__(nt_of(kGroup), (occupancy<V, M, kGroup>())) void ti
   if (Bg) {  // resident table: installed as loaded
     bt32[tid * (kBPT / 2)] = btw.x;
     bt32[tid * (kBPT / 2) + 1] = btw.y;
-    if constexpr (kBPT == 8) {
-      bt32[tid * (kBPT / 2) + 2] = btw.z;
-      bt32[tid * (kBPT / 2) + 3] = btw.w;
-    }
     if (tid == 0) bt[kNB] = (uint16_t)nt;
   } else {
     uint32_t z = 0;  // zero

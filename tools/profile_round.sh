@@ -22,6 +22,9 @@ timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d $OUT/k
 python3 tools/pmc_traffic.py $OUT/pmc/summary.json $BPL tile_kernel profiles/pmc_summary.json > $OUT/pmc_traffic.json || exit 1
 cp profiles/pmc_summary.json $OUT/pmc_summary.json
 PASSES="1 2 3" ./tools/pmc2.sh $OUT/pmc_cfg5 "--workload cfg5" > $OUT/pmc_cfg5.log 2>&1 || { echo "pmc cfg5 failed"; tail -5 $OUT/pmc_cfg5.log; exit 1; }
+BPL5=$(python3 -c "import json;print(json.load(open('$OUT/ktrace_cfg5.json'))['roofline']['bytes_per_launch'])") || exit 1
+python3 tools/pmc_traffic.py $OUT/pmc_cfg5/summary.json $BPL5 tile_packed_kernel profiles/pmc_summary_cfg5.json cfg5 > $OUT/pmc_traffic_cfg5.json || exit 1
+cp profiles/pmc_summary_cfg5.json $OUT/pmc_summary_cfg5.json
 timeout -k 10 600 python3 bench.py > $OUT/bench.json 2> $OUT/bench.err || { echo "bench failed"; tail -5 $OUT/bench.err; exit 1; }
 cat $OUT/bench.json
 echo done
