@@ -140,10 +140,10 @@ int psg_value_copy(psg_ctx* ctx, int chl, size_t off, size_t n, void* out);
  * hipHostRegister) is DMA'd directly, pageable memory is copied into a
  * pinned staging ring whose DMA continues after return.  The merge runs
  * asynchronously on the context's stream and its match check is reported
- * by psg_received for `time`.  Every push of one `time` carries the same m
- * (PSG_ERR_ARG otherwise): the reference would append an aggregate entry
- * per extra value index (kv_vector.h:189-196); a server sends one m per
- * time (Darling: 2), so the aggregate is sized once. */
+ * by psg_received for `time`.  Pushes of one `time` may carry different m:
+ * the aggregate's list of arrays grows to the largest (recved_val_[t],
+ * kv_vector.h:110-129,189-196); array i is assigned by the first push
+ * holding an i-th array and added to by the later pushes holding one. */
 int psg_push(psg_ctx* ctx, int chl, int time, uint64_t kb, uint64_t ke,
              const uint64_t* keys, size_t n, int m, const void* const* vals);
 

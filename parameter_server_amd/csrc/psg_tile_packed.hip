@@ -223,6 +223,11 @@ __global__ __launch_bounds__(kNT, (occupancy<V, M>())) void tile_packed_kernel(
 #pragma unroll
     for (int j = 0; j < 4; ++j) d[j] = s0i + j < nt ? G(Dg)[s0i + j] : ~0ull;
   }
+  // the plan's resident bucket table (psg_tile.hip bucket_index_kernel<64>:
+  // the same 2048 buckets over the same tile), kBPT u16 entries per thread
+  const uint32_t* Bg = T.bt;
+  u32x2 btw = {0u, 0u};
+  if (Bg) btw = __builtin_nontemporal_load((const AS1 u32x2*)Bg + tid);
   V a0[M][4];
 #pragma unroll
   for (int mi = 0; mi < M; ++mi)
@@ -257,11 +262,12 @@ __global__ __launch_bounds__(kNT, (occupancy<V, M>())) void tile_packed_kernel(
   {
     uint32_t z = 0;  // opaque zero: not a hoisted (and spilled) constant vector
     asm volatile("" : "+v"(z));
-    *(u32x2*)&bt[tid * kBPT] = u32x2{z, z};
+    *(u32x2*)&bt[tid * kBPT] = Bg ? btw : u32x2{z, z};  // resident table, or a cleared histogram
+    if (Bg && tid == 0) bt[kNB] = (uint16_t)nt;
     if (lane < kTS / 32) cbits[w][lane] = z;
   }
   if (tid == 0) pcarry = -1;
-  __syncthreads();  // (1) tables, D, cleared histogram
+  __syncthreads();  // (1) tables, D, cleared histogram (or the resident bucket table)
 
   // ---- a pass: this wave's run of rounds, loaded into registers
   uint32_t gp = np ? uni(gsh[0]) : 0u;
@@ -307,8 +313,9 @@ __global__ __launch_bounds__(kNT, (occupancy<V, M>())) void tile_packed_kernel(
   if (U) load_pass();
 
   // ---- bucket table: histogram, exclusive scan -> bt[b] = first slot of bucket b
-  // D keys back from LDS: the registers that held them are free during the
-  // pass's element loads
+  // (skipped when the plan's resident index supplied it).  D keys back from
+  // LDS: the registers that held them are free during the pass's element loads
+  if (!Bg) {
   const u64x2 y0 = *(const u64x2*)&dk[s0i];
   const u64x2 y1 = *(const u64x2*)&dk[s0i + 2];
   const uint64_t dd[4] = {y0.x, y0.y, y1.x, y1.y};
@@ -342,6 +349,7 @@ __global__ __launch_bounds__(kNT, (occupancy<V, M>())) void tile_packed_kernel(
     if (tid == 0) bt[kNB] = (uint16_t)nt;
   }
   __syncthreads();  // (4)
+  }
 
   for (;;) {
     if (!U) {  // this group of pushes has no keys in the tile, or is done
