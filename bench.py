@@ -548,7 +548,7 @@ def cfg5_unsliced(args, rank, world, bounds, dist, dev, local, stream, pushes, D
     log(f"rank {rank}: unsliced cfg5 leg: {b - a} whole pushes, RCCL communicator")
     comm = shard.make_comm(local, rank, world, dist)
     x = shard.RcclExchange(comm, dp, world, PSG_F32)
-    log(f"rank {rank}: exchange set up: {x.nsent:,} keys sent, {x.nrecv:,} received")
+    log(f"rank {rank}: exchange set up: {x.nsent:,} keys to peers, {x.nrecv:,} received")
     try:
         pcs = x.pieces()  # (offset, count) per (source, push), arrival order
         dD = to_dev(D, dev)

@@ -299,7 +299,9 @@ int psg_comm_destroy(psg_comm* comm);
  * Run (collective, enqueued on `stream`): pack + one grouped send/recv per
  * peer.  Afterwards psg_exchange_recv gives the received keys / m value
  * arrays (device) and recv_cnt[src * npush + p] (host, may be NULL): the
- * piece of push p of rank src starts after all earlier (src, p) pieces. */
+ * piece of push p of rank src starts after all earlier (src, p) pieces;
+ * *nsent = keys this rank sends to the other ranks (its own pieces are
+ * packed straight into its receive buffers and never cross the transport). */
 typedef struct psg_exchange psg_exchange;
 int psg_exchange_create(psg_comm* comm, int dtype, int m, int npush,
                         const uint64_t* const* push_keys, const uint64_t* push_n,

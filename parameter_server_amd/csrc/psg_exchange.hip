@@ -15,9 +15,11 @@
 // A step (psg_exchange_run, on a stream, no host wait): the cut is redone
 // on the device and compared with the layout (a push whose keys changed
 // since set-up is counted, psg_exchange_status), one gather kernel packs
-// every piece into destination-major send buffers (16-B lanes where the
-// piece allows), then per peer one ncclSend/ncclRecv of the keys and one per
-// value array in a single group.  After a step, shard `rank` holds, for
+// every piece into destination-major send buffers (2048-element chunks, all
+// of a thread's loads before its stores; this rank's own pieces straight
+// into its receive buffers, so they never cross the transport), then per
+// peer one ncclSend/ncclRecv of the keys and one per value array in a
+// single group.  After a step, shard `rank` holds, for
 // each source rank src and push p, the piece at recv offset off[src][p]
 // with cnt[src][p] keys (the layout a psg_plan job points at directly).
 //
@@ -75,55 +77,58 @@ __global__ __launch_bounds__(256) void cut_kernel(const uint64_t* const* __restr
 // one piece of the send layout
 struct Piece {
   uint64_t src;  // element offset inside push p
-  uint64_t dst;  // element offset in the send buffers
+  uint64_t dst;  // element offset in the send buffers (tgt 0) or receive buffers (tgt 1)
   uint64_t len;
-  uint32_t p, pad;
+  uint32_t p;
+  uint32_t tgt;  // 1: this rank's own piece, packed straight into its receive buffers
 };
 
-typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
+constexpr uint32_t kChunk = 2048;  // elements per pack workgroup: 8 per thread
 
-// bytes [0, len) from s to d, 256 threads: 16-B lanes when both ends share
-// their offset mod 16 (the head and tail bytes around them by 4-B or 1-B
-// lanes), else element lanes of `eb` bytes
-__device__ __forceinline__ void copy_run(char* __restrict__ d, const char* __restrict__ s,
-                                         uint64_t len, int eb) {
-  const uint64_t mis = ((uintptr_t)d ^ (uintptr_t)s) & 15u;
-  if (mis == 0 && len >= 64) {
-    const uint64_t head = (16u - ((uintptr_t)d & 15u)) & 15u;
-    for (uint64_t i = threadIdx.x; i < head; i += 256) d[i] = s[i];
-    const uint64_t n16 = (len - head) / 16;
-    const u32x4* s16 = (const u32x4*)(s + head);
-    u32x4* d16 = (u32x4*)(d + head);
-    for (uint64_t i = threadIdx.x; i < n16; i += 256) d16[i] = __builtin_nontemporal_load(s16 + i);
-    for (uint64_t i = head + 16 * n16 + threadIdx.x; i < len; i += 256) d[i] = s[i];
-  } else if (eb == 8) {
-    for (uint64_t i = threadIdx.x; i < len / 8; i += 256)
-      ((uint64_t*)d)[i] = ((const uint64_t*)s)[i];
-  } else {
-    for (uint64_t i = threadIdx.x; i < len / 4; i += 256)
-      ((uint32_t*)d)[i] = ((const uint32_t*)s)[i];
+// elements [0, n <= kChunk) from s to d: every thread issues its 8 loads
+// (coalesced wave accesses of consecutive elements) before any store
+template <typename T>
+__device__ __forceinline__ void copy_chunk(T* __restrict__ d, const T* __restrict__ s, uint32_t n) {
+  T r[kChunk / 256];
+#pragma unroll
+  for (int j = 0; j < (int)(kChunk / 256); ++j) {
+    const uint32_t i = 256u * j + threadIdx.x;
+    if (i < n) r[j] = __builtin_nontemporal_load(s + i);
+  }
+#pragma unroll
+  for (int j = 0; j < (int)(kChunk / 256); ++j) {
+    const uint32_t i = 256u * j + threadIdx.x;
+    if (i < n) d[i] = r[j];
   }
 }
 
-// every piece into the destination-major send buffers: keys (8 B) and m
-// value arrays of `vb` bytes per element; a workgroup per 2048-element chunk
+// every piece into the destination-major send buffers (this rank's own
+// pieces into its receive buffers: no transport copy for them): keys (8 B)
+// and m value arrays of `vb` bytes per element; a workgroup per chunk
 __global__ __launch_bounds__(256) void pack_kernel(const Piece* __restrict__ pieces,
                                                    const uint64_t* __restrict__ chunk_piece,
                                                    uint64_t nchunks,
                                                    const uint64_t* const* __restrict__ keys,
                                                    const void* const* __restrict__ vals, int m,
                                                    int vb, uint64_t* __restrict__ skeys,
-                                                   void* const* __restrict__ svals) {
-  constexpr uint64_t kChunk = 2048;
+                                                   void* const* __restrict__ svals,
+                                                   uint64_t* __restrict__ rkeys,
+                                                   void* const* __restrict__ rvals) {
   for (uint64_t c = blockIdx.x; c < nchunks; c += gridDim.x) {
     const uint64_t e = chunk_piece[c];
     const Piece pc = pieces[e >> 24];
     const uint64_t c0 = (e & 0xffffffull) * kChunk;
-    const uint64_t len = pc.len - c0 < kChunk ? pc.len - c0 : kChunk;
-    copy_run((char*)(skeys + pc.dst + c0), (const char*)(keys[pc.p] + pc.src + c0), 8 * len, 8);
-    for (int a = 0; a < m; ++a)
-      copy_run((char*)svals[a] + (pc.dst + c0) * vb,
-               (const char*)vals[(size_t)pc.p * m + a] + (pc.src + c0) * vb, len * vb, vb);
+    const uint32_t len = (uint32_t)(pc.len - c0 < kChunk ? pc.len - c0 : kChunk);
+    uint64_t* const dk = pc.tgt ? rkeys : skeys;
+    void* const* const dv = pc.tgt ? rvals : svals;
+    copy_chunk(dk + pc.dst + c0, keys[pc.p] + pc.src + c0, len);
+    for (int a = 0; a < m; ++a) {
+      const uint64_t o = pc.src + c0, q = pc.dst + c0;
+      if (vb == 4)
+        copy_chunk((uint32_t*)dv[a] + q, (const uint32_t*)vals[(size_t)pc.p * m + a] + o, len);
+      else
+        copy_chunk((uint64_t*)dv[a] + q, (const uint64_t*)vals[(size_t)pc.p * m + a] + o, len);
+    }
   }
 }
 
@@ -149,6 +154,7 @@ struct psg_exchange {
   const uint64_t* const* d_keys = nullptr;
   const void* const* d_vals = nullptr;
   void* const* d_svals = nullptr;
+  void* const* d_rvals = nullptr;
   Piece* d_pieces = nullptr;
   uint64_t* d_chunks = nullptr;
   const uint64_t* d_n = nullptr;       // push lengths
@@ -273,6 +279,11 @@ int exchange_create(psg_comm* comm, int device, int S, int dtype, int m, int npu
   std::vector<Piece> pieces;
   std::vector<uint64_t> chunks;
   uint64_t off = 0;
+  // this rank's own pieces (a communicator's rank) go straight to the
+  // receive buffers: their offsets there (push order, from recv_off[rank])
+  // are fixed once the counts are known
+  const int self = comm ? comm->rank : -1;
+  uint64_t own = 0;  // elements of this rank's own pieces so far
   for (int s = 0; s < S; ++s) {
     x->send_off[s] = off;
     for (int p = 0; p < P; ++p) {
@@ -284,10 +295,12 @@ int exchange_create(psg_comm* comm, int device, int S, int dtype, int m, int npu
           err = fail(PSG_ERR_ARG, "too many pieces (> 2^24)");
           break;
         }
-        for (uint64_t q = 0; q * 2048 < c; ++q) chunks.push_back((uint64_t)pieces.size() << 24 | q);
-        pieces.push_back(Piece{a, off, c, (uint32_t)p, 0});
+        for (uint64_t q = 0; q * kChunk < c; ++q) chunks.push_back((uint64_t)pieces.size() << 24 | q);
+        const bool mine = s == self;
+        pieces.push_back(Piece{a, mine ? own : off, c, (uint32_t)p, mine ? 1u : 0u});
       }
-      off += c;
+      if (s == self) own += c;  // own pieces take no send-buffer space
+      else off += c;
     }
     x->send_tot[s] = off - x->send_off[s];
   }
@@ -333,6 +346,8 @@ int exchange_create(psg_comm* comm, int device, int S, int dtype, int m, int npu
   }
   x->nrecv = roff;
   x->nchunks = chunks.size();
+  for (Piece& pc : pieces)
+    if (pc.tgt) pc.dst += x->recv_off[self];
   // ---- the step's device block: send / receive buffers and the tables
   size_t b = 0;
   const size_t b_sk = b; b += al(8 * x->nsend);
@@ -344,6 +359,7 @@ int exchange_create(psg_comm* comm, int device, int S, int dtype, int m, int npu
   const size_t b_keys = b; b += al(8 * (size_t)P);
   const size_t b_vals = b; b += al(8 * (size_t)P * m);
   const size_t b_svp = b; b += al(8 * (size_t)m);
+  const size_t b_rvp = b; b += al(8 * (size_t)m);
   const size_t b_pc = b; b += al(sizeof(Piece) * pieces.size());
   const size_t b_ch = b; b += al(8 * chunks.size());
   const size_t b_n = b; b += al(8 * (size_t)P);
@@ -354,15 +370,17 @@ int exchange_create(psg_comm* comm, int device, int S, int dtype, int m, int npu
   char* d = (char*)x->dev;
   x->skeys = (uint64_t*)(d + b_sk);
   x->rkeys = (uint64_t*)(d + b_rk);
-  std::vector<uint64_t> svp(m);
+  std::vector<uint64_t> svp(m), rvp(m);
   for (int a = 0; a < m; ++a) {
     x->svals[a] = d + b_sv[a];
     x->rvals[a] = d + b_rv[a];
     svp[a] = (uint64_t)x->svals[a];
+    rvp[a] = (uint64_t)x->rvals[a];
   }
   x->d_keys = (const uint64_t* const*)(d + b_keys);
   x->d_vals = (const void* const*)(d + b_vals);
   x->d_svals = (void* const*)(d + b_svp);
+  x->d_rvals = (void* const*)(d + b_rvp);
   x->d_pieces = (Piece*)(d + b_pc);
   x->d_chunks = (uint64_t*)(d + b_ch);
   x->d_n = (const uint64_t*)(d + b_n);
@@ -378,6 +396,7 @@ int exchange_create(psg_comm* comm, int device, int S, int dtype, int m, int npu
   X_TRY(hipMemcpyAsync(d + b_bd, bounds.data(), 8 * (size_t)S1, hipMemcpyHostToDevice, st));
   X_TRY(hipMemsetAsync(d + b_bad, 0, 8, st));
   X_TRY(hipMemcpyAsync(d + b_svp, svp.data(), 8 * (size_t)m, hipMemcpyHostToDevice, st));
+  X_TRY(hipMemcpyAsync(d + b_rvp, rvp.data(), 8 * (size_t)m, hipMemcpyHostToDevice, st));
   if (!pieces.empty())
     X_TRY(hipMemcpyAsync(d + b_pc, pieces.data(), sizeof(Piece) * pieces.size(),
                          hipMemcpyHostToDevice, st));
@@ -424,12 +443,13 @@ int psg_exchange_run(psg_exchange* x, void* stream) {
     const uint64_t blocks = x->nchunks < 4096 ? x->nchunks : 4096;
     hipLaunchKernelGGL(pack_kernel, dim3((uint32_t)blocks), dim3(256), 0, st, x->d_pieces,
                        x->d_chunks, x->nchunks, x->d_keys, x->d_vals, x->m, vb, x->skeys,
-                       x->d_svals);
+                       x->d_svals, x->rkeys, x->d_rvals);
     HIP_TRY(hipGetLastError());
   }
   if (!x->comm) return PSG_OK;  // local shards: the packed buffers are the result
   ncclResult_t r = ncclGroupStart();
   for (int s = 0; r == ncclSuccess && s < x->S; ++s) {
+    if (s == x->comm->rank) continue;  // own pieces were packed into the receive buffers
     if (x->send_tot[s]) {
       r = ncclSend(x->skeys + x->send_off[s], x->send_tot[s], ncclUint64, s, x->comm->nccl, st);
       for (int a = 0; r == ncclSuccess && a < x->m; ++a)
