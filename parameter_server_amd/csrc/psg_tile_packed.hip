@@ -15,7 +15,9 @@
 // Shape:
 //   * the partition (psg_partition.hip) has cut every push at every tile:
 //     push q's keys of this tile are S_q[seg(q, t), seg(q, t+1));
-//   * pushes are taken in groups of <= kG = 128 (wave 0, two per lane) whose
+//   * pushes are taken in groups of <= kG = 256 (waves 0 and 1, two per
+//     lane; cfg5's 256 pushes are one group: one table chain and, at
+//     ~8 keys per push per tile, one pass per tile) whose
 //     elements fit one pass; the group's pieces are concatenated push-major
 //     and cut into ROUNDS of 64 consecutive elements, so a round may hold the
 //     tail of one piece and the heads of the next (short pieces of many
@@ -66,12 +68,12 @@ constexpr int kNW = kNT / 64;    // waves
 constexpr int kSPT = kTS / kNT;  // slots per thread (contiguous)
 constexpr int kNB = kTS;         // buckets (one per slot: the LDS budget of 4 workgroups per CU)
 constexpr int kBPT = kNB / kNT;  // bucket-table entries per thread in the scan
-constexpr int kCap = 6;          // rounds a wave holds per pass
-constexpr int kG = 128;          // pushes per group (two lanes' worth per lane of wave 0)
+constexpr int kCap = 5;          // rounds a wave holds per pass
+constexpr int kG = 256;          // pushes per group (waves 0 and 1, two per lane)
 constexpr int kECap = kNW * kCap * 64;  // elements per group: one pass
 static_assert(kSPT == 4 && kBPT == 4, "layout");
 static_assert(kTS <= 0x7ffe, "u16 positions");
-static_assert(kG + 2 <= 255 && kG <= 256, "u8 lastl, u8 element -> push map");
+static_assert(kG <= 256, "u8 element -> push map, 8-bit push field of a round entry");
 static_assert(kECap >= kTS, "a piece (<= kTS keys) always fits a group");
 
 typedef unsigned long long u64x2 __attribute__((ext_vector_type(2)));
@@ -102,7 +104,7 @@ __device__ __forceinline__ uint32_t wave_scan_incl(uint32_t x) {
 // the register budget follows it through __launch_bounds__
 template <typename V, int M>
 constexpr int occupancy() {
-  constexpr int lds = 38560 + (int)(M * sizeof(V) - 4) * kTS + (M - 1) * 8 * kG;
+  constexpr int lds = 40900 + (int)(M * sizeof(V) - 4) * kTS + (M - 1) * 8 * kG;
   // waves per SIMD (the launch bound's unit): workgroups per CU x waves / 4
   constexpr int w = (163840 / lds) * kNW / 4;
   return w >= 8 ? 8 : (w < 1 ? 1 : w);
@@ -119,19 +121,26 @@ __global__ __launch_bounds__(kNT, (occupancy<V, M>())) void tile_packed_kernel(
   uint16_t* const bt = (uint16_t*)bt32;
   __shared__ __attribute__((aligned(16))) V acc[M][kTS];
   // last push holding the slot, relative to the group base g0: last + 2 - g0,
-  // 0 when it precedes g0 - 1 (so the value fits a byte for any push count)
-  __shared__ __attribute__((aligned(16))) uint8_t lastl[kTS];
+  // 0 when it precedes g0 - 1 (<= kG + 1 for any push count)
+  __shared__ __attribute__((aligned(16))) uint16_t lastl[kTS];
   // pre[q] = elements of the group before push q; ep[e] = push of the
   // group's element e (written by the push's lane: one LDS read per element
   // instead of a search over pre)
   __shared__ uint32_t pre[kG + 1];
   __shared__ uint8_t ep[kECap];
   __shared__ uint64_t pkp[kG], pvp[kG * M];  // piece starts (keys, values)
-  __shared__ uint32_t cbits[kNW][kTS / 32];  // per-wave slot bitmap: collision test
+  // slot bitmap of the collision test, used by one wave at a time (inside
+  // its fold step): one bitmap instead of one per wave keeps 4 workgroups
+  // per CU with 256-push groups
+  __shared__ uint32_t cbits[kTS / 32];
   __shared__ int lastpos[kNW];
   __shared__ int pcarry;
   __shared__ uint32_t wsum[kNW];
-  __shared__ uint32_t gsh[2];            // pushes in the group, rounds in the group
+  // pushes in the group, elements of the group, wave 0's element count
+  __shared__ uint32_t gsh[3];
+  // pushes of the group whose piece overflowed (an unsorted or duplicated
+  // push): phase B recounts them; rare, so not kept in registers
+  __shared__ uint32_t ovf[kG / 32];
 
   const uint32_t w = uni((uint32_t)threadIdx.x >> 6);
   const int tid = threadIdx.x;
@@ -145,72 +154,122 @@ __global__ __launch_bounds__(kNT, (occupancy<V, M>())) void tile_packed_kernel(
   const bool cont = (T.flags & kFlagCont) != 0;
   const uint64_t* Dg = T.dk;
 
-  // ---- push tables of a group (wave 0, pushes lane and 64 + lane), the
-  // element -> push map
-  auto load_tables = [&](uint32_t g0) {
-    if (w == 0) {
+  // ---- push tables of a group: waves 0 and 1, pushes w*128 + lane and
+  // w*128 + 64 + lane.  Phase A loads the pieces, writes their start
+  // pointers and each wave's own inclusive prefix of the lengths (pre[q+1])
+  // into LDS; phase B (after a barrier: wave 1 needs wave 0's total) turns
+  // them into the group's prefix, keeps the pushes whose elements fit one
+  // pass and writes the element -> push map.  Nothing stays in registers
+  // across the barrier but the group size.
+  uint32_t tgq = 0;
+  // a piece's overflow: keys past the tile or bounds out of order (they
+  // cannot all match)
+  auto piece = [&](uint32_t q, uint32_t* a_out, uint32_t* over) -> uint32_t {
+    const uint32_t* sg = T.seg + (size_t)q * T.stride;
+    const uint32_t n = (uint32_t)G(T.pn)[q];
+    uint32_t a = G(sg)[0], b = G(sg)[T.segb];
+    // bounds from a failed partition (an unsorted push) stay inside the push
+    a = a < n ? a : n;
+    b = b < n ? b : n;
+    *over = b < a ? 1u : (b - a > (uint32_t)kTS ? b - a - (uint32_t)kTS : 0u);
+    *a_out = a;
+    return b > a ? (b - a < (uint32_t)kTS ? b - a : (uint32_t)kTS) : 0u;
+  };
+  auto tables_a = [&](uint32_t g0) {
+    if (w < 2) {
       // a fresh copy of the lane id per call: otherwise the compiler hoists
       // the lane-derived LDS addresses out of the push-group loop and, at
       // 64 VGPRs, spills them to scratch in every workgroup (HBM writes)
       int lane = tid & 63;
       asm volatile("" : "+v"(lane));
-      const uint32_t gq = np - g0 < (uint32_t)kG ? np - g0 : (uint32_t)kG;
-      uint32_t len[2] = {0, 0}, over[2] = {0, 0};
-      uint64_t kp[2] = {0, 0}, vp[2][M];
+      tgq = np - g0 < (uint32_t)kG ? np - g0 : (uint32_t)kG;
+      uint32_t len[2], ov[2];
 #pragma unroll
       for (int h = 0; h < 2; ++h) {
-#pragma unroll
-        for (int mi = 0; mi < M; ++mi) vp[h][mi] = 0;
-        const uint32_t ql = (uint32_t)lane + 64u * h;
-        if (ql < gq) {
+        len[h] = 0;
+        ov[h] = 0;
+        const uint32_t ql = 128u * w + (uint32_t)lane + 64u * h;
+        if (ql < tgq) {
           const uint32_t q = g0 + ql;
-          const uint32_t* sg = T.seg + (size_t)q * T.stride;
-          const uint32_t n = (uint32_t)G(T.pn)[q];
-          uint32_t a = G(sg)[0], b = G(sg)[T.segb];
-          // bounds from a failed partition (an unsorted push) stay inside the push
-          a = a < n ? a : n;
-          b = b < n ? b : n;
-          // pieces out of order or longer than the tile (duplicates): those
-          // keys cannot all match
-          over[h] = b < a ? 1u : (b - a > (uint32_t)kTS ? b - a - (uint32_t)kTS : 0u);
-          len[h] = b > a ? (b - a < (uint32_t)kTS ? b - a : (uint32_t)kTS) : 0u;
-          kp[h] = (uint64_t)(G(T.pkeys)[q] + a);
+          uint32_t a;
+          len[h] = piece(q, &a, &ov[h]);
+          // a push that does not fit this group's pass is written again
+          // (at its new index) by the next group's phase A
+          pkp[ql] = (uint64_t)(G(T.pkeys)[q] + a);
 #pragma unroll
           for (int mi = 0; mi < M; ++mi)
-            vp[h][mi] = (uint64_t)((const V*)G(T.pvals)[(size_t)q * M + mi] + a);
+            pvp[ql * M + mi] = (uint64_t)((const V*)G(T.pvals)[(size_t)q * M + mi] + a);
         }
       }
-      // elements through each push
+      // elements through each push, inside this wave
       const uint32_t x0 = wave_scan_incl(len[0]);
       const uint32_t x1 = wave_scan_incl(len[1]) + uni(__builtin_amdgcn_readlane((int)x0, 63));
-      // the group: the pushes whose elements fit one pass (>= 1: a piece is <= kTS)
-      const uint32_t gp =
-          (uint32_t)__popcll(__ballot((uint32_t)lane < gq && x0 <= (uint32_t)kECap)) +
-          (uint32_t)__popcll(__ballot((uint32_t)lane + 64u < gq && x1 <= (uint32_t)kECap));
+      const uint32_t ql0 = 128u * w + (uint32_t)lane;
+      if (ql0 < tgq) pre[ql0 + 1] = x0;
+      if (ql0 + 64u < tgq) pre[ql0 + 65] = x1;
+      if (w == 0 && lane == 63) gsh[2] = x1;
 #pragma unroll
       for (int h = 0; h < 2; ++h) {
-        const uint32_t ql = (uint32_t)lane + 64u * h;
-        const uint32_t x = h ? x1 : x0;
-        if (ql < gp) {
-          pkp[ql] = kp[h];
-#pragma unroll
-          for (int mi = 0; mi < M; ++mi) pvp[ql * M + mi] = vp[h][mi];
-          if (over[h])
-            __hip_atomic_fetch_add(GW(T.fail) + g0 + ql, (unsigned long long)over[h],
-                                   __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-          pre[ql + 1] = x;
-#pragma nounroll
-          for (uint32_t e = x - len[h]; e < x; ++e) ep[e] = (uint8_t)ql;
-        }
-        if (ql + 1u == gp) gsh[1] = (x + 63u) >> 6;  // rounds of the group
+        const unsigned long long om = __ballot(ov[h] != 0u);
+        if (lane < 2) ovf[4u * w + 2u * h + lane] = (uint32_t)(om >> (32 * lane));
       }
-      if (lane == 0) {
-        pre[0] = 0;
-        gsh[0] = gp;
+      if (w == 0 && lane == 0) {
+        uint32_t z = 0;  // opaque zero: not a constant kept (and spilled) across the loop
+        asm volatile("" : "+v"(z));
+        gsh[0] = z;
+        gsh[1] = z;
       }
     }
   };
-  if (np) load_tables(0);
+  auto tables_b = [&](uint32_t g0) {
+    if (w < 2) {
+      int lane = tid & 63;
+      asm volatile("" : "+v"(lane));
+      const uint32_t base = w == 1 ? uni(gsh[2]) : 0u;
+      uint32_t xl[2], pl[2];
+#pragma unroll
+      for (int h = 0; h < 2; ++h) {  // all reads before any write
+        const uint32_t ql = 128u * w + (uint32_t)lane + 64u * h;
+        xl[h] = ql < tgq ? pre[ql + 1] : 0u;
+        pl[h] = (h == 0 && lane == 0) || ql >= tgq ? 0u : pre[ql];
+      }
+      uint32_t fit = 0, emax = 0;
+#pragma unroll
+      for (int h = 0; h < 2; ++h) {
+        const uint32_t ql = 128u * w + (uint32_t)lane + 64u * h;
+        const uint32_t x = xl[h] + base;
+        // the group: the pushes whose elements fit one pass (a prefix; >= 1:
+        // a piece is <= kTS)
+        const bool in = ql < tgq && x <= (uint32_t)kECap;
+        fit += (uint32_t)__popcll(__ballot(in));
+        if (in) {
+          if ((ovf[ql >> 5] >> (ql & 31u)) & 1u) {  // recount the overflow (rare)
+            uint32_t a, over;
+            (void)piece(g0 + ql, &a, &over);
+            __hip_atomic_fetch_add(GW(T.fail) + g0 + ql, (unsigned long long)over,
+                                   __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+          }
+          pre[ql + 1] = x;
+#pragma nounroll
+          for (uint32_t e = x - (xl[h] - pl[h]); e < x; ++e) ep[e] = (uint8_t)ql;
+          emax = x;  // increasing with ql: the last fitting push's count
+        }
+      }
+      // wave maximum of the fitting counts
+#pragma unroll
+      for (int o = 32; o > 0; o >>= 1) {
+        const uint32_t y = (uint32_t)__shfl_xor((int)emax, o, 64);
+        emax = y > emax ? y : emax;
+      }
+      if (lane == 0) {
+        __hip_atomic_fetch_add(&gsh[0], fit, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+        __hip_atomic_fetch_max(&gsh[1], emax, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+        if (w == 0) pre[0] = 0;
+      }
+    }
+  };
+  if (np) tables_a(0);
+
 
   // ---- D keys, continued sums: thread t owns slots 4t..4t+3
   const uint32_t s0i = 4u * (uint32_t)tid;
@@ -264,19 +323,21 @@ __global__ __launch_bounds__(kNT, (occupancy<V, M>())) void tile_packed_kernel(
     asm volatile("" : "+v"(z));
     *(u32x2*)&bt[tid * kBPT] = Bg ? btw : u32x2{z, z};  // resident table, or a cleared histogram
     if (Bg && tid == 0) bt[kNB] = (uint16_t)nt;
-    if (lane < kTS / 32) cbits[w][lane] = z;
+    if (tid < kTS / 32) cbits[tid] = z;
   }
   if (tid == 0) pcarry = -1;
-  __syncthreads();  // (1) tables, D, cleared histogram (or the resident bucket table)
+  __syncthreads();  // (1) pieces scanned, D, cleared histogram (or the resident bucket table)
+  if (np) tables_b(0);
+  __syncthreads();  // (1b) the group's tables
 
   // ---- a pass: this wave's run of rounds, loaded into registers
   uint32_t gp = np ? uni(gsh[0]) : 0u;
-  uint32_t U = np ? uni(gsh[1]) : 0u;
-  uint32_t Et = np ? uni(pre[gp]) : 0u;  // elements of the group
+  uint32_t Et = np ? uni(gsh[1]) : 0u;  // elements of the group
+  uint32_t U = (Et + 63u) >> 6;        // rounds of the group
   uint32_t done = 0, g0 = 0;
   uint32_t nrw = 0, ua = 0, Rw = 0;
-  // per lane and held round r, 10 bits: q | first-of-piece << 7 | exists << 8
-  // (packed 3 rounds per register: a 64-VGPR budget holds 6 rounds unspilled)
+  // per lane and held round r, 10 bits: q | first-of-piece << 8 | exists << 9
+  // (packed 3 rounds per register)
   uint32_t rp[(kCap + 2) / 3];
   uint64_t ek[kCap];
   V ev[kCap][M];
@@ -303,7 +364,7 @@ __global__ __launch_bounds__(kNT, (occupancy<V, M>())) void tile_packed_kernel(
         const uint32_t qlo = uni(q);
         const uint32_t i = have ? e - pre[q] : 0u;
         mmask |= (__ballot(have && q != qlo) != 0 ? 1u : 0u) << r;
-        rp[r / 3] |= (q | (uint32_t)(have && i == 0u) << 7 | (uint32_t)have << 8) << (10 * (r % 3));
+        rp[r / 3] |= (q | (uint32_t)(have && i == 0u) << 8 | (uint32_t)have << 9) << (10 * (r % 3));
         ek[r] = G((const uint64_t*)pkp[q])[i];
 #pragma unroll
         for (int mi = 0; mi < M; ++mi) ev[r][mi] = G((const V*)pvp[q * M + mi])[i];
@@ -358,11 +419,13 @@ __global__ __launch_bounds__(kNT, (occupancy<V, M>())) void tile_packed_kernel(
       // rebase lastl on the new group: last == g0 - 1 -> 1, older -> 0
 #pragma unroll
       for (int j = 0; j < 4; ++j) lastl[s0i + j] = lastl[s0i + j] == gp + 1u ? 1 : 0;
-      load_tables(g0);
+      tables_a(g0);
+      __syncthreads();
+      tables_b(g0);
       __syncthreads();
       gp = uni(gsh[0]);
-      U = uni(gsh[1]);
-      Et = uni(pre[gp]);
+      Et = uni(gsh[1]);
+      U = (Et + 63u) >> 6;
       done = 0;
       if (U) load_pass();
       continue;
@@ -408,8 +471,8 @@ __global__ __launch_bounds__(kNT, (occupancy<V, M>())) void tile_packed_kernel(
         if (r > 0) prev0 = __builtin_amdgcn_readlane((int)pos[r - 1], 63);
         else prev0 = w > 0 ? lastpos[w - 1] : pcarry;
         int prev = __builtin_amdgcn_update_dpp(prev0, (int)pos[r], 0x138, 0xf, 0xf, false);
-        if ((re(r) >> 7) & 1u) prev = -1;  // first element of its piece
-        const bool ok = ((re(r) >> 8) & 1u) && ((okm >> r) & 1u) && (int)pos[r] > prev;
+        if ((re(r) >> 8) & 1u) prev = -1;  // first element of its piece
+        const bool ok = ((re(r) >> 9) & 1u) && ((okm >> r) & 1u) && (int)pos[r] > prev;
         okm |= (uint32_t)ok << (8 + r);
       }
     }
@@ -418,47 +481,47 @@ __global__ __launch_bounds__(kNT, (occupancy<V, M>())) void tile_packed_kernel(
     {
       uint32_t exist = 0;
 #pragma unroll
-      for (int r = 0; r < kCap; ++r) exist |= ((re(r) >> 8) & 1u) << r;
+      for (int r = 0; r < kCap; ++r) exist |= ((re(r) >> 9) & 1u) << r;
       const uint32_t badm = exist & ~(okm >> 8);
       if (__ballot(badm != 0u)) {
 #pragma unroll
         for (int r = 0; r < kCap; ++r)
           if ((badm >> r) & 1u)
-            __hip_atomic_fetch_add(GW(T.fail) + g0 + (re(r) & 127u), 1ull, __ATOMIC_RELAXED,
+            __hip_atomic_fetch_add(GW(T.fail) + g0 + (re(r) & 255u), 1ull, __ATOMIC_RELAXED,
                                    __HIP_MEMORY_SCOPE_AGENT);
       }
     }
-    // ---- rounds holding several pushes: do two of them hit one slot?
-    // cl[r] (wave-uniform): the lanes of round r that found their slot's bit
-    // already set -- each names a slot hit more than once in the round
-    unsigned long long cl[kCap];
-#pragma unroll
-    for (int r = 0; r < kCap; ++r) cl[r] = 0;
-    if (mmask) {
-#pragma unroll
-      for (int r = 0; r < kCap; ++r) {
-        if ((mmask >> r) & 1u) {
-          const bool ok = (okm >> (8 + r)) & 1u;
-          const uint32_t s = pos[r], bit = 1u << (s & 31u);
-          uint32_t old = 0;
-          if (ok) old = __hip_atomic_fetch_or(&cbits[w][s >> 5], bit, __ATOMIC_RELAXED,
-                                              __HIP_MEMORY_SCOPE_WAVEFRONT);
-          cl[r] = __ballot(ok && (old & bit));
-          if (ok) cbits[w][s >> 5] = 0u;
-        }
-      }
-    }
-
     // ---- fold, wave by wave (rounds are push-major)
     const uint32_t inpass = (U - done) < kNW * Rw ? U - done : kNW * Rw;
     const uint32_t wl = (inpass - 1) / Rw;  // wave holding the pass's last round
     for (uint32_t st = 0; st < (uint32_t)kNW; ++st) {
       if (st == w) {
+        // rounds holding several pushes: do two of them hit one slot?
+        // cl[r] (wave-uniform): the lanes of round r that found their slot's
+        // bit already set -- each names a slot hit more than once in the
+        // round (the bitmap is this wave's during its step)
+        unsigned long long cl[kCap];
+#pragma unroll
+        for (int r = 0; r < kCap; ++r) cl[r] = 0;
+        if (mmask) {
+#pragma unroll
+          for (int r = 0; r < kCap; ++r) {
+            if ((mmask >> r) & 1u) {
+              const bool ok = (okm >> (8 + r)) & 1u;
+              const uint32_t s = pos[r], bit = 1u << (s & 31u);
+              uint32_t old = 0;
+              if (ok) old = __hip_atomic_fetch_or(&cbits[s >> 5], bit, __ATOMIC_RELAXED,
+                                                  __HIP_MEMORY_SCOPE_WAVEFRONT);
+              cl[r] = __ballot(ok && (old & bit));
+              if (ok) cbits[s >> 5] = 0u;
+            }
+          }
+        }
 #pragma unroll
         for (int r = 0; r < kCap; ++r) {
           if ((uint32_t)r < nrw) {
             bool pend = (okm >> (8 + r)) & 1u;
-            const uint32_t q = re(r) & 127u;
+            const uint32_t q = re(r) & 255u;
             const uint32_t s = pos[r];
             const bool first = g0 + q == 0u && !cont;
             auto apply = [&]() {
@@ -470,7 +533,7 @@ __global__ __launch_bounds__(kNT, (occupancy<V, M>())) void tile_packed_kernel(
                 const V ag = gap ? a + V(0) : a;
                 acc[mi][s] = first ? ev[r][mi] : ag + ev[r][mi];
               }
-              lastl[s] = (uint8_t)(q + 2u);
+              lastl[s] = (uint16_t)(q + 2u);
             };
             const unsigned long long cm = cl[r];
             if (!cm) {

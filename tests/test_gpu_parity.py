@@ -191,6 +191,40 @@ def test_packed_rounds_value_types(torch_cuda, dtype, m):
             assert_bitexact(out[i][1], want[i])
 
 
+@pytest.mark.parametrize("npush,density,nD", [(700, 0.002, 40000), (40, 0.6, 12000)])
+def test_packed_push_groups(torch_cuda, npush, density, nD):
+    """The packed kernel's push groups (up to 256 pushes whose elements fit
+    one pass of 2,560): 700 sparse pushes (three groups per tile, the
+    lastl rebase between them) and 40 dense pushes (~1,200 elements per push
+    per tile: groups cut by the pass capacity, a piece per group at most
+    2,048), serial and parallel, plan and context paths, bit-exact against
+    the oracle; an unsorted push in the second case is reported."""
+    torch = torch_cuda
+    from parameter_server_amd._lib import PSG_FORM_PACKED
+    D, pushes = random_case(900 + npush, np.float32, 1, npush, density, nD)
+    pushes = [p for p in pushes if p[0].size]
+    for parallel in (False, True):
+        out = run_ctx(D, pushes, parallel=parallel, flags=PSG_FORM_PACKED)
+        rc, lo, hi, want, _ = O.aggregate(D, *ALL, pushes, parallel, 1, np.float32)
+        assert rc == 0
+        assert_bitexact(out[0][1], want[0])
+        plan, keep = plan_for(torch, [(D, pushes)], parallel=parallel, flags=PSG_FORM_PACKED)
+        plan.run()
+        assert plan.matched().tolist() == [k.size for k, _ in pushes]
+        assert_bitexact(keep[3][0].cpu().numpy()[: D.size], want[0])
+        plan.close()
+    if npush == 40:
+        bad = list(pushes)
+        k = bad[7][0].copy()
+        k[[100, 101]] = k[[101, 100]]  # two keys out of order
+        bad[7] = (k, bad[7][1])
+        plan, keep = plan_for(torch, [(D, bad)], flags=PSG_FORM_PACKED)
+        plan.run()
+        mt = plan.matched().tolist()
+        assert mt[7] < k.size and all(mt[i] == bad[i][0].size for i in range(len(bad)) if i != 7)
+        plan.close()
+
+
 def extreme_range_keys():
     """5 tiles of 1024 server keys whose key ranges hit the bucket map's
     edges: 1023 wide; just under 2^32; exactly 2^32 (33 bits); one crowded

@@ -18,7 +18,9 @@ def rows(pattern):
 def short(name):
     for k in ("tile_packed_kernel", "tile_kernel", "splitter_kernel", "partition_kernel",
               "unmatched_kernel", "gather_kernel", "union", "slice_kernel", "crc_kernel",
-              "darling_kernel", "cm_"):
+              "darling_kernel", "cm_insert", "cm_count", "cm_scan", "cm_scatter",
+              "snappy_lit_kernel", "snappy_kernel", "nw_tile_kernel", "nw_cand", "nw_seg",
+              "dense_kernel"):
         if k in name:
             return k
     return None
