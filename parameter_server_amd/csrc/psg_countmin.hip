@@ -16,8 +16,9 @@
 // their low byte -- exact, since (sum mod 2^32) mod 2^8 = sum mod 2^8 and
 // addition mod 2^8 does not depend on order, so any interleaving of inserts
 // gives the reference's table.  Each counter costs one random 4-byte
-// read-modify-write in L2/HBM either way.  queryKeys is a flag pass and an
-// order-preserving compaction (workgroup scan + one scan of block totals).
+// read-modify-write in L2/HBM either way.  queryKeys is a query pass that
+// keeps one bit per key and an order-preserving compaction of those bits
+// (workgroup scan + one scan of block totals): the table is read once.
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
@@ -76,19 +77,25 @@ __global__ __launch_bounds__(kNT) void cm_insert_kernel(const uint64_t* __restri
   }
 }
 
-// pass 1: keys kept per workgroup tile
+// pass 1: the query of every key (each probe a random 4-byte read of the
+// table: the cost of queryKeys), its keep bit, and the keys kept per
+// workgroup tile.  Thread-contiguous runs of kIPT keys, so the bits are in
+// input order; pass 3 reads the bits instead of querying the table again.
 __global__ __launch_bounds__(kNT) void cm_count_kernel(const uint64_t* __restrict__ keys,
                                                        uint64_t nk, const uint32_t* __restrict__ t,
                                                        uint32_t n, int k, int freq,
-                                                       uint32_t* __restrict__ tile_cnt) {
+                                                       uint32_t* __restrict__ tile_cnt,
+                                                       uint8_t* __restrict__ keep_bits) {
   __shared__ uint32_t ws[kNT / 64];
-  const uint64_t base = (uint64_t)blockIdx.x * kQTile;
-  uint32_t c = 0;
+  const uint64_t base = (uint64_t)blockIdx.x * kQTile + (uint64_t)threadIdx.x * kIPT;
+  uint32_t keep = 0;
 #pragma unroll
   for (int r = 0; r < kIPT; ++r) {
-    const uint64_t i = base + (uint64_t)r * kNT + threadIdx.x;
-    if (i < nk && (int)cm_query(t, n, k, keys[i]) > freq) ++c;
+    const uint64_t i = base + r;
+    if (i < nk && (int)cm_query(t, n, k, keys[i]) > freq) keep |= 1u << r;
   }
+  keep_bits[(uint64_t)blockIdx.x * kNT + threadIdx.x] = (uint8_t)keep;
+  uint32_t c = (uint32_t)__popc(keep);
   for (int s = 32; s >= 1; s >>= 1) c += (uint32_t)__shfl_xor((int)c, s, 64);
   if ((threadIdx.x & 63) == 0) ws[threadIdx.x >> 6] = c;
   __syncthreads();
@@ -121,29 +128,20 @@ __global__ __launch_bounds__(kNT) void cm_scan_kernel(uint32_t* __restrict__ til
   if (threadIdx.x == 0) *total = carry;
 }
 
-// pass 3: scatter the kept keys in input order
+// pass 3: scatter the kept keys in input order (from pass 1's bits)
 __global__ __launch_bounds__(kNT) void cm_scatter_kernel(const uint64_t* __restrict__ keys,
                                                          uint64_t nk,
-                                                         const uint32_t* __restrict__ t,
-                                                         uint32_t n, int k, int freq,
+                                                         const uint8_t* __restrict__ keep_bits,
                                                          const uint32_t* __restrict__ tile_off,
                                                          uint64_t* __restrict__ out) {
   __shared__ uint32_t ws[kNT / 64];
-  const uint64_t base = (uint64_t)blockIdx.x * kQTile;
-  // thread-contiguous runs keep the output in input order
-  uint32_t keep = 0;
-  uint64_t kk[kIPT];
-#pragma unroll
-  for (int r = 0; r < kIPT; ++r) {
-    const uint64_t i = base + (uint64_t)threadIdx.x * kIPT + r;
-    kk[r] = i < nk ? keys[i] : 0;
-    if (i < nk && (int)cm_query(t, n, k, kk[r]) > freq) keep |= 1u << r;
-  }
+  const uint64_t base = (uint64_t)blockIdx.x * kQTile + (uint64_t)threadIdx.x * kIPT;
+  const uint32_t keep = keep_bits[(uint64_t)blockIdx.x * kNT + threadIdx.x];
   uint32_t tot;
   uint32_t pos = tile_off[blockIdx.x] + dev::block_excl_scan<kNT>(__popc(keep), ws, &tot);
 #pragma unroll
   for (int r = 0; r < kIPT; ++r)
-    if ((keep >> r) & 1u) out[pos++] = kk[r];
+    if (((keep >> r) & 1u) && base + r < nk) out[pos++] = keys[base + r];
 }
 
 }  // namespace
@@ -156,20 +154,25 @@ hipError_t launch_cm_insert(const uint64_t* keys, const uint32_t* counts, uint64
   return hipGetLastError();
 }
 
-size_t cm_query_scratch_bytes(uint64_t nk) { return 4 * ((nk + kQTile - 1) / kQTile) + 64; }
+// tile counts (u32 per tile) then the keep bits (a byte per thread)
+size_t cm_query_scratch_bytes(uint64_t nk) {
+  const uint64_t ntiles = (nk + kQTile - 1) / kQTile;
+  return ((4 * ntiles + 255) / 256) * 256 + ntiles * kNT + 64;
+}
 
 hipError_t launch_cm_query(const uint64_t* keys, uint64_t nk, const uint32_t* table, uint32_t n,
                            int k, int freq, uint64_t* out, unsigned long long* nout,
                            void* scratch, hipStream_t s) {
   const uint32_t ntiles = (uint32_t)((nk + kQTile - 1) / kQTile);
   uint32_t* cnt = (uint32_t*)scratch;
+  uint8_t* bits = (uint8_t*)scratch + ((4 * (uint64_t)ntiles + 255) / 256) * 256;
   if (ntiles)
     hipLaunchKernelGGL(cm_count_kernel, dim3(ntiles), dim3(kNT), 0, s, keys, nk, table, n, k,
-                       freq, cnt);
+                       freq, cnt, bits);
   hipLaunchKernelGGL(cm_scan_kernel, dim3(1), dim3(kNT), 0, s, cnt, ntiles, nout);
   if (ntiles)
-    hipLaunchKernelGGL(cm_scatter_kernel, dim3(ntiles), dim3(kNT), 0, s, keys, nk, table, n, k,
-                       freq, cnt, out);
+    hipLaunchKernelGGL(cm_scatter_kernel, dim3(ntiles), dim3(kNT), 0, s, keys, nk, bits, cnt,
+                       out);
   return hipGetLastError();
 }
 
