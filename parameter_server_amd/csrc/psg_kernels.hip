@@ -26,12 +26,14 @@ namespace {
 // req[i] repeats req[i-1] (the reference merge walk advances past a match,
 // message.h:256-260, so a repeated request key reads 0).
 //
-// A workgroup takes kGR consecutive (sorted) requests.  Two 64-ary wave
-// searches bound their server positions, [lower_bound(first),
-// upper_bound(last)); when that span fits kGS keys (a dense pull) it is
-// staged in LDS with one coalesced read and every request searches there,
-// otherwise (a sparse pull) each searches the span in global memory.  Each
-// thread keeps kGR/256 requests in flight so their loads overlap.
+// A workgroup takes kGR consecutive (sorted) requests, four consecutive ones
+// per thread, loaded first so they arrive while two 64-ary wave searches
+// bound their server positions, [lower_bound(first), upper_bound(last));
+// when that span fits kGS keys (a dense pull) it is staged in LDS with one
+// batch of coalesced reads and every request searches there, otherwise (a
+// sparse pull) each searches the span in global memory.  The repeat test
+// takes the previous request from a register (the thread's own, its lane
+// neighbour's, or the previous wave's last through LDS), not from memory.
 // ----------------------------------------------------------------------
 constexpr int kGR = 1024;  // requests per workgroup
 constexpr int kGS = 4096;  // server keys staged in LDS (32 KB)
@@ -44,31 +46,47 @@ __global__ __launch_bounds__(256) void gather_kernel(
   constexpr int kI = kGR / 256;
   __shared__ uint64_t t[kGS];
   __shared__ uint64_t rg[2];
+  __shared__ uint64_t wlast[4];  // each wave's last request
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
   const uint64_t r0 = (uint64_t)blockIdx.x * kGR;
   const uint64_t r1 = nreq - r0 < (uint64_t)kGR ? nreq : r0 + kGR;
+  const uint64_t ib = r0 + (uint64_t)kI * threadIdx.x;
+  uint64_t k[kI];
+#pragma unroll
+  for (int q = 0; q < kI; ++q) k[q] = ib + q < r1 ? req[ib + q] : 0;
+  const uint64_t before = r0 > 0 ? req[r0 - 1] : 0;  // the request before the block's first
   if (w < 2) {
     const uint64_t r = wave_search(D, nd, req[w == 0 ? r0 : r1 - 1], w == 1, lane);
     if (lane == 0) rg[w] = r;
   }
+  if (lane == 63) wlast[w] = k[kI - 1];
   __syncthreads();
   const uint64_t lo = rg[0], hi = rg[1] > rg[0] ? rg[1] : rg[0];
   const uint64_t n = hi - lo;
   const bool staged = n <= (uint64_t)kGS;
   if (staged) {
-    for (int j = threadIdx.x; j < (int)n; j += 256) t[j] = __builtin_nontemporal_load(D + lo + j);
+    uint64_t x[kGS / 256];
+#pragma unroll
+    for (int j = 0; j < kGS / 256; ++j) {
+      const uint64_t e = (uint64_t)j * 256 + threadIdx.x;
+      if (e < n) x[j] = __builtin_nontemporal_load(D + lo + e);
+    }
+#pragma unroll
+    for (int j = 0; j < kGS / 256; ++j) {
+      const uint64_t e = (uint64_t)j * 256 + threadIdx.x;
+      if (e < n) t[e] = x[j];
+    }
     __syncthreads();
   }
-  uint64_t k[kI], pos[kI];
+  // the request before each of this thread's: its own previous one, lane
+  // - 1's last, or the previous wave's last (the block's first: `before`)
+  const uint64_t up = (uint64_t)__shfl_up((long long)k[kI - 1], 1, 64);
+  const uint64_t prev0 = lane > 0 ? up : (w > 0 ? wlast[w - 1] : before);
+  uint64_t pos[kI];
   bool ok[kI];
 #pragma unroll
   for (int q = 0; q < kI; ++q) {
-    const uint64_t i = r0 + (uint64_t)(q * 256 + threadIdx.x);
-    k[q] = i < r1 ? req[i] : 0;
-  }
-#pragma unroll
-  for (int q = 0; q < kI; ++q) {
-    const uint64_t i = r0 + (uint64_t)(q * 256 + threadIdx.x);
+    const uint64_t i = ib + q;
     uint64_t p;
     bool hit;
     if (staged) {
@@ -79,17 +97,19 @@ __global__ __launch_bounds__(256) void gather_kernel(
       p = lo + gl_lower_bound(D + lo, n, k[q]);
       hit = p < hi && D[p] == k[q];
     }
-    const bool rep = i > 0 && i < r1 && req[i - 1] == k[q];
+    const uint64_t prev = q == 0 ? prev0 : k[q > 0 ? q - 1 : 0];
+    const bool rep = i > 0 && i < r1 && prev == k[q];
     ok[q] = i < r1 && hit && !rep;
     pos[q] = ok[q] ? p : 0;
   }
+  V x[kI];
+#pragma unroll
+  for (int q = 0; q < kI; ++q) x[q] = nd && ok[q] ? W[pos[q]] : V(0);
   int found = 0;
 #pragma unroll
   for (int q = 0; q < kI; ++q) {
-    const uint64_t i = r0 + (uint64_t)(q * 256 + threadIdx.x);
-    if (i < r1) {
-      const V x = nd ? W[pos[q]] : V(0);  // W[0] stands in for a miss
-      out[i] = ok[q] ? x : V(0);
+    if (ib + q < r1) {
+      out[ib + q] = x[q];
       found += ok[q];
     }
   }
