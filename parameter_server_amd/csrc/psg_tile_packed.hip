@@ -62,6 +62,10 @@ __device__ __forceinline__ AS1 T* GW(T* p) {
   return (AS1 T*)p;
 }
 
+#ifndef PSG_SKELETON
+#define PSG_SKELETON 0  // diagnostic A/B builds: 1 = loads and stores only
+#endif
+
 constexpr int kTS = kPackTileSlots;  // slots per tile
 constexpr int kNT = 512;             // threads
 constexpr int kNW = kNT / 64;    // waves
@@ -431,6 +435,24 @@ __global__ __launch_bounds__(kNT, (occupancy<V, M>())) void tile_packed_kernel(
       continue;
     }
     auto re = [&](int r) -> uint32_t { return (rp[r / 3] >> (10 * (r % 3))) & 0x3ffu; };
+#if PSG_SKELETON == 1
+    // diagnostic (A/B builds only): the loads and stores, no search, check
+    // or fold -- the memory side's own time
+    {
+      V t = V(0);
+#pragma unroll
+      for (int r = 0; r < kCap; ++r)
+        if ((uint32_t)r < nrw && ((re(r) >> 9) & 1u)) t += ev[r][0] + (V)(uint32_t)(ek[r] & 1u);
+      acc[0][s0i] += t;
+      done += kNW * Rw;
+      if (done < U) {
+        load_pass();
+        continue;
+      }
+      U = 0;
+      continue;
+    }
+#endif
     // ---- search every held round
     uint32_t pos[kCap];
     uint32_t okm = 0;  // per lane: bit r = found; bit 8 + r = found and in order
@@ -491,9 +513,27 @@ __global__ __launch_bounds__(kNT, (occupancy<V, M>())) void tile_packed_kernel(
                                    __HIP_MEMORY_SCOPE_AGENT);
       }
     }
-    // ---- fold, wave by wave (rounds are push-major)
+#if PSG_SKELETON == 2
+    // diagnostic: loads, stores, search and order check; no collision test
+    // and no fold
+    {
+      V t = V(0);
+#pragma unroll
+      for (int r = 0; r < kCap; ++r)
+        if ((uint32_t)r < nrw && ((okm >> (8 + r)) & 1u)) t += ev[r][0] + (V)pos[r];
+      acc[0][s0i] += t;
+      done += kNW * Rw;
+      if (done < U) {
+        load_pass();
+        continue;
+      }
+      U = 0;
+      continue;
+    }
+#endif
     const uint32_t inpass = (U - done) < kNW * Rw ? U - done : kNW * Rw;
     const uint32_t wl = (inpass - 1) / Rw;  // wave holding the pass's last round
+    // ---- fold, wave by wave (rounds are push-major)
     for (uint32_t st = 0; st < (uint32_t)kNW; ++st) {
       if (st == w) {
         // rounds holding several pushes: do two of them hit one slot?
