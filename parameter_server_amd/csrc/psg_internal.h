@@ -13,7 +13,10 @@ constexpr int kTileSlots = 1024;  // server slots per aggregate-kernel tile
 // sparse (packed-round) plans use tiles twice as large: each push's piece
 // per tile doubles, so a round's element loads touch half as many pushes
 // (pages) per element
-constexpr int kPackTileSlots = 2048;
+#ifndef PSG_PACK_TS
+#define PSG_PACK_TS 2048  // A/B builds: 4096
+#endif
+constexpr int kPackTileSlots = PSG_PACK_TS;
 // and so do tile-kernel plans with more than 32 pushes (psg_tile.hip)
 constexpr int kWideSlots = 2048;
 
@@ -99,8 +102,9 @@ hipError_t launch_aggregate_tile(int dtype, int m, const TileDesc* d_tiles, uint
                                  int form, hipStream_t stream);
 // the bucket tables of the tile kernel's tiles (psg_tile.hip), built from D
 // alone: bucket_index_words(wide) u32 per tile at out + tile * words
-uint32_t bucket_index_words(bool wide);
-hipError_t launch_bucket_index(const TileDesc* d_tiles, uint32_t ntiles, bool wide, uint32_t* out,
+uint32_t bucket_index_words(uint32_t tile_slots);
+hipError_t launch_bucket_index(const TileDesc* d_tiles, uint32_t ntiles, uint32_t tile_slots,
+                               uint32_t* out,
                                hipStream_t stream);
 hipError_t launch_aggregate_tile_packed(int dtype, int m, const TileDesc* d_tiles,
                                         uint32_t ntiles, hipStream_t stream);

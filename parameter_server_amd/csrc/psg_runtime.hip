@@ -300,11 +300,10 @@ struct JobTable {
     size_t off = align_up(sizeof(JobDev) * jobs.size(), 256);
     const size_t tiles_off = off;
     off = align_up(off + sizeof(psg::TileDesc) * tiles, 256);
-    // the packed kernel's tiles are the 64-push form's (2048 slots, one
-    // bucket per slot, the same bucket map): the same index serves both
+    // one bucket per slot in every kernel (the same bucket map): the index
+    // depends only on D and the tile size
     const bool use_index = index && !dense;
-    const bool iwide = wide || pack;
-    const uint32_t iw = psg::bucket_index_words(iwide);
+    const uint32_t iw = psg::bucket_index_words(tile);
     const size_t index_off = off;
     if (use_index) off = align_up(off + 4 * (size_t)iw * tiles, 256);
     const size_t sitems_off = off;
@@ -448,7 +447,7 @@ struct JobTable {
       HIP_TRY(hipMemcpyAsync(blob, img, off, hipMemcpyHostToDevice, strm));
     HIP_TRY(hipEventRecord(himg_ev[ib], strm));
     if (use_index)
-      HIP_TRY(psg::launch_bucket_index(d_tiles, ntiles, iwide,
+      HIP_TRY(psg::launch_bucket_index(d_tiles, ntiles, tile,
                                        (uint32_t*)((char*)blob + index_off), strm));
     if (!async) HIP_TRY(hipStreamSynchronize(strm));
     return PSG_OK;

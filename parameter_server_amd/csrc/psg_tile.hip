@@ -558,12 +558,12 @@ __global__ __launch_bounds__(nt_of(kGroup), (occupancy<V, M, kGroup>())) void ti
 // built once at plan creation: the plan contract fixes D for its
 // lifetime).  Exactly the tile kernel's histogram + scan with the same
 // bucket map, written out as the kNB u16 bucket starts of each tile.
-template <int kGroup>
-__global__ __launch_bounds__(nt_of(kGroup)) void bucket_index_kernel(
+template <int kTSl>
+__global__ __launch_bounds__(kTSl / 4) void bucket_index_kernel(
     const TileDesc* __restrict__ tiles, uint32_t ntiles, uint32_t* __restrict__ out) {
-  constexpr int kNT = nt_of(kGroup);
+  constexpr int kNT = kTSl / 4;
   constexpr int kNW = kNT / 64;
-  constexpr int kNB = nb_of(kGroup);
+  constexpr int kNB = kTSl;  // one bucket per slot (every kernel's map)
   constexpr int kBPT = kNB / kNT;
   __shared__ __attribute__((aligned(16))) uint32_t bt32[(kNB + 8) / 2];
   __shared__ uint32_t wsum[kNW];
@@ -650,17 +650,27 @@ extern "C" int psg_debug_phases(uint32_t* out, uint32_t ntiles) {
 }
 #endif
 
-uint32_t bucket_index_words(bool wide) { return (uint32_t)(wide ? nb_of(64) : nb_of(32)) / 2u; }
+uint32_t bucket_index_words(uint32_t tile_slots) { return tile_slots / 2u; }
 
-hipError_t launch_bucket_index(const TileDesc* d_tiles, uint32_t ntiles, bool wide, uint32_t* out,
-                               hipStream_t stream) {
+hipError_t launch_bucket_index(const TileDesc* d_tiles, uint32_t ntiles, uint32_t tile_slots,
+                               uint32_t* out, hipStream_t stream) {
   if (ntiles == 0) return hipSuccess;
-  if (wide)
-    hipLaunchKernelGGL(bucket_index_kernel<64>, dim3(ntiles), dim3(nt_of(64)), 0, stream, d_tiles,
-                       ntiles, out);
-  else
-    hipLaunchKernelGGL(bucket_index_kernel<32>, dim3(ntiles), dim3(nt_of(32)), 0, stream, d_tiles,
-                       ntiles, out);
+  switch (tile_slots) {
+    case 1024:
+      hipLaunchKernelGGL(bucket_index_kernel<1024>, dim3(ntiles), dim3(256), 0, stream, d_tiles,
+                         ntiles, out);
+      break;
+    case 2048:
+      hipLaunchKernelGGL(bucket_index_kernel<2048>, dim3(ntiles), dim3(512), 0, stream, d_tiles,
+                         ntiles, out);
+      break;
+    case 4096:
+      hipLaunchKernelGGL(bucket_index_kernel<4096>, dim3(ntiles), dim3(1024), 0, stream, d_tiles,
+                         ntiles, out);
+      break;
+    default:
+      return hipErrorInvalidValue;
+  }
   return hipGetLastError();
 }
 

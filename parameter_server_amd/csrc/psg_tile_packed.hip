@@ -67,7 +67,7 @@ __device__ __forceinline__ AS1 T* GW(T* p) {
 #endif
 
 constexpr int kTS = kPackTileSlots;  // slots per tile
-constexpr int kNT = 512;             // threads
+constexpr int kNT = kTS / 4;         // threads (512 for 2048-slot tiles)
 constexpr int kNW = kNT / 64;    // waves
 constexpr int kSPT = kTS / kNT;  // slots per thread (contiguous)
 constexpr int kNB = kTS;         // buckets (one per slot: the LDS budget of 4 workgroups per CU)
@@ -106,9 +106,16 @@ __device__ __forceinline__ uint32_t wave_scan_incl(uint32_t x) {
 
 // waves per SIMD the LDS allows (8 for the f32, m = 1 case: 4 workgroups per CU):
 // the register budget follows it through __launch_bounds__
+// D, buckets, sums, last-push marks, group tables, element map, bitmap,
+// per-wave words (40.9 KB for 2048-slot tiles, f32, m = 1)
+template <typename V, int M>
+constexpr int lds_bytes() {
+  return (kTS + 8) * 8 + (kTS + 8) * 2 + M * (int)sizeof(V) * kTS + 2 * kTS + 4 * (kG + 1) +
+         kECap + 8 * kG * (1 + M) + kTS / 8 + 12 * kNW + 48;
+}
 template <typename V, int M>
 constexpr int occupancy() {
-  constexpr int lds = 40900 + (int)(M * sizeof(V) - 4) * kTS + (M - 1) * 8 * kG;
+  constexpr int lds = lds_bytes<V, M>();
   // waves per SIMD (the launch bound's unit): workgroups per CU x waves / 4
   constexpr int w = (163840 / lds) * kNW / 4;
   return w >= 8 ? 8 : (w < 1 ? 1 : w);
@@ -669,8 +676,12 @@ __global__ __launch_bounds__(kNT, (occupancy<V, M>())) void tile_packed_kernel(
 
 template <typename V, int M>
 hipError_t go(const TileDesc* t, uint32_t n, hipStream_t s) {
-  hipLaunchKernelGGL((tile_packed_kernel<V, M>), dim3(n), dim3(kNT), 0, s, t, n);
-  return hipGetLastError();
+  if constexpr (lds_bytes<V, M>() <= 163840) {
+    hipLaunchKernelGGL((tile_packed_kernel<V, M>), dim3(n), dim3(kNT), 0, s, t, n);
+    return hipGetLastError();
+  } else {
+    return hipErrorInvalidValue;  // larger tiles (A/B builds) hold fewer value arrays
+  }
 }
 
 template <typename V>
