@@ -84,6 +84,12 @@ typedef unsigned long long u64x2 __attribute__((ext_vector_type(2)));
 typedef uint32_t u32x2 __attribute__((ext_vector_type(2)));
 
 __device__ __forceinline__ uint32_t uni(uint32_t v) { return __builtin_amdgcn_readfirstlane(v); }
+// the lane index recomputed from nothing (mbcnt over a full mask), so a value
+// needed late in the kernel does not keep the thread-id register live (at 64
+// VGPRs it is the value that would be spilled to scratch: HBM writes)
+__device__ __forceinline__ uint32_t lane_id() {
+  return __builtin_amdgcn_mbcnt_hi(~0u, __builtin_amdgcn_mbcnt_lo(~0u, 0u));
+}
 
 // blocks b and b+8 share an XCD (observed dispatch, speed only): give each
 // XCD a contiguous run of tiles
@@ -191,7 +197,7 @@ __global__ __launch_bounds__(kNT, (occupancy<V, M>())) void tile_packed_kernel(
       // a fresh copy of the lane id per call: otherwise the compiler hoists
       // the lane-derived LDS addresses out of the push-group loop and, at
       // 64 VGPRs, spills them to scratch in every workgroup (HBM writes)
-      int lane = tid & 63;
+      int lane = (int)lane_id();
       asm volatile("" : "+v"(lane));
       tgq = np - g0 < (uint32_t)kG ? np - g0 : (uint32_t)kG;
       uint32_t len[2], ov[2];
@@ -234,7 +240,7 @@ __global__ __launch_bounds__(kNT, (occupancy<V, M>())) void tile_packed_kernel(
   };
   auto tables_b = [&](uint32_t g0) {
     if (w < 2) {
-      int lane = tid & 63;
+      int lane = (int)lane_id();
       asm volatile("" : "+v"(lane));
       const uint32_t base = w == 1 ? uni(gsh[2]) : 0u;
       uint32_t xl[2], pl[2];
@@ -630,14 +636,14 @@ __global__ __launch_bounds__(kNT, (occupancy<V, M>())) void tile_packed_kernel(
       continue;
     }
     U = 0;  // group finished
-    if (tid == 0) pcarry = -1;
+    if (w == 0 && lane_id() == 0u) pcarry = -1;
   }
 
   // ---- trailing "+0.0" of absent last pushes (serial), stores
   const uint32_t gl = g0 - gp;  // base of the last group (0 without pushes)
   // the slot offset afresh (an opaque thread id): kept live across the main
   // loop it is the one value the 64-VGPR budget spills to scratch
-  uint32_t s0 = (uint32_t)threadIdx.x;
+  uint32_t s0 = 64u * w + lane_id();
   asm volatile("" : "+v"(s0));
   s0 *= 4u;
   V res[M][4];
