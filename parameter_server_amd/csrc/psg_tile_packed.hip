@@ -546,30 +546,42 @@ __global__ __launch_bounds__(kNT, (occupancy<V, M>())) void tile_packed_kernel(
 #endif
     const uint32_t inpass = (U - done) < kNW * Rw ? U - done : kNW * Rw;
     const uint32_t wl = (inpass - 1) / Rw;  // wave holding the pass's last round
+    // ---- rounds holding several pushes: do two of them hit one slot?
+    // cl[r] (wave-uniform): the lanes of round r that found their slot's bit
+    // already set -- each names a slot hit more than once in the round.
+    // Plans: every wave at once, each with its own bitmap in the bucket
+    // table's LDS (free once every search of the pass is done, (5); put back
+    // from the resident index if another pass or group searches); context
+    // flushes: inside the wave's fold step, with the one shared bitmap.
+    unsigned long long cl[kCap];
+#pragma unroll
+    for (int r = 0; r < kCap; ++r) cl[r] = 0;
+    auto collide = [&](uint32_t* cb) {
+      if (mmask) {
+#pragma unroll
+        for (int r = 0; r < kCap; ++r) {
+          if ((mmask >> r) & 1u) {
+            const bool ok = (okm >> (8 + r)) & 1u;
+            const uint32_t s = pos[r], bit = 1u << (s & 31u);
+            uint32_t old = 0;
+            if (ok) old = __hip_atomic_fetch_or(&cb[s >> 5], bit, __ATOMIC_RELAXED,
+                                                __HIP_MEMORY_SCOPE_WAVEFRONT);
+            cl[r] = __ballot(ok && (old & bit));
+            if (ok) cb[s >> 5] = 0u;
+          }
+        }
+      }
+    };
+    static_assert(kNW * (kTS / 32) <= (kNB + 8) / 2 && kTS / 32 == 64, "per-wave bitmaps in bt");
+    if (Bg) {
+      uint32_t* const cb = bt32 + w * (kTS / 32);
+      cb[lane_id()] = 0u;  // this wave's bitmap (its own LDS accesses stay in order)
+      collide(cb);
+    }
     // ---- fold, wave by wave (rounds are push-major)
     for (uint32_t st = 0; st < (uint32_t)kNW; ++st) {
       if (st == w) {
-        // rounds holding several pushes: do two of them hit one slot?
-        // cl[r] (wave-uniform): the lanes of round r that found their slot's
-        // bit already set -- each names a slot hit more than once in the
-        // round (the bitmap is this wave's during its step)
-        unsigned long long cl[kCap];
-#pragma unroll
-        for (int r = 0; r < kCap; ++r) cl[r] = 0;
-        if (mmask) {
-#pragma unroll
-          for (int r = 0; r < kCap; ++r) {
-            if ((mmask >> r) & 1u) {
-              const bool ok = (okm >> (8 + r)) & 1u;
-              const uint32_t s = pos[r], bit = 1u << (s & 31u);
-              uint32_t old = 0;
-              if (ok) old = __hip_atomic_fetch_or(&cbits[s >> 5], bit, __ATOMIC_RELAXED,
-                                                  __HIP_MEMORY_SCOPE_WAVEFRONT);
-              cl[r] = __ballot(ok && (old & bit));
-              if (ok) cbits[s >> 5] = 0u;
-            }
-          }
-        }
+        if (!Bg) collide(cbits);
 #pragma unroll
         for (int r = 0; r < kCap; ++r) {
           if ((uint32_t)r < nrw) {
@@ -626,6 +638,13 @@ __global__ __launch_bounds__(kNT, (occupancy<V, M>())) void tile_packed_kernel(
         }
         if (w == wl && lane == 63) pcarry = mylast;
       }
+      __syncthreads();
+    }
+    // the bucket table back from the resident index when another pass or
+    // group searches it (its first half held the collision bitmaps)
+    if (Bg && (done + kNW * Rw < U || g0 + gp < np)) {
+      const uint32_t t = 64u * w + lane_id();
+      *(u32x2*)&bt[t * kBPT] = __builtin_nontemporal_load((const AS1 u32x2*)Bg + t);
       __syncthreads();
     }
 
