@@ -117,7 +117,7 @@ __device__ __forceinline__ uint32_t wave_scan_incl(uint32_t x) {
 template <typename V, int M>
 constexpr int lds_bytes() {
   return (kTS + 8) * 8 + (kTS + 8) * 2 + M * (int)sizeof(V) * kTS + 2 * kTS + 4 * (kG + 1) +
-         kECap + 8 * kG * (1 + M) + kTS / 8 + 12 * kNW + 48;
+         kECap + 8 * kG * (1 + M) + 12 * kNW + 48;
 }
 template <typename V, int M>
 constexpr int occupancy() {
@@ -146,10 +146,6 @@ __global__ __launch_bounds__(kNT, (occupancy<V, M>())) void tile_packed_kernel(
   __shared__ uint32_t pre[kG + 1];
   __shared__ uint8_t ep[kECap];
   __shared__ uint64_t pkp[kG], pvp[kG * M];  // piece starts (keys, values)
-  // slot bitmap of the collision test, used by one wave at a time (inside
-  // its fold step): one bitmap instead of one per wave keeps 4 workgroups
-  // per CU with 256-push groups
-  __shared__ uint32_t cbits[kTS / 32];
   __shared__ int lastpos[kNW];
   __shared__ int pcarry;
   __shared__ uint32_t wsum[kNW];
@@ -340,7 +336,6 @@ __global__ __launch_bounds__(kNT, (occupancy<V, M>())) void tile_packed_kernel(
     asm volatile("" : "+v"(z));
     *(u32x2*)&bt[tid * kBPT] = Bg ? btw : u32x2{z, z};  // resident table, or a cleared histogram
     if (Bg && tid == 0) bt[kNB] = (uint16_t)nt;
-    if (tid < kTS / 32) cbits[tid] = z;
   }
   if (tid == 0) pcarry = -1;
   __syncthreads();  // (1) pieces scanned, D, cleared histogram (or the resident bucket table)
@@ -392,42 +387,53 @@ __global__ __launch_bounds__(kNT, (occupancy<V, M>())) void tile_packed_kernel(
 
   // ---- bucket table: histogram, exclusive scan -> bt[b] = first slot of bucket b
   // (skipped when the plan's resident index supplied it).  D keys back from
-  // LDS: the registers that held them are free during the pass's element loads
-  if (!Bg) {
-  const u64x2 y0 = *(const u64x2*)&dk[s0i];
-  const u64x2 y1 = *(const u64x2*)&dk[s0i + 2];
-  const uint64_t dd[4] = {y0.x, y0.y, y1.x, y1.y};
-#pragma unroll
-  for (int j = 0; j < 4; ++j)
-    if (s0i + j < nt)
-    {  // counts <= kTS < 2^16: no carry between the packed halves
-      const uint32_t b = bucket(dd[j]);
-      __hip_atomic_fetch_add(&bt32[b >> 1], 1u << (16 * (b & 1u)), __ATOMIC_RELAXED,
-                             __HIP_MEMORY_SCOPE_WORKGROUP);
+  // LDS: the registers that held them are free during the pass's element
+  // loads.  `again`: a rebuild after the collision bitmaps used the table's
+  // LDS (context flushes whose tile takes another pass): cleared first.
+  auto build_bt = [&](bool again) {
+    const uint32_t t = 64u * w + lane_id();
+    const uint32_t sb = 4u * t;
+    if (again) {
+      uint32_t z = 0;
+      asm volatile("" : "+v"(z));
+      *(u32x2*)&bt[t * kBPT] = u32x2{z, z};
+      __syncthreads();
     }
-  __syncthreads();  // (2)
-  {
-    const u32x2 h = *(const u32x2*)&bt[tid * kBPT];
-    uint32_t e[kBPT] = {h.x & 0xffffu, h.x >> 16, h.y & 0xffffu, h.y >> 16};
-    uint32_t tot = 0;
+    const u64x2 y0 = *(const u64x2*)&dk[sb];
+    const u64x2 y1 = *(const u64x2*)&dk[sb + 2];
+    const uint64_t dd[4] = {y0.x, y0.y, y1.x, y1.y};
 #pragma unroll
-    for (int j = 0; j < kBPT; ++j) {
-      const uint32_t c = e[j];
-      e[j] = tot;
-      tot += c;
+    for (int j = 0; j < 4; ++j)
+      if (sb + j < nt)
+      {  // counts <= kTS < 2^16: no carry between the packed halves
+        const uint32_t b = bucket(dd[j]);
+        __hip_atomic_fetch_add(&bt32[b >> 1], 1u << (16 * (b & 1u)), __ATOMIC_RELAXED,
+                               __HIP_MEMORY_SCOPE_WORKGROUP);
+      }
+    __syncthreads();  // (2)
+    {
+      const u32x2 h = *(const u32x2*)&bt[t * kBPT];
+      uint32_t e[kBPT] = {h.x & 0xffffu, h.x >> 16, h.y & 0xffffu, h.y >> 16};
+      uint32_t tot = 0;
+#pragma unroll
+      for (int j = 0; j < kBPT; ++j) {
+        const uint32_t c = e[j];
+        e[j] = tot;
+        tot += c;
+      }
+      const uint32_t x = wave_scan_incl(tot);
+      if (lane_id() == 63u) wsum[w] = x;
+      __syncthreads();  // (3)
+      uint32_t off = x - tot;
+#pragma unroll
+      for (uint32_t v = 0; v < (uint32_t)kNW - 1u; ++v) off += v < w ? wsum[v] : 0u;
+      const u32x2 o = {(e[0] + off) | (e[1] + off) << 16, (e[2] + off) | (e[3] + off) << 16};
+      *(u32x2*)&bt[t * kBPT] = o;
+      if (t == 0) bt[kNB] = (uint16_t)nt;
     }
-    const uint32_t x = wave_scan_incl(tot);
-    if (lane == 63) wsum[w] = x;
-    __syncthreads();  // (3)
-    uint32_t off = x - tot;
-#pragma unroll
-    for (uint32_t v = 0; v < (uint32_t)kNW - 1u; ++v) off += v < w ? wsum[v] : 0u;
-    const u32x2 o = {(e[0] + off) | (e[1] + off) << 16, (e[2] + off) | (e[3] + off) << 16};
-    *(u32x2*)&bt[tid * kBPT] = o;
-    if (tid == 0) bt[kNB] = (uint16_t)nt;
-  }
-  __syncthreads();  // (4)
-  }
+    __syncthreads();  // (4)
+  };
+  if (!Bg) build_bt(false);
 
   for (;;) {
     if (!U) {  // this group of pushes has no keys in the tile, or is done
@@ -549,10 +555,9 @@ __global__ __launch_bounds__(kNT, (occupancy<V, M>())) void tile_packed_kernel(
     // ---- rounds holding several pushes: do two of them hit one slot?
     // cl[r] (wave-uniform): the lanes of round r that found their slot's bit
     // already set -- each names a slot hit more than once in the round.
-    // Plans: every wave at once, each with its own bitmap in the bucket
-    // table's LDS (free once every search of the pass is done, (5); put back
-    // from the resident index if another pass or group searches); context
-    // flushes: inside the wave's fold step, with the one shared bitmap.
+    // Every wave at once, each with its own bitmap in the bucket table's LDS
+    // (free once every search of the pass is done, (5); put back -- from the
+    // plan's resident index, or rebuilt -- if another pass or group searches).
     unsigned long long cl[kCap];
 #pragma unroll
     for (int r = 0; r < kCap; ++r) cl[r] = 0;
@@ -573,7 +578,7 @@ __global__ __launch_bounds__(kNT, (occupancy<V, M>())) void tile_packed_kernel(
       }
     };
     static_assert(kNW * (kTS / 32) <= (kNB + 8) / 2 && kTS / 32 == 64, "per-wave bitmaps in bt");
-    if (Bg) {
+    {
       uint32_t* const cb = bt32 + w * (kTS / 32);
       cb[lane_id()] = 0u;  // this wave's bitmap (its own LDS accesses stay in order)
       collide(cb);
@@ -581,7 +586,6 @@ __global__ __launch_bounds__(kNT, (occupancy<V, M>())) void tile_packed_kernel(
     // ---- fold, wave by wave (rounds are push-major)
     for (uint32_t st = 0; st < (uint32_t)kNW; ++st) {
       if (st == w) {
-        if (!Bg) collide(cbits);
 #pragma unroll
         for (int r = 0; r < kCap; ++r) {
           if ((uint32_t)r < nrw) {
@@ -642,10 +646,14 @@ __global__ __launch_bounds__(kNT, (occupancy<V, M>())) void tile_packed_kernel(
     }
     // the bucket table back from the resident index when another pass or
     // group searches it (its first half held the collision bitmaps)
-    if (Bg && (done + kNW * Rw < U || g0 + gp < np)) {
-      const uint32_t t = 64u * w + lane_id();
-      *(u32x2*)&bt[t * kBPT] = __builtin_nontemporal_load((const AS1 u32x2*)Bg + t);
-      __syncthreads();
+    if (done + kNW * Rw < U || g0 + gp < np) {
+      if (Bg) {
+        const uint32_t t = 64u * w + lane_id();
+        *(u32x2*)&bt[t * kBPT] = __builtin_nontemporal_load((const AS1 u32x2*)Bg + t);
+        __syncthreads();
+      } else {
+        build_bt(true);
+      }
     }
 
     // ---- next pass, or next group of pushes
