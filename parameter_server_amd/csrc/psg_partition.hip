@@ -177,10 +177,34 @@ __device__ __forceinline__ void stream_item(const JobDev& J, uint32_t p, uint32_
   uint64_t w0 = ~0ull, w1 = ~0ull;
   int32_t win = -1;
   if (i0 > 0) {
+    // a first window guessed from the chunk's position in the push (pushes
+    // of hashed keys spread over the job's key range like D does), loaded
+    // together with the chunk's keys and S[i0-1]: when it brackets S[i0-1]
+    // (most chunks) the interpolated window below, which waits for
+    // S[i0-1], is not needed
+    int64_t gq = (int64_t)((double)i0 / (double)n * (double)nt) - 32;
+    gq = gq + 128 > (int64_t)nt + 1 ? (int64_t)nt + 1 - 128 : gq;
+    gq = gq < 0 ? 0 : gq;
+    const int64_t tq = gq + lane;
+    const uint64_t q0 = tq <= (int64_t)nt ? sp[tq] : ~0ull;
+    const uint64_t q1 = tq + 64 <= (int64_t)nt ? sp[tq + 64] : ~0ull;
     const uint64_t kp = uni64(S[i0 - 1]);
     const uint64_t s0 = uni64(sp[0]), sn = uni64(sp[nt]);
+    uint32_t qc = 64;  // splitters <= kp in the guessed window (64+: not usable)
+    if (kp >= s0 && kp < sn) {
+      qc = (uint32_t)__popcll(__ballot(tq <= (int64_t)nt && q0 <= kp));
+      if (qc == 64u) qc += (uint32_t)__popcll(__ballot(tq + 64 <= (int64_t)nt && q1 <= kp));
+    }
     if (kp >= sn) {
       T0 = nt;
+    } else if (kp >= s0 && (qc > 0 || gq == 0) && qc < 64u) {
+      // T0 + 1 is the window's splitter qc (< 64): the first pass reads
+      // splitters qc .. qc + 63 of the 128 in registers
+      g = gq;
+      w0 = q0;
+      w1 = q1;
+      T0 = g + (int64_t)qc - 1;
+      win = (int32_t)qc;
     } else if (kp >= s0) {
       const double f = (double)(kp - s0) / (double)(sn - s0);
       g = (int64_t)(f * (double)nt) - 24;
