@@ -1068,7 +1068,10 @@ def cpu_baseline(inst, seconds):
     except AttributeError:
         share = os.cpu_count() or 1
     par = {}
-    for nt in sorted({4, max(1, min(16, share))}):
+    # 4 threads (local.sh:25) and nproc; plus this job's CPU
+    # share (16 on the GPU box, whose cgroup quota also throttles nproc)
+    nproc = os.cpu_count() or 1
+    for nt in sorted({4, max(1, min(16, share)), nproc}):
         vp, repsp, elp = timed(1, nt)
         par[str(nt)] = {"value": vp, "reps": repsp, "seconds": elp}
     model = ""
