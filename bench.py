@@ -1001,7 +1001,9 @@ def bench_rows(device, reps=5):
     _lib.check(L.psg_freq_resize(v._h, 0, 1 << 26, 4))
     ms = timed(lambda: _lib.check(L.psg_freq_insert_dev(v._h, 0, keys.data_ptr(),
                                                         cnt.data_ptr(), nk, None)))
-    row("countmin_insert", ms, nk * (8 + 4) + nk * 4 * 8, nk, "keys/s")
+    # keys + counts read; per probe one counter byte read and written
+    # (countmin.h:69: uint8 counters, the table 64 MB)
+    row("countmin_insert", ms, nk * (8 + 4) + nk * 4 * 2, nk, "keys/s")
     scratch = torch.empty(L.psg_freq_query_scratch_bytes(nk), dtype=torch.uint8, device=dev)
     qo = torch.empty(nk, dtype=torch.int64, device=dev)
     qn = torch.zeros(1, dtype=torch.int64, device=dev)
@@ -1009,7 +1011,8 @@ def bench_rows(device, reps=5):
                                                        qo.data_ptr(), qn.data_ptr(),
                                                        scratch.data_ptr(), None)))
     kept = int(qn.item())
-    row("countmin_query", ms, nk * 8 * 2 + nk * 4 * 4 * 2 + kept * 8, nk, "keys/s")
+    # keys read by the count and the scatter pass, one byte per probe, kept keys written
+    row("countmin_query", ms, nk * 8 * 2 + nk * 4 + kept * 8, nk, "keys/s")
     v.close()
     del keys, cnt, qo, scratch
     # Darling's server step over 16.8 M f64 positions: the (G, U) aggregate of

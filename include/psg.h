@@ -218,7 +218,14 @@ typedef struct psg_merge_job {
 
 typedef struct psg_plan psg_plan;
 
-/* All jobs share dtype, m and flags; npush <= psg_plan_max_push() per job. */
+/* All jobs share dtype, m and flags; npush <= psg_plan_max_push() per job.
+ * CONTRACT: each job's server keys (the `keys` array, D) must keep their
+ * contents for the plan's lifetime.  The plan builds a bucket index of D at
+ * creation and every run searches with it; if D changes between runs, keys
+ * are misplaced and show up as unmatched in psg_plan_matched.  To merge
+ * against a different D, create a new plan (or pass PSG_NO_INDEX, which
+ * rebuilds the tables from D in every run).  Push keys and values may
+ * change between runs (see PSG_STATIC_KEYS for the one exception). */
 int psg_plan_create(int device, int dtype, int m, unsigned flags,
                     const psg_merge_job* jobs, int njobs, psg_plan** out);
 int psg_plan_max_push(void);
@@ -289,6 +296,15 @@ int psg_comm_unique_id(uint8_t* id);
 int psg_comm_init(int device, int nranks, const uint8_t* id, int rank,
                   psg_comm** out);
 int psg_comm_destroy(psg_comm* comm);
+/* nranks loopback communicators of ONE process on one device (out[r] is
+ * rank r): the exchange's collective rounds run with the same pairing rule
+ * as RCCL's grouped send/recv, each matched pair a device copy.  Each rank
+ * must call the collective functions from its own host thread, all ranks
+ * concurrently (as RCCL ranks do from their own processes); a rank whose
+ * peers do not join within 120 s gets PSG_ERR_DEVICE.  For tests of the
+ * multi-rank path on one GPU (RCCL refuses two ranks on one device).
+ * Destroy every rank's communicator. */
+int psg_comm_init_loopback(int device, int nranks, psg_comm** out);
 
 /* RNode::submit's slice-and-send (remote_node.cc:39-60: KVVector::slice ->
  * sliceKeyOrderedMsg, message.h:89-123) for a batch of npush sorted

@@ -131,6 +131,7 @@ SIGNATURES = {
     "psg_comm_unique_id": (C.c_int, [_p]),
     "psg_comm_init": (C.c_int, [C.c_int, C.c_int, _p, C.c_int, C.POINTER(_p)]),
     "psg_comm_destroy": (C.c_int, [_p]),
+    "psg_comm_init_loopback": (C.c_int, [C.c_int, C.c_int, C.POINTER(_p)]),
     "psg_exchange_create": (C.c_int, [_p, C.c_int, C.c_int, C.c_int, _p, _p, _p,
                                       C.POINTER(_p)]),
     "psg_exchange_run": (C.c_int, [_p, _p]),

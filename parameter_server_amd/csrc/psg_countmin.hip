@@ -10,15 +10,19 @@
 // query = min over probes, starting from 255; queryKeys keeps, in input
 // order, the keys whose query is > freqency.
 //
-// GPU form.  Byte counters under concurrent inserts need a byte-wide
-// atomic add that wraps inside its byte: the table is held as uint32
-// counters instead, added with native 32-bit atomics, and read through
-// their low byte -- exact, since (sum mod 2^32) mod 2^8 = sum mod 2^8 and
-// addition mod 2^8 does not depend on order, so any interleaving of inserts
-// gives the reference's table.  Each counter costs one random 4-byte
-// read-modify-write in L2/HBM either way.  queryKeys is a query pass that
-// keeps one bit per key and an order-preserving compaction of those bits
-// (workgroup scan + one scan of block totals): the table is read once.
+// GPU form.  The table is the reference's: n_ bytes (countmin.h:69,
+// SArray<uint8>), 64 MB for 2^26 counters, so it stays resident in the
+// 256 MB Infinity Cache while keys stream past.  There is no byte-wide
+// global atomic, and a 32-bit add would carry out of the byte: a probe is a
+// compare-and-swap of the aligned dword that holds its byte, the byte
+// replaced by (byte + count) mod 2^8 and the other three kept.  A key's k
+// probes are independent: their dword loads go out together, then rounds of
+// CAS over the probes still pending (a failed CAS returns the current word,
+// the next round retries with it).  Addition mod 2^8 does not depend on
+// order, so any interleaving of inserts gives the reference's table
+// byte for byte.  queryKeys is a query pass that keeps one bit per key and an
+// order-preserving compaction of those bits (workgroup scan + one scan of
+// block totals): the table is read once.
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
@@ -48,22 +52,29 @@ __device__ __forceinline__ uint32_t cm_hash(uint64_t key) {
   return h;
 }
 
-__device__ __forceinline__ uint32_t cm_query(const uint32_t* __restrict__ t, uint32_t n, int k,
+__device__ __forceinline__ uint32_t cm_query(const uint8_t* __restrict__ t, uint32_t n, int k,
                                              uint64_t key) {
   uint32_t res = 255u;  // (uint8)kuint64max
   uint32_t h = cm_hash(key);
   const uint32_t delta = (h >> 17) | (h << 15);
   for (int j = 0; j < k; ++j) {
-    const uint32_t v = t[h % n] & 0xffu;
+    const uint32_t v = t[h % n];
     res = v < res ? v : res;
     h += delta;
   }
   return res;
 }
 
+constexpr int kProbeRegs = 8;  // probes held in registers (k <= 8: every app's k)
+
+__device__ __forceinline__ uint32_t byte_add(uint32_t w, uint32_t sh, uint32_t c) {
+  const uint32_t nb = ((w >> sh) + c) & 0xffu;
+  return (w & ~(0xffu << sh)) | (nb << sh);
+}
+
 __global__ __launch_bounds__(kNT) void cm_insert_kernel(const uint64_t* __restrict__ keys,
                                                         const uint32_t* __restrict__ counts,
-                                                        uint64_t nk, uint32_t* __restrict__ t,
+                                                        uint64_t nk, uint8_t* __restrict__ t,
                                                         uint32_t n, int k) {
   const uint64_t i = (uint64_t)blockIdx.x * kNT + threadIdx.x;
   if (i >= nk) return;
@@ -71,8 +82,42 @@ __global__ __launch_bounds__(kNT) void cm_insert_kernel(const uint64_t* __restri
   if (!c) return;
   uint32_t h = cm_hash(keys[i]);
   const uint32_t delta = (h >> 17) | (h << 15);
+  if (k <= kProbeRegs) {
+    uint32_t* wp[kProbeRegs];
+    uint32_t sh[kProbeRegs], old[kProbeRegs];
+#pragma unroll
+    for (int j = 0; j < kProbeRegs; ++j) {
+      if (j < k) {
+        const uint32_t idx = h % n;
+        wp[j] = (uint32_t*)(t + (idx & ~3u));
+        sh[j] = 8u * (idx & 3u);
+        old[j] = __hip_atomic_load(wp[j], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        h += delta;
+      }
+    }
+    uint32_t pend = (1u << k) - 1u;
+    while (pend) {
+#pragma unroll
+      for (int j = 0; j < kProbeRegs; ++j) {
+        if ((pend >> j) & 1u) {
+          const uint32_t seen = atomicCAS(wp[j], old[j], byte_add(old[j], sh[j], c));
+          if (seen == old[j]) pend &= ~(1u << j);
+          else old[j] = seen;
+        }
+      }
+    }
+    return;
+  }
   for (int j = 0; j < k; ++j) {
-    __hip_atomic_fetch_add(t + h % n, c, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    const uint32_t idx = h % n;
+    uint32_t* w = (uint32_t*)(t + (idx & ~3u));
+    const uint32_t s8 = 8u * (idx & 3u);
+    uint32_t o = __hip_atomic_load(w, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    for (;;) {
+      const uint32_t seen = atomicCAS(w, o, byte_add(o, s8, c));
+      if (seen == o) break;
+      o = seen;
+    }
     h += delta;
   }
 }
@@ -82,7 +127,7 @@ __global__ __launch_bounds__(kNT) void cm_insert_kernel(const uint64_t* __restri
 // workgroup tile.  Thread-contiguous runs of kIPT keys, so the bits are in
 // input order; pass 3 reads the bits instead of querying the table again.
 __global__ __launch_bounds__(kNT) void cm_count_kernel(const uint64_t* __restrict__ keys,
-                                                       uint64_t nk, const uint32_t* __restrict__ t,
+                                                       uint64_t nk, const uint8_t* __restrict__ t,
                                                        uint32_t n, int k, int freq,
                                                        uint32_t* __restrict__ tile_cnt,
                                                        uint8_t* __restrict__ keep_bits) {
@@ -147,7 +192,7 @@ __global__ __launch_bounds__(kNT) void cm_scatter_kernel(const uint64_t* __restr
 }  // namespace
 
 hipError_t launch_cm_insert(const uint64_t* keys, const uint32_t* counts, uint64_t nk,
-                            uint32_t* table, uint32_t n, int k, hipStream_t s) {
+                            uint8_t* table, uint32_t n, int k, hipStream_t s) {
   if (nk == 0) return hipSuccess;
   hipLaunchKernelGGL(cm_insert_kernel, dim3((uint32_t)((nk + kNT - 1) / kNT)), dim3(kNT), 0, s,
                      keys, counts, nk, table, n, k);
@@ -160,7 +205,7 @@ size_t cm_query_scratch_bytes(uint64_t nk) {
   return ((4 * ntiles + 255) / 256) * 256 + ntiles * kNT + 64;
 }
 
-hipError_t launch_cm_query(const uint64_t* keys, uint64_t nk, const uint32_t* table, uint32_t n,
+hipError_t launch_cm_query(const uint64_t* keys, uint64_t nk, const uint8_t* table, uint32_t n,
                            int k, int freq, uint64_t* out, unsigned long long* nout,
                            void* scratch, hipStream_t s) {
   const uint32_t ntiles = (uint32_t)((nk + kQTile - 1) / kQTile);

@@ -27,10 +27,28 @@
 // one device with no communicator: a step re-cuts and packs, and
 // psg_exchange_send_layout hands out the packed buffers (tests of the
 // multi-shard layout on one GPU, SURVEY 4 "8 shards on 1 device").
+//
+// Transport.  Both rounds (counts at create, payload per run) are one group
+// of point-to-point sends and receives (xport_group).  A communicator from
+// psg_comm_init runs the group over RCCL (ncclGroupStart / ncclSend /
+// ncclRecv / ncclGroupEnd on the caller's stream); one from
+// psg_comm_init_loopback is one of S ranks living in this process on one
+// device (one host thread per rank, as RCCL ranks are one process each): a
+// rank's sends and receives are matched in posting order per (source,
+// destination) pair, exactly RCCL's pairing rule, and each matched pair is
+// a device copy on the receiver's stream ordered after the sender's stream.
+// The count round, the layout and the pairing code are the same for both,
+// so the multi-rank path runs on one GPU before it meets xGMI (RCCL itself
+// refuses two ranks on one device).
 #include <hip/hip_runtime.h>
 #include <rccl/rccl.h>
 
+#include <chrono>
+#include <condition_variable>
 #include <cstring>
+#include <deque>
+#include <memory>
+#include <mutex>
 #include <vector>
 
 #include "psg_device.h"
@@ -134,10 +152,169 @@ __global__ __launch_bounds__(256) void pack_kernel(const Piece* __restrict__ pie
 
 }  // namespace
 
+namespace {
+
+// One point-to-point operation of a transport group.
+struct XOp {
+  bool send;
+  int peer;
+  void* buf;
+  size_t bytes;
+};
+
+// ---- loopback hub: S ranks of one process on one device.  Sends and
+// receives queue per ordered (source, destination) pair; the k-th send of
+// src to dst pairs with the k-th receive of dst from src (RCCL's rule within
+// and across groups).  Whoever completes a pair issues its copy: the
+// receiver's stream waits for the sender's "data ready" event, copies, and
+// records the pair's "copied" event, which the sender's stream then waits
+// for before it may overwrite the send buffer (no host wait on the data).
+struct LoopPair {
+  // send side
+  const void* src = nullptr;
+  size_t sbytes = 0;
+  hipEvent_t ready = nullptr;  // recorded on the sender's stream at group end
+  // receive side
+  void* dst = nullptr;
+  size_t rbytes = 0;
+  hipStream_t rstream = nullptr;
+  // result
+  bool have_send = false, have_recv = false, done = false;
+  int status = PSG_OK;
+  hipEvent_t copied = nullptr;
+  int users = 2;  // sender + receiver; the last one to leave frees the events
+};
+
+struct LoopHub {
+  int S = 0, device = 0;
+  std::mutex mu;
+  std::condition_variable cv;
+  // per ordered pair src * S + dst: pairs in posting order not yet completed
+  std::vector<std::deque<std::shared_ptr<LoopPair>>> q;
+  int refs = 0;
+
+  void complete(LoopPair& P) {  // with mu held; both sides present
+    P.done = true;
+    if (P.sbytes != P.rbytes) {
+      P.status = PSG_ERR_SIZE;
+      return;
+    }
+    hipError_t e = hipEventCreateWithFlags(&P.copied, hipEventDisableTiming);
+    if (e == hipSuccess) e = hipStreamWaitEvent(P.rstream, P.ready, 0);
+    if (e == hipSuccess && P.sbytes)
+      e = hipMemcpyAsync(P.dst, P.src, P.sbytes, hipMemcpyDeviceToDevice, P.rstream);
+    if (e == hipSuccess) e = hipEventRecord(P.copied, P.rstream);
+    if (e != hipSuccess) P.status = PSG_ERR_DEVICE;
+  }
+  static void leave(LoopPair& P) {  // with mu held
+    if (--P.users == 0) {
+      if (P.ready) (void)hipEventDestroy(P.ready);
+      if (P.copied) (void)hipEventDestroy(P.copied);
+      P.ready = P.copied = nullptr;
+    }
+  }
+};
+
+}  // namespace
+
 struct psg_comm {
   ncclComm_t nccl = nullptr;
+  LoopHub* loop = nullptr;  // loopback rank (psg_comm_init_loopback)
   int device = 0, nranks = 1, rank = 0;
 };
+
+namespace {
+
+// seconds a loopback rank waits for its peers to post their side of a group
+constexpr int kLoopTimeoutS = 120;
+
+int loop_group(psg_comm* c, hipStream_t st, const std::vector<XOp>& ops) {
+  LoopHub& H = *c->loop;
+  const int S = H.S, me = c->rank;
+  for (const XOp& o : ops)
+    if (o.peer < 0 || o.peer >= S) return fail(PSG_ERR_ARG, "loopback peer %d", o.peer);
+  // a "data ready" event per send: everything enqueued on `st` so far
+  std::vector<hipEvent_t> ready(ops.size(), nullptr);
+  for (size_t i = 0; i < ops.size(); ++i)
+    if (ops[i].send) {
+      hipError_t e = hipEventCreateWithFlags(&ready[i], hipEventDisableTiming);
+      if (e == hipSuccess) e = hipEventRecord(ready[i], st);
+      if (e != hipSuccess) {
+        for (hipEvent_t x : ready)
+          if (x) (void)hipEventDestroy(x);
+        return fail(PSG_ERR_DEVICE, "loopback event: %s", hipGetErrorString(e));
+      }
+    }
+  std::vector<std::shared_ptr<LoopPair>> mine;
+  std::unique_lock<std::mutex> lk(H.mu);
+  for (size_t i = 0; i < ops.size(); ++i) {
+    const XOp& o = ops[i];
+    auto& qq = o.send ? H.q[(size_t)me * S + o.peer] : H.q[(size_t)o.peer * S + me];
+    // the oldest pair of this direction still missing this side
+    std::shared_ptr<LoopPair> P;
+    for (auto& x : qq)
+      if (o.send ? !x->have_send : !x->have_recv) {
+        P = x;
+        break;
+      }
+    if (!P) {
+      P = std::make_shared<LoopPair>();
+      qq.push_back(P);
+    }
+    if (o.send) {
+      P->have_send = true;
+      P->src = o.buf;
+      P->sbytes = o.bytes;
+      P->ready = ready[i];
+    } else {
+      P->have_recv = true;
+      P->dst = o.buf;
+      P->rbytes = o.bytes;
+      P->rstream = st;
+    }
+    if (P->have_send && P->have_recv) {
+      H.complete(*P);
+      while (!qq.empty() && qq.front()->done) qq.pop_front();
+      H.cv.notify_all();
+    }
+    mine.push_back(P);
+  }
+  const auto until = std::chrono::steady_clock::now() + std::chrono::seconds(kLoopTimeoutS);
+  int rc = PSG_OK;
+  for (auto& P : mine) {
+    if (!H.cv.wait_until(lk, until, [&] { return P->done; })) {
+      rc = fail(PSG_ERR_DEVICE, "loopback rank %d: a peer did not join the group", me);
+      break;
+    }
+    if (P->status != PSG_OK && rc == PSG_OK)
+      rc = fail(P->status, "loopback rank %d: %s", me,
+                P->status == PSG_ERR_SIZE ? "send and receive sizes differ" : "device copy failed");
+  }
+  // a send buffer is reusable once its copy ran: later work on `st` waits
+  for (size_t i = 0; rc == PSG_OK && i < ops.size(); ++i)
+    if (ops[i].send && mine[i]->copied && hipStreamWaitEvent(st, mine[i]->copied, 0) != hipSuccess)
+      rc = fail(PSG_ERR_DEVICE, "loopback: stream wait");
+  for (auto& P : mine)
+    if (P->done) LoopHub::leave(*P);
+  return rc;
+}
+
+// One transport group: every op of `ops` on stream `st`.
+int xport_group(psg_comm* c, hipStream_t st, const std::vector<XOp>& ops) {
+  if (c->loop) return loop_group(c, st, ops);
+  ncclResult_t r = ncclGroupStart();
+  for (size_t i = 0; r == ncclSuccess && i < ops.size(); ++i) {
+    const XOp& o = ops[i];
+    r = o.send ? ncclSend(o.buf, o.bytes, ncclUint8, o.peer, c->nccl, st)
+               : ncclRecv(o.buf, o.bytes, ncclUint8, o.peer, c->nccl, st);
+  }
+  const ncclResult_t r2 = ncclGroupEnd();
+  if (r != ncclSuccess || r2 != ncclSuccess)
+    return fail(PSG_ERR_DEVICE, "RCCL group: %s", ncclGetErrorString(r != ncclSuccess ? r : r2));
+  return PSG_OK;
+}
+
+}  // namespace
 
 struct psg_exchange {
   psg_comm* comm = nullptr;  // null: a local exchange (S virtual shards, no transport)
@@ -198,9 +375,46 @@ int psg_comm_init(int device, int nranks, const uint8_t* id, int rank, psg_comm*
   return PSG_OK;
 }
 
+int psg_comm_init_loopback(int device, int nranks, psg_comm** out) {
+  if (!out || nranks < 1) return fail(PSG_ERR_ARG, "bad loopback arguments");
+  HIP_TRY(hipSetDevice(device));
+  LoopHub* H = new LoopHub();
+  H->S = nranks;
+  H->device = device;
+  H->q.resize((size_t)nranks * nranks);
+  H->refs = nranks;
+  for (int r = 0; r < nranks; ++r) {
+    psg_comm* c = new psg_comm();
+    c->device = device;
+    c->nranks = nranks;
+    c->rank = r;
+    c->loop = H;
+    out[r] = c;
+  }
+  return PSG_OK;
+}
+
 int psg_comm_destroy(psg_comm* c) {
   if (!c) return PSG_OK;
   if (c->nccl) (void)ncclCommDestroy(c->nccl);
+  if (c->loop) {
+    LoopHub* H = c->loop;
+    bool last;
+    {
+      std::lock_guard<std::mutex> lk(H->mu);
+      last = --H->refs == 0;
+    }
+    if (last) {
+      (void)hipSetDevice(H->device);
+      (void)hipDeviceSynchronize();
+      for (auto& qq : H->q)
+        for (auto& P : qq) {
+          if (P->ready) (void)hipEventDestroy(P->ready);
+          if (P->copied) (void)hipEventDestroy(P->copied);
+        }
+      delete H;
+    }
+  }
   delete c;
   return PSG_OK;
 }
@@ -220,18 +434,21 @@ int exchange_create(psg_comm* comm, int device, int S, int dtype, int m, int npu
   else if (m < 1 || m > PSG_MAX_VALUE_ARRAYS)
     err = fail(PSG_ERR_ARG, "m=%d", m);
   if (err && !comm) return err;
-  if (err) npush = 0;  // take part in the count round with an error word only
   HIP_TRY(hipSetDevice(device));
-  const int P = npush, S1 = S + 1;
+  // an erring rank still takes part in the header round (its npush and an
+  // error word), so every rank fails together instead of waiting on it
+  const int P = npush < 0 ? 0 : npush, S1 = S + 1;
   const int vb = dtype == PSG_F32 ? 4 : 8;
   std::vector<uint64_t> bounds(S1);
   if (int rc = psg_shard_bounds((size_t)S, bounds.data())) return rc;
   hipStream_t st;
   HIP_TRY(hipStreamCreateWithFlags(&st, hipStreamNonBlocking));
-  // ---- set-up block: bounds, push tables, cut positions, counts (+1 error word per peer)
+  // ---- set-up block: bounds, push tables, cut positions, headers {npush,
+  // error} to and from every peer, counts [s][p] to and from every peer
   const size_t o_b = 0, o_k = al(8 * S1), o_n = o_k + al(8 * P), o_pos = o_n + al(8 * P),
-               o_sc = o_pos + al(8 * (size_t)P * S1), o_rc = o_sc + al(8 * (size_t)(P + 1) * S),
-               tot = o_rc + al(8 * (size_t)(P + 1) * S);
+               o_hs = o_pos + al(8 * (size_t)P * S1), o_hr = o_hs + al(16 * (size_t)S),
+               o_sc = o_hr + al(16 * (size_t)S), o_rc = o_sc + al(8 * (size_t)P * S),
+               tot = o_rc + al(8 * (size_t)P * S);
   char* setup = nullptr;
   if (hipMalloc((void**)&setup, tot) != hipSuccess) {
     (void)hipStreamDestroy(st);
@@ -258,7 +475,7 @@ int exchange_create(psg_comm* comm, int device, int S, int dtype, int m, int npu
     if (_e != hipSuccess)                                                            \
       return done(fail(PSG_ERR_DEVICE, "%s: %s", #expr, hipGetErrorString(_e)));   \
   } while (0)
-  if (P) {
+  if (P && !err) {
     X_TRY(hipMemcpyAsync(setup + o_b, bounds.data(), 8 * S1, hipMemcpyHostToDevice, st));
     X_TRY(hipMemcpyAsync(setup + o_k, push_keys, 8 * (size_t)P, hipMemcpyHostToDevice, st));
     X_TRY(hipMemcpyAsync(setup + o_n, push_n, 8 * (size_t)P, hipMemcpyHostToDevice, st));
@@ -308,33 +525,46 @@ int exchange_create(psg_comm* comm, int device, int S, int dtype, int m, int npu
   if (!comm) {
     if (err) return done(err);
   } else {
-    // counts to their shards: P words + the error word to and from every peer
-    std::vector<uint64_t> sc((size_t)(P + 1) * S);
+    // header round: {npush, error} to and from every peer.  Every rank
+    // sees every header, so all decide alike: any error or a differing npush
+    // fails every rank before the count round (whose sizes rest on npush)
+    std::vector<uint64_t> hs(2 * (size_t)S), hr(2 * (size_t)S);
     for (int s = 0; s < S; ++s) {
-      for (int p = 0; p < P; ++p) sc[(size_t)s * (P + 1) + p] = x->send_cnt[(size_t)s * P + p];
-      sc[(size_t)s * (P + 1) + P] = err ? 1u : 0u;
+      hs[2 * (size_t)s] = (uint64_t)P;
+      hs[2 * (size_t)s + 1] = err ? 1u : 0u;
     }
-    X_TRY(hipMemcpyAsync(setup + o_sc, sc.data(), 8 * sc.size(), hipMemcpyHostToDevice, st));
-    ncclResult_t r = ncclGroupStart();
-    for (int s = 0; r == ncclSuccess && s < S; ++s) {
-      r = ncclSend(setup + o_sc + 8 * (size_t)s * (P + 1), P + 1, ncclUint64, s, comm->nccl, st);
-      if (r == ncclSuccess)
-        r = ncclRecv(setup + o_rc + 8 * (size_t)s * (P + 1), P + 1, ncclUint64, s, comm->nccl, st);
+    X_TRY(hipMemcpyAsync(setup + o_hs, hs.data(), 16 * (size_t)S, hipMemcpyHostToDevice, st));
+    std::vector<XOp> ops;
+    for (int s = 0; s < S; ++s) {
+      ops.push_back(XOp{true, s, setup + o_hs + 16 * (size_t)s, 16});
+      ops.push_back(XOp{false, s, setup + o_hr + 16 * (size_t)s, 16});
     }
-    const ncclResult_t r2 = ncclGroupEnd();
-    if (r != ncclSuccess || r2 != ncclSuccess)
-      return done(fail(PSG_ERR_DEVICE, "count exchange: %s",
-                       ncclGetErrorString(r != ncclSuccess ? r : r2)));
-    std::vector<uint64_t> rc((size_t)(P + 1) * S);
-    X_TRY(hipMemcpyAsync(rc.data(), setup + o_rc, 8 * rc.size(), hipMemcpyDeviceToHost, st));
+    if (int rc = xport_group(comm, st, ops)) return done(rc);
+    X_TRY(hipMemcpyAsync(hr.data(), setup + o_hr, 16 * (size_t)S, hipMemcpyDeviceToHost, st));
     X_TRY(hipStreamSynchronize(st));
     if (err) return done(err);
-    for (int s = 0; s < S; ++s)
-      if (rc[(size_t)s * (P + 1) + P])
+    for (int s = 0; s < S; ++s) {
+      if (hr[2 * (size_t)s + 1])
         return done(fail(PSG_ERR_ARG, "exchange set-up failed on rank %d", s));
-    x->recv_cnt.assign((size_t)S * P, 0);
-    for (int s = 0; s < S; ++s)
-      for (int p = 0; p < P; ++p) x->recv_cnt[(size_t)s * P + p] = rc[(size_t)s * (P + 1) + p];
+      if (hr[2 * (size_t)s] != (uint64_t)P)
+        return done(fail(PSG_ERR_ARG, "rank %d has %llu pushes, this rank %d (every rank passes "
+                         "the same npush)", s, (unsigned long long)hr[2 * (size_t)s], P));
+    }
+    // counts to their shards: P words to and from every peer
+    std::vector<uint64_t> rc((size_t)P * S);
+    if (P) {
+      X_TRY(hipMemcpyAsync(setup + o_sc, x->send_cnt.data(), 8 * (size_t)P * S,
+                           hipMemcpyHostToDevice, st));
+      ops.clear();
+      for (int s = 0; s < S; ++s) {
+        ops.push_back(XOp{true, s, setup + o_sc + 8 * (size_t)s * P, 8 * (size_t)P});
+        ops.push_back(XOp{false, s, setup + o_rc + 8 * (size_t)s * P, 8 * (size_t)P});
+      }
+      if (int r = xport_group(comm, st, ops)) return done(r);
+      X_TRY(hipMemcpyAsync(rc.data(), setup + o_rc, 8 * rc.size(), hipMemcpyDeviceToHost, st));
+      X_TRY(hipStreamSynchronize(st));
+    }
+    x->recv_cnt = rc;
   }
   x->recv_tot.assign(S, 0);
   x->recv_off.assign(S, 0);
@@ -447,27 +677,23 @@ int psg_exchange_run(psg_exchange* x, void* stream) {
     HIP_TRY(hipGetLastError());
   }
   if (!x->comm) return PSG_OK;  // local shards: the packed buffers are the result
-  ncclResult_t r = ncclGroupStart();
-  for (int s = 0; r == ncclSuccess && s < x->S; ++s) {
+  std::vector<XOp> ops;
+  for (int s = 0; s < x->S; ++s) {
     if (s == x->comm->rank) continue;  // own pieces were packed into the receive buffers
     if (x->send_tot[s]) {
-      r = ncclSend(x->skeys + x->send_off[s], x->send_tot[s], ncclUint64, s, x->comm->nccl, st);
-      for (int a = 0; r == ncclSuccess && a < x->m; ++a)
-        r = ncclSend((char*)x->svals[a] + x->send_off[s] * vb, x->send_tot[s] * vb, ncclUint8, s,
-                     x->comm->nccl, st);
+      ops.push_back(XOp{true, s, x->skeys + x->send_off[s], 8 * x->send_tot[s]});
+      for (int a = 0; a < x->m; ++a)
+        ops.push_back(XOp{true, s, (char*)x->svals[a] + x->send_off[s] * vb,
+                          (size_t)vb * x->send_tot[s]});
     }
-    if (r == ncclSuccess && x->recv_tot[s]) {
-      r = ncclRecv(x->rkeys + x->recv_off[s], x->recv_tot[s], ncclUint64, s, x->comm->nccl, st);
-      for (int a = 0; r == ncclSuccess && a < x->m; ++a)
-        r = ncclRecv((char*)x->rvals[a] + x->recv_off[s] * vb, x->recv_tot[s] * vb, ncclUint8, s,
-                     x->comm->nccl, st);
+    if (x->recv_tot[s]) {
+      ops.push_back(XOp{false, s, x->rkeys + x->recv_off[s], 8 * x->recv_tot[s]});
+      for (int a = 0; a < x->m; ++a)
+        ops.push_back(XOp{false, s, (char*)x->rvals[a] + x->recv_off[s] * vb,
+                          (size_t)vb * x->recv_tot[s]});
     }
   }
-  const ncclResult_t r2 = ncclGroupEnd();
-  if (r != ncclSuccess || r2 != ncclSuccess)
-    return fail(PSG_ERR_DEVICE, "payload exchange: %s",
-                ncclGetErrorString(r != ncclSuccess ? r : r2));
-  return PSG_OK;
+  return xport_group(x->comm, st, ops);
 }
 
 int psg_exchange_status(psg_exchange* x, uint64_t* changed) {

@@ -172,11 +172,12 @@ hipError_t launch_popcount(const uint32_t* a, uint64_t nw, unsigned long long* o
                            hipStream_t stream);
 
 // FreqencyFilter / CountMin<uint64, uint8> (psg_countmin.hip); the table is
-// n uint32 counters read through their low byte
+// n byte counters (allocated to a multiple of 4 bytes: dword CAS)
+inline size_t cm_table_bytes(uint32_t n) { return ((size_t)n + 3) & ~(size_t)3; }
 hipError_t launch_cm_insert(const uint64_t* keys, const uint32_t* counts, uint64_t nk,
-                            uint32_t* table, uint32_t n, int k, hipStream_t stream);
+                            uint8_t* table, uint32_t n, int k, hipStream_t stream);
 size_t cm_query_scratch_bytes(uint64_t nk);
-hipError_t launch_cm_query(const uint64_t* keys, uint64_t nk, const uint32_t* table, uint32_t n,
+hipError_t launch_cm_query(const uint64_t* keys, uint64_t nk, const uint8_t* table, uint32_t n,
                            int k, int freq, uint64_t* out, unsigned long long* nout,
                            void* scratch, hipStream_t stream);
 

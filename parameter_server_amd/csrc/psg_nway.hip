@@ -625,8 +625,9 @@ int psg_nway_create(int device, int dtype, int m, unsigned flags, int npush,
   u->ntot = ntot;
   u->layout.plan(K, pn.data(), m);
   if (hipMalloc(&u->blob, u->layout.bytes) != hipSuccess) {
+    const size_t want = u->layout.bytes;
     delete u;
-    return fail(PSG_ERR_OOM, "nway: %zu bytes", u->layout.bytes);
+    return fail(PSG_ERR_OOM, "nway: %zu bytes", want);
   }
   const hipError_t e = u->layout.upload((char*)u->blob, pk.data(), pv.data(), pn.data(),
                                         (const void* const*)out_vals, m, nullptr, true);

@@ -628,7 +628,7 @@ bool host_pinned(const void* p, const void** dev = nullptr) {
 
 // FreqencyFilter<uint64> of one channel (CountMin n_, k_, table)
 struct Filter {
-  uint32_t* d_table = nullptr;
+  uint8_t* d_table = nullptr;  // n byte counters (countmin.h:69)
   uint32_t n = 0;
   int k = 1;
   // the caller's stream of the last psg_freq_*_dev call: the table is not
@@ -688,13 +688,60 @@ struct psg_ctx {
 #define PSG_SLAB_BLOCK (size_t(16) << 20)  // A/B builds: 0 = no slabs
 #endif
   static constexpr size_t kSlab = size_t(256) << 20, kSlabBlock = PSG_SLAB_BLOCK;
-  std::vector<std::pair<char*, size_t>> slabs;
+  // carved: bytes handed out by the bump pointer; back: bytes of those
+  // returned (in the pool, or dropped after a failed event).  A slab with
+  // back == carved holds no live block and can be freed whole (reclaim_slabs:
+  // when an allocation fails, or when idle carved bytes pass kPoolCap), so
+  // blocks stranded by drifting sizes do not hold HBM for the context's life
+  struct Slab {
+    char* p;
+    size_t size, carved, back;
+  };
+  std::vector<Slab> slabs;
   char* slab_cur = nullptr;
   size_t slab_left = 0;
-  bool in_slab(const void* p) const {
-    for (const auto& s : slabs)
-      if ((const char*)p >= s.first && (const char*)p < s.first + s.second) return true;
-    return false;
+  size_t slab_idle = 0;  // sum of back over the slabs
+  int slab_of(const void* p) const {
+    for (size_t i = 0; i < slabs.size(); ++i)
+      if ((const char*)p >= slabs[i].p && (const char*)p < slabs[i].p + slabs[i].size)
+        return (int)i;
+    return -1;
+  }
+  bool in_slab(const void* p) const { return slab_of(p) >= 0; }
+  // frees every slab none of whose blocks is live; returns the bytes freed
+  size_t reclaim_slabs() {
+    bool any = false;
+    for (const Slab& s : slabs) any |= s.carved && s.back == s.carved;
+    if (!any) return 0;
+    // pooled blocks carry events on `stream`: once it is idle none is read
+    (void)hipStreamSynchronize(stream);
+    (void)hipStreamSynchronize(copy);
+    size_t freed = 0;
+    for (size_t i = 0; i < slabs.size();) {
+      Slab& s = slabs[i];
+      if (!(s.carved && s.back == s.carved)) {
+        ++i;
+        continue;
+      }
+      for (auto it = pool.begin(); it != pool.end();) {
+        const char* q = (const char*)it->second.p;
+        if (q >= s.p && q < s.p + s.size) {
+          free_ev.push_back(it->second.ev);
+          it = pool.erase(it);
+        } else {
+          ++it;
+        }
+      }
+      if (slab_cur >= s.p && slab_cur <= s.p + s.size) {
+        slab_cur = nullptr;
+        slab_left = 0;
+      }
+      slab_idle -= s.back;
+      freed += s.size;
+      (void)hipFree(s.p);
+      slabs.erase(slabs.begin() + (ptrdiff_t)i);
+    }
+    return freed;
   }
 
   int event(hipEvent_t* e) {
@@ -714,29 +761,46 @@ struct psg_ctx {
       *p = it->second.p;
       if (writer != stream) HIP_TRY(hipStreamWaitEvent(writer, it->second.ev, 0));
       free_ev.push_back(it->second.ev);
-      if (!in_slab(*p)) pool_bytes -= it->first;
+      const int si = slab_of(*p);
+      if (si < 0) {
+        pool_bytes -= it->first;
+      } else {
+        slabs[si].back -= it->first;
+        slab_idle -= it->first;
+      }
       pool.erase(it);
       return PSG_OK;
     }
     if (b <= kSlabBlock) {
       if (slab_left < b) {
         char* sp = nullptr;
-        if (hipMalloc((void**)&sp, kSlab) == hipSuccess) {
-          slabs.emplace_back(sp, kSlab);
+        if (hipMalloc((void**)&sp, kSlab) != hipSuccess) {
+          (void)hipGetLastError();
+          if (reclaim_slabs() && hipMalloc((void**)&sp, kSlab) != hipSuccess) {
+            (void)hipGetLastError();
+            sp = nullptr;
+          }
+        }
+        if (sp) {
+          slabs.push_back(Slab{sp, kSlab, 0, 0});
           slab_cur = sp;
           slab_left = kSlab;
-        } else {
-          (void)hipGetLastError();  // no room for a slab: an allocation of its own
-        }
+        }  // else no room for a slab: an allocation of its own
       }
       if (slab_left >= b) {
         *p = slab_cur;
         slab_cur += b;
         slab_left -= b;
+        slabs[(size_t)slab_of(*p)].carved += b;
         return PSG_OK;
       }
     }
-    HIP_TRY(hipMalloc(p, b));
+    if (hipMalloc(p, b) != hipSuccess) {
+      (void)hipGetLastError();
+      // idle slabs (blocks stranded by sizes that drifted) go back first
+      if (!reclaim_slabs()) return fail(PSG_ERR_OOM, "device allocation of %zu bytes", b);
+      HIP_TRY(hipMalloc(p, b));
+    }
     return PSG_OK;
   }
   void dev_put(void* p, size_t b) {
@@ -745,17 +809,24 @@ struct psg_ctx {
     // the block's release event on `stream`
     if (zc.n) (void)join_copy();
     b = align_up(b ? b : 1, 4096);
-    const bool carved = in_slab(p);  // always pooled: its slab stays allocated anyway
+    const int si = slab_of(p);  // a carved block is pooled (or counted back) always
+    const bool carved = si >= 0;
+    if (carved) {
+      slabs[si].back += b;
+      slab_idle += b;
+    }
     hipEvent_t e = nullptr;
     if ((!carved && pool_bytes + b > kPoolCap) || event(&e) != PSG_OK ||
         hipEventRecord(e, stream) != hipSuccess) {
       if (e) free_ev.push_back(e);
       (void)hipStreamSynchronize(stream);
-      if (!carved) (void)hipFree(p);  // a carved block is lost until the slab goes
+      if (!carved) (void)hipFree(p);  // a carved block goes with its slab
       return;
     }
     pool.emplace(b, Pooled{p, e});
     if (!carved) pool_bytes += b;
+    // idle carved bytes are bounded like the pool: whole idle slabs go back
+    if (carved && slab_idle > kPoolCap) (void)reclaim_slabs();
   }
   void pool_release() {
     for (auto& kv : pool) {
@@ -764,10 +835,11 @@ struct psg_ctx {
     }
     pool.clear();
     pool_bytes = 0;
-    for (auto& sl : slabs) (void)hipFree(sl.first);
+    for (auto& sl : slabs) (void)hipFree(sl.p);
     slabs.clear();
     slab_cur = nullptr;
     slab_left = 0;
+    slab_idle = 0;
     for (hipEvent_t e : free_ev) (void)hipEventDestroy(e);
     free_ev.clear();
   }
@@ -1167,6 +1239,9 @@ int psg_key_union_dev(const uint64_t* a, uint64_t na, const uint64_t* b,
   if (e == hipSuccess) e = hipStreamSynchronize(s);
   (void)hipFree(scratch);
   if (e != hipSuccess) return fail(PSG_ERR_DEVICE, "key union: %s", hipGetErrorString(e));
+  // high bits: tile overflow (1 << 32) / look-back timeout (1 << 40) of the
+  // N-way kernels, a device fault and not an order violation
+  if (h[0] >> 32) return fail(PSG_ERR_DEVICE, "key union: device fault (%llx)", h[0]);
   if (h[0]) return fail(PSG_ERR_UNSORTED, "%llu order violations", h[0]);
   *nout = h[1];
   return PSG_OK;
@@ -1275,7 +1350,7 @@ int psg_destroy(psg_ctx* c) {
   c->ch.clear();
   for (auto& kv : c->ff) {
     kv.second.sync_ext();
-    c->dev_put(kv.second.d_table, 4 * (size_t)kv.second.n);
+    c->dev_put(kv.second.d_table, psg::cm_table_bytes(kv.second.n));
   }
   c->ff.clear();
   if (c->stream) (void)hipStreamSynchronize(c->stream);
@@ -1351,6 +1426,17 @@ int key_union_impl(psg_ctx* c, int chl, const std::vector<const uint64_t*>& d_pu
       if (int rc = c->flush(kv.second)) return rc;
   if (int rc = c->join_copy()) return rc;
   bool changed = false;
+  // once a merge applied, the key set (so every position) changed: the
+  // mirror is refreshed and val_[chl] cleared (kv_vector.h:180) on every
+  // way out, an error in a later chunk of pushes included
+  auto settle = [&](int rc) -> int {
+    if (!changed) return rc;
+    const int mr = refresh_mirror(c, C);
+    c->dev_put(C.d_vals, C.nvals * vsize(c->dtype));
+    C.d_vals = nullptr;
+    C.nvals = 0;
+    return rc != PSG_OK ? rc : mr;
+  };
   for (size_t i = 0; i < d_push.size();) {
     std::vector<const uint64_t*> pk;
     std::vector<uint64_t> pn;
@@ -1367,12 +1453,12 @@ int key_union_impl(psg_ctx* c, int chl, const std::vector<const uint64_t*>& d_pu
     if (pk.size() == base) continue;  // only empty pushes: ignored (kv_vector.h:177)
     uint64_t cap = 0;
     for (uint64_t x : pn) cap += x;
-    if (cap >= (1ull << 32)) return fail(PSG_ERR_ARG, "key union of %llu keys >= 2^32",
-                                         (unsigned long long)cap);
+    if (cap >= (1ull << 32))
+      return settle(fail(PSG_ERR_ARG, "key union of %llu keys >= 2^32", (unsigned long long)cap));
     const uint32_t K = (uint32_t)pk.size();
-    if (int rc = c->ensure_scratch(psg::nway_scratch_bytes(K, pn.data()))) return rc;
+    if (int rc = c->ensure_scratch(psg::nway_scratch_bytes(K, pn.data()))) return settle(rc);
     uint64_t* d_out = nullptr;
-    if (int rc = c->dev_get(8 * cap, (void**)&d_out, c->stream)) return rc;
+    if (int rc = c->dev_get(8 * cap, (void**)&d_out, c->stream)) return settle(rc);
     unsigned long long* d_bad = nullptr;
     hipError_t e = psg::nway_union_enqueue(K, pk.data(), pn.data(), d_out, c->scratch, &d_bad,
                                            c->stream);
@@ -1381,14 +1467,13 @@ int key_union_impl(psg_ctx* c, int chl, const std::vector<const uint64_t*>& d_pu
     if (e == hipSuccess) e = hipStreamSynchronize(c->stream);
     if (e != hipSuccess) {
       c->dev_put(d_out, 8 * cap);
-      return fail(PSG_ERR_DEVICE, "key union: %s", hipGetErrorString(e));
+      return settle(fail(PSG_ERR_DEVICE, "key union: %s", hipGetErrorString(e)));
     }
     const unsigned long long bad = c->h_small[0], nu = c->h_small[1];
     if (bad) {  // the pushes of this merge are not applied; earlier ones are
       c->dev_put(d_out, 8 * cap);
-      if (changed) (void)refresh_mirror(c, C);
-      return fail(bad >> 32 ? PSG_ERR_DEVICE : PSG_ERR_UNSORTED,
-                  "key-only push: %llu order violations", bad);
+      return settle(fail(bad >> 32 ? PSG_ERR_DEVICE : PSG_ERR_UNSORTED,
+                         "key-only push: %llu order violations", bad));
     }
     c->dev_put(C.d_keys, C.kbytes);
     C.d_keys = d_out;
@@ -1396,13 +1481,7 @@ int key_union_impl(psg_ctx* c, int chl, const std::vector<const uint64_t*>& d_pu
     C.n = (size_t)nu;
     changed = true;
   }
-  if (!changed) return PSG_OK;
-  if (int rc = refresh_mirror(c, C)) return rc;
-  // val_[chl].clear()  (kv_vector.h:180)
-  c->dev_put(C.d_vals, C.nvals * vsize(c->dtype));
-  C.d_vals = nullptr;
-  C.nvals = 0;
-  return PSG_OK;
+  return settle(PSG_OK);
 }
 
 // findRange of a push and the consistency checks of setValue, before any
@@ -2053,14 +2132,14 @@ int psg_freq_resize(psg_ctx* c, int chl, int n, int k) {
   const uint32_t nn = (uint32_t)std::max(n, 64);  // countmin.h:15
   F.sync_ext();
   if (nn != F.n) {
-    c->dev_put(F.d_table, 4 * (size_t)F.n);
+    c->dev_put(F.d_table, psg::cm_table_bytes(F.n));
     F.d_table = nullptr;
     F.n = 0;
-    if (int rc = c->dev_get(4 * (size_t)nn, (void**)&F.d_table, c->stream)) return rc;
+    if (int rc = c->dev_get(psg::cm_table_bytes(nn), (void**)&F.d_table, c->stream)) return rc;
     F.n = nn;
   }
   F.k = std::min(30, std::max(1, k));  // countmin.h:18
-  HIP_TRY(hipMemsetAsync(F.d_table, 0, 4 * (size_t)F.n, c->stream));
+  HIP_TRY(hipMemsetAsync(F.d_table, 0, psg::cm_table_bytes(F.n), c->stream));
   return PSG_OK;
 }
 
@@ -2070,7 +2149,7 @@ int psg_freq_clear(psg_ctx* c, int chl) {
   auto it = c->ff.find(chl);
   if (it != c->ff.end()) {
     it->second.sync_ext();
-    c->dev_put(it->second.d_table, 4 * (size_t)it->second.n);
+    c->dev_put(it->second.d_table, psg::cm_table_bytes(it->second.n));
     c->ff.erase(it);
   }
   return PSG_OK;
@@ -2181,10 +2260,8 @@ int psg_freq_table(psg_ctx* c, int chl, uint8_t* out, size_t n) {
   if (int rc = filter_of(c, chl, &F)) return rc;
   if (n > F->n) return fail(PSG_ERR_ARG, "table copy of %zu > %u counters", n, F->n);
   if (int rc = set_dev(c->device)) return rc;
-  std::vector<uint32_t> t(n);
-  HIP_TRY(hipMemcpyAsync(t.data(), F->d_table, 4 * n, hipMemcpyDeviceToHost, c->stream));
+  if (n) HIP_TRY(hipMemcpyAsync(out, F->d_table, n, hipMemcpyDeviceToHost, c->stream));
   HIP_TRY(hipStreamSynchronize(c->stream));
-  for (size_t i = 0; i < n; ++i) out[i] = (uint8_t)t[i];
   return PSG_OK;
 }
 

@@ -161,6 +161,12 @@ __global__ __launch_bounds__(nt_of(kGroup), (occupancy<V, M, kGroup>())) void ti
   __shared__ int lastpos[kNW];
   __shared__ int pcarry;
   __shared__ uint32_t wsum[kNW];
+#ifdef PSG_PAD_LDS
+  // diagnostic A/B builds only: extra LDS per workgroup to lower the
+  // workgroups per CU at unchanged code (occupancy sensitivity)
+  __shared__ uint32_t ldspad[PSG_PAD_LDS / 4];
+  if (threadIdx.x == 0) ldspad[blockIdx.x % (PSG_PAD_LDS / 4)] = 0u;
+#endif
 
   const uint32_t w = uni((uint32_t)threadIdx.x >> 6);
   const int tid = threadIdx.x;

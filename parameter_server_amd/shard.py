@@ -229,6 +229,19 @@ def destroy_comm(h) -> None:
     _lib.lib().psg_comm_destroy(h)
 
 
+def loopback_comms(device: int, world: int):
+    """`world` psg_comm ranks living in this process on one device
+    (psg_comm_init_loopback): the exchange's collective rounds with RCCL's
+    pairing rule, each matched send/recv a device copy.  Drive each rank
+    from its own thread (ctypes releases the GIL), all ranks concurrently,
+    as RCCL ranks run in their own processes."""
+    import ctypes as C
+    from . import _lib
+    hs = (C.c_void_p * world)()
+    _lib.check(_lib.lib().psg_comm_init_loopback(device, world, hs))
+    return [C.c_void_p(hs[r]) for r in range(world)]
+
+
 class RcclExchange:
     """Mode B re-homing of this rank's device-resident pushes through
     psg_exchange_* (one grouped RCCL send/recv per peer per step).

@@ -181,3 +181,145 @@ def test_local_exchange_detects_changed_keys():
     with pytest.raises(PSGError):
         x.status()
     x.close()
+
+
+def _threads(fns):
+    """Run fns[r]() for every rank r on its own thread (loopback ranks must
+    enter the collective rounds concurrently); returns (results, errors)."""
+    import threading
+    res, err = [None] * len(fns), [None] * len(fns)
+
+    def body(r):
+        try:
+            res[r] = fns[r]()
+        except BaseException as e:  # noqa: BLE001 - reported per rank
+            err[r] = e
+
+    ts = [threading.Thread(target=body, args=(r,)) for r in range(len(fns))]
+    for t in ts:
+        t.start()
+    for t in ts:
+        t.join(timeout=300)
+        assert not t.is_alive(), "a loopback rank hung"
+    return res, err
+
+
+@pytest.mark.parametrize("dtype,m", [(np.float32, 1), (np.float64, 2)])
+def test_loopback_8_ranks_exchange_then_hip_merge(dtype, m):
+    """The multi-rank exchange at S = 8 ranks (psg_comm_init_loopback: 8
+    ranks of one process on one GPU, one host thread each), cfg5-shaped
+    pushes (murmur-shuffled uniform ranks, 8 whole pushes per rank): the
+    collective count round, the receive offsets and the pairing of sends and
+    receives across peers run exactly as over RCCL.  Per rank, recv counts
+    equal the oracle's sliceKeyOrderedMsg cut (message.h:89-123) at
+    evenDivide(8) of every source's pushes, the received keys/values are
+    those pieces in (source, push) order, and the HIP plan's merge of them
+    equals the oracle's aggregate over the rank's key range, bit for bit.
+    Two runs land in the same buffers."""
+    import torch
+    from parameter_server_amd import shard, synth
+    from parameter_server_amd._lib import PSG_F32, PSG_F64
+    from parameter_server_amd.kv_vector import MergePlan, shard_bounds
+    S, PR = 8, 8
+    _, pushes = synth.uniform_pushes(seed=51, npush=S * PR, n=12000, dtype=dtype, m=m,
+                                     union=False)
+    b = shard_bounds(S)
+    # a push holding the shard edges, one confined to shard 6, an empty one
+    pushes[3] = (np.array([b[1] - 1, b[1], b[2], b[7] - 1, b[7]], np.uint64),
+                 [np.arange(5, dtype=dtype) - 2 for _ in range(m)])
+    pushes[20] = (np.arange(b[6] + 5, b[6] + 2005, dtype=np.uint64),
+                  [np.full(2000, 0.25, dtype) for _ in range(m)])
+    pushes[41] = (np.zeros(0, np.uint64), [np.zeros(0, dtype) for _ in range(m)])
+    dev = torch.device("cuda", 0)
+    comms = shard.loopback_comms(0, S)
+    held = [_dev_pushes(pushes[r * PR:(r + 1) * PR], dev) for r in range(S)]
+    vt = PSG_F32 if dtype == np.float32 else PSG_F64
+    xs, err = _threads([lambda r=r: shard.RcclExchange(comms[r], held[r], S, vt)
+                        for r in range(S)])
+    assert not any(err), err
+    streams = [torch.cuda.Stream(device=dev) for _ in range(S)]
+    for _ in range(2):
+        _, err = _threads([lambda r=r: xs[r].run(streams[r].cuda_stream) for r in range(S)])
+        assert not any(err), err
+    torch.cuda.synchronize()
+    sv = np.dtype(dtype).itemsize
+    ALL = (0, (1 << 64) - 1)
+    cut = [O.slice_key_ordered(k, *ALL, b)[0].astype(np.int64) for k, _ in pushes]
+    D = np.unique(np.concatenate([k for k, _ in pushes]))
+    for r in range(S):
+        x = xs[r]
+        assert x.status() == 0
+        want_cnt = np.array([[cut[src * PR + p][r + 1] - cut[src * PR + p][r] for p in range(PR)]
+                             for src in range(S)], np.int64)
+        assert np.array_equal(x.recv_cnt, want_cnt), f"rank {r} recv counts"
+        assert x.nsent == sum(int(cut[r * PR + p][s + 1] - cut[r * PR + p][s])
+                              for p in range(PR) for s in range(S) if s != r)
+        rk = d2h(x.recv_keys_ptr, 8 * x.nrecv).view(np.uint64)
+        rv = [d2h(p, sv * x.nrecv).view(dtype) for p in x.recv_vals_ptr]
+        pieces = []
+        for src in range(S):
+            for p in range(PR):
+                k, vs = pushes[src * PR + p]
+                a, e = int(cut[src * PR + p][r]), int(cut[src * PR + p][r + 1])
+                o = int(x.recv_off[src, p])
+                assert np.array_equal(rk[o:o + e - a], k[a:e]), f"rank {r} keys of {src},{p}"
+                for i in range(m):
+                    assert rv[i][o:o + e - a].tobytes() == vs[i][a:e].tobytes()
+                if e > a:
+                    pieces.append((k[a:e], [v[a:e] for v in vs]))
+        # the rank's merge of what it received (arrival order: source, push)
+        lo, hi = O.find_range(D, int(b[r]), int(b[r + 1]))
+        dD = torch.from_numpy(D[lo:hi].view(np.int64)).to(dev)
+        o = [torch.empty(max(1, hi - lo), dtype=torch.float32 if dtype == np.float32
+                         else torch.float64, device=dev) for _ in range(m)]
+        pcs = x.pieces()
+        plan = MergePlan(0, vt, m, [{
+            "keys": dD.data_ptr(), "nslots": hi - lo,
+            "push_keys": [x.recv_keys_ptr + 8 * a for a, _ in pcs],
+            "push_vals": [[x.recv_vals_ptr[i] + sv * a for i in range(m)] for a, _ in pcs],
+            "push_n": [c for _, c in pcs], "out": [t.data_ptr() for t in o]}])
+        plan.run()
+        torch.cuda.synchronize()
+        assert list(plan.matched()) == [c for _, c in pcs]
+        rc, _, _, want, _ = O.aggregate(D, int(b[r]), int(b[r + 1]), pieces, dtype=dtype)
+        assert rc == 0
+        for i in range(m):
+            assert o[i].cpu().numpy()[:hi - lo].tobytes() == np.asarray(want[i], dtype).tobytes()
+        plan.close()
+    for x in xs:
+        x.close()
+    for c in comms:
+        shard.destroy_comm(c)
+
+
+def test_loopback_bad_rank_fails_everywhere_without_hang():
+    """One rank of 8 passes a bad dtype to psg_exchange_create: it still
+    takes part in the collective count round (with an error word), so every
+    rank returns an error instead of waiting on it; the communicators are
+    usable afterwards (a good exchange on the same ranks succeeds)."""
+    import time
+    import torch
+    from parameter_server_amd import shard, synth
+    from parameter_server_amd._lib import PSG_F32, PSGError
+    S = 8
+    _, pushes = synth.uniform_pushes(seed=53, npush=S, n=3000, union=False)
+    dev = torch.device("cuda", 0)
+    comms = shard.loopback_comms(0, S)
+    held = [_dev_pushes(pushes[r:r + 1], dev) for r in range(S)]
+    t0 = time.time()
+    _, err = _threads([lambda r=r: shard.RcclExchange(comms[r], held[r], S,
+                                                      99 if r == 3 else PSG_F32)
+                       for r in range(S)])
+    assert time.time() - t0 < 60
+    assert all(isinstance(e, PSGError) for e in err), err
+    xs, err = _threads([lambda r=r: shard.RcclExchange(comms[r], held[r], S, PSG_F32)
+                        for r in range(S)])
+    assert not any(err), err
+    _, err = _threads([lambda r=r: xs[r].run(None) for r in range(S)])
+    assert not any(err), err
+    torch.cuda.synchronize()
+    assert sum(x.nrecv for x in xs) == sum(k.size for k, _ in pushes)
+    for x in xs:
+        x.close()
+    for c in comms:
+        shard.destroy_comm(c)

@@ -183,3 +183,42 @@ def test_context_key_union_on_device():
     assert np.array_equal(v2.key(0), want2)
     v1.close()
     v2.close()
+
+
+def test_key_union_batch_fails_in_later_chunk():
+    """A batched key union of more pushes than one N-way merge takes
+    (psg_nway_max_push() - 1 besides the resident keys) whose bad push sits
+    in the second chunk: the first chunk is applied, the error is
+    PSG_ERR_UNSORTED, and since the key set changed the value array is
+    cleared (kv_vector.h:180) -- no stale values stay attached to a new key
+    set, even when the first chunk added no new key."""
+    from parameter_server_amd._lib import PSGError, PSG_ERR_UNSORTED, lib
+    from parameter_server_amd.kv_vector import KVVector, Message
+    rng = np.random.default_rng(11)
+    D = np.unique(rng.integers(0, 1 << 62, 50000, dtype=np.uint64))
+    nmax = lib().psg_nway_max_push()
+    npush = nmax + 6
+    # every push a subset of D: the first chunk adds no new key
+    pushes = [np.sort(rng.choice(D, 3000, replace=False)) for _ in range(npush)]
+    bad_at = nmax + 2  # in the second chunk
+    bad = pushes[bad_at].copy()
+    bad[5], bad[6] = bad[6], bad[5]
+    pushes[bad_at] = bad
+    v = KVVector(0)
+    v.setValue(Message(key=D))
+    v.set_value_array(0, rng.standard_normal(D.size).astype(np.float32))
+    assert v.value(0).size == D.size
+    with pytest.raises(PSGError) as e:
+        v.union_keys(0, pushes)
+    assert e.value.status == PSG_ERR_UNSORTED
+    assert np.array_equal(v.key(0), D)
+    assert v.value(0).size == 0, "stale values survived a partially applied key union"
+    # and with new keys in the first chunk: they are applied
+    extra = np.unique(rng.integers(1 << 62, 1 << 63, 1000, dtype=np.uint64))
+    pushes[0] = extra
+    v.set_value_array(0, np.zeros(D.size, np.float32))
+    with pytest.raises(PSGError):
+        v.union_keys(0, pushes)
+    assert np.array_equal(v.key(0), O.set_union(D, extra))
+    assert v.value(0).size == 0
+    v.close()

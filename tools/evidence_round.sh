@@ -1,13 +1,12 @@
-# r03 final evidence (after the parallel collision test): GPU tests, smoke, profile_round, side lines, row counters
-# PMC cfg2 + cfg5, default bench line), cfg3/cfg4 side lines, f64 cfg2 side line, row counters
+# A round's final evidence: GPU tests, smoke, profile_round, side lines, row counters.  usage: tools/evidence_round.sh r04
 set -o pipefail
 export TMPDIR=/tmp
-O=gpurun_out/r03ah; mkdir -p $O
+R=${1:-r04}; O=gpurun_out/$R; mkdir -p $O
 timeout -k 10 600 python3 -u -m pytest tests -m gpu -x -q --timeout 180 --timeout-method thread > $O/gputest.log 2>&1 || { echo TESTFAIL; tail -30 $O/gputest.log; exit 1; }
 tail -1 $O/gputest.log
 timeout -k 10 300 python3 -c "import __graft_entry__ as g; g.smoke()" > $O/smoke.log 2>&1 || { echo SMOKEFAIL; tail -20 $O/smoke.log; exit 1; }
 tail -1 $O/smoke.log
-bash tools/profile_round.sh r03ah > $O/profile_round.log 2>&1 || { echo PROFFAIL; tail -20 $O/profile_round.log; exit 1; }
+bash tools/profile_round.sh $R > $O/profile_round.log 2>&1 || { echo PROFFAIL; tail -20 $O/profile_round.log; exit 1; }
 NOTEST=1 WLS="cfg3 cfg4" bash tools/quick_bench.sh $O/side || exit 1
 timeout -k 10 300 python3 bench.py --no-cpu-baseline --no-cfg5 --dtype f64 > $O/side/cfg2_f64.json 2> $O/side/cfg2_f64.err || { echo "f64 failed"; exit 1; }
 python3 -c "import json;d=json.load(open('$O/side/cfg2_f64.json'));r=d['roofline'];print('cfg2 f64 %.3e kern %.4f part %.4f frac %.3f step_frac %.3f'%(d['value'],r['kernel_ms'],r['partition_ms'],r['frac'],r['step_frac']))"
