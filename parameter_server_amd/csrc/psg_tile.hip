@@ -45,7 +45,7 @@
 
 #define AS1 __attribute__((address_space(1)))
 #ifndef KCAP64
-#define KCAP64 8
+#define KCAP64 7
 #endif
 
 namespace psg {
@@ -122,8 +122,8 @@ __device__ __forceinline__ uint32_t wave_scan_incl(uint32_t x) {
 template <typename V, int M, int kGroup>
 constexpr int occupancy() {
   constexpr int ts = ts_of(kGroup), nw = nt_of(kGroup) / 64;
-  constexpr int lds = (ts + 8) * 8 + (nb_of(kGroup) + 8) * 2 + M * (int)sizeof(V) * ts + ts * 2 +
-                      (kGroup + 1) * 4 + kGroup * (ts / 64) * 2 + kGroup * 12 + kGroup * M * 8 +
+  constexpr int lds = (ts + 4) * 8 + (nb_of(kGroup) + 8) * 2 + M * (int)sizeof(V) * ts +
+                      ts * (kGroup == 32 ? 4 : 2) + (kGroup + 1) * 4 + kGroup * 12 + kGroup * M * 8 +
                       nw * 8 + 8;
   // waves per SIMD (the launch bound's unit): workgroups per CU x waves / 4
   constexpr int w = (163840 / lds) * nw / 4;
@@ -144,7 +144,7 @@ __global__ __launch_bounds__(nt_of(kGroup), (occupancy<V, M, kGroup>())) void ti
   // 64-push form runs 7 per CU and affords 8 (4 waves x 8 = 32 rounds: a
   // group of 64 one-round pieces in 2 passes)
   constexpr int kCap = kGroup == 64 ? KCAP64 : 6;
-  __shared__ __attribute__((aligned(16))) uint64_t dk[kTS + 8];
+  __shared__ __attribute__((aligned(16))) uint64_t dk[kTS + 4];  // + sentinels ~0: the search window reads up to slot nt + 3
   // bucket starts (u16); the histogram counts in it as packed pairs by 32-bit atomics
   __shared__ __attribute__((aligned(16))) uint32_t bt32[(kNB + 8) / 2];
   uint16_t* const bt = (uint16_t*)bt32;
@@ -153,20 +153,16 @@ __global__ __launch_bounds__(nt_of(kGroup), (occupancy<V, M, kGroup>())) void ti
   // LDS adds during the search, off the fold's dependency chain): the fold
   // adds the "+0.0" of absent pushes as ONE trailing +0.0 when the count is
   // below np (see the stores)
-  __shared__ __attribute__((aligned(16))) uint32_t cnt32[kTS / 2];
+  // 1024-slot form: one u32 per slot (the add is a constant 1); the
+  // 2048-slot form keeps u16 pairs (LDS: 4 workgroups per CU)
+  constexpr bool kCntW = kGroup == 32;
+  __shared__ __attribute__((aligned(16))) uint32_t cnt32[kCntW ? kTS : kTS / 2];
   __shared__ uint32_t rpre[kGroup + 1];             // rounds before push q of the group
-  __shared__ uint16_t rtab[kGroup * (kTS / 64)];    // round -> q << kCB | chunk
   __shared__ uint32_t pln[kGroup];                  // piece length
   __shared__ uint64_t pkp[kGroup], pvp[kGroup * M];  // piece starts (keys, values)
   __shared__ int lastpos[kNW];
   __shared__ int pcarry;
   __shared__ uint32_t wsum[kNW];
-#ifdef PSG_PAD_LDS
-  // diagnostic A/B builds only: extra LDS per workgroup to lower the
-  // workgroups per CU at unchanged code (occupancy sensitivity)
-  __shared__ uint32_t ldspad[PSG_PAD_LDS / 4];
-  if (threadIdx.x == 0) ldspad[blockIdx.x % (PSG_PAD_LDS / 4)] = 0u;
-#endif
 
   const uint32_t w = uni((uint32_t)threadIdx.x >> 6);
   const int tid = threadIdx.x;
@@ -223,8 +219,6 @@ __global__ __launch_bounds__(nt_of(kGroup), (occupancy<V, M, kGroup>())) void ti
       const uint32_t x = wave_scan_incl(nr);
       if (lane < kGroup) rpre[lane + 1] = x;
       if (lane == 0) rpre[0] = 0;
-#pragma nounroll
-      for (uint32_t c = 0; c < nr; ++c) rtab[x - nr + c] = (uint16_t)((uint32_t)lane << kCB | c);
     }
   };
   if (np) load_tables(0);
@@ -266,7 +260,11 @@ __global__ __launch_bounds__(nt_of(kGroup), (occupancy<V, M, kGroup>())) void ti
   const uint32_t mul = dev::bucket_scale(r32, kNB);
   auto bucket = [&](uint64_t k) -> uint32_t {
     const uint64_t x = (k - klo) >> s2;
-    return x > r32 ? (uint32_t)(kNB - 1) : __umulhi((uint32_t)x, mul);
+    // no branch: an out-of-range x saturates, and the clamp puts it in the
+    // end bucket (umulhi(r32, mul) < kNB for every in-range x)
+    const uint32_t xs = x > r32 ? 0xffffffffu : (uint32_t)x;
+    const uint32_t b = __umulhi(xs, mul);
+    return b < (uint32_t)(kNB - 1) ? b : (uint32_t)(kNB - 1);
   };
 
   // ---- install D, sums, counts; clear the histogram
@@ -276,9 +274,14 @@ __global__ __launch_bounds__(nt_of(kGroup), (occupancy<V, M, kGroup>())) void ti
 #pragma unroll
     for (int mi = 0; mi < M; ++mi) acc[mi][s0 + j] = a0[mi][j];
   }
-  cnt32[2 * tid] = 0u;
-  cnt32[2 * tid + 1] = 0u;
-  if (tid < 8) dk[kTS + tid] = ~0ull;
+  if constexpr (kCntW) {
+    typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
+    *(u32x4*)&cnt32[4 * tid] = u32x4{0u, 0u, 0u, 0u};
+  } else {
+    cnt32[2 * tid] = 0u;
+    cnt32[2 * tid + 1] = 0u;
+  }
+  if (tid < 4) dk[kTS + tid] = ~0ull;
   if (Bg) {  // resident table: installed as loaded
     bt32[tid * (kBPT / 2)] = btw.x;
     bt32[tid * (kBPT / 2) + 1] = btw.y;
@@ -299,8 +302,10 @@ __global__ __launch_bounds__(nt_of(kGroup), (occupancy<V, M, kGroup>())) void ti
   uint32_t re[kCap];  // round: q << kCB | chunk (the same in every lane)
   uint64_t ek[kCap];
   V ev[kCap][M];
-  uint32_t fl = 0;  // per lane: bit r = element of round r exists, bit 8+r = found,
-                    // bit 16+r = found and in order (VGPR bits, not SGPR lane masks)
+  // per lane, bit r of round r (VGPR bit words, not SGPR lane masks; one
+  // word each keeps the shifted bits inline constants): the element exists,
+  // it was found, it was found and in order
+  uint32_t hv = 0, fd = 0, okb = 0;
   auto load_pass = [&]() {
     const uint32_t rem = U - done;
     Rw = (rem + kNW - 1) / kNW;
@@ -308,21 +313,45 @@ __global__ __launch_bounds__(nt_of(kGroup), (occupancy<V, M, kGroup>())) void ti
     ua = done + w * Rw;
     const uint32_t ub = ua + Rw < U ? ua + Rw : U;
     nrw = ub > ua ? ub - ua : 0u;
-    fl = 0;
+    hv = 0;
+    // the group's push table, one push per lane (lane q = push g0 + q), from
+    // LDS in one round trip; a round's push is then a ballot over the lanes'
+    // round ends and its bounds and pointers are lane reads: no dependent
+    // LDS reads per round
+    const uint32_t gp = np - g0 < (uint32_t)kGroup ? np - g0 : (uint32_t)kGroup;
+    uint32_t t_len = 0, t_end = 0xffffffffu;
+    uint64_t t_kp = 0, t_vp[M];
+#pragma unroll
+    for (int mi = 0; mi < M; ++mi) t_vp[mi] = 0;
+    if ((uint32_t)lane < gp) {
+      t_len = pln[lane];
+      t_end = rpre[lane + 1];
+      t_kp = pkp[lane];
+#pragma unroll
+      for (int mi = 0; mi < M; ++mi) t_vp[mi] = pvp[lane * M + mi];
+    }
 #pragma unroll
     for (int r = 0; r < kCap; ++r) {
       re[r] = 0;
       if ((uint32_t)r < nrw) {
-        const uint32_t e = rtab[ua + (uint32_t)r];
-        const uint32_t q = e >> kCB;
-        const uint32_t i = (e & ((1u << kCB) - 1u)) * 64u + (uint32_t)lane;
-        re[r] = e;
-        const bool have = i < pln[q];
-        fl |= (uint32_t)have << r;  // shift of a 0/1: no literal masks held in VGPRs
-        const uint32_t x = have ? i : 0u;
-        ek[r] = G((const uint64_t*)pkp[q])[x];
+        const uint32_t ru = ua + (uint32_t)r;
+        const uint32_t q = (uint32_t)__popcll(__ballot(t_end <= ru));
+        const uint32_t rs = q ? (uint32_t)__builtin_amdgcn_readlane((int)t_end, (int)q - 1) : 0u;
+        const uint32_t c = ru - rs;
+        re[r] = q << kCB | c;
+        const uint32_t len = (uint32_t)__builtin_amdgcn_readlane((int)t_len, (int)q);
+        const bool have = c * 64u + (uint32_t)lane < len;
+        hv |= (uint32_t)have << r;
+        const uint64_t kp = (uint64_t)(uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)t_kp, (int)q) |
+                            (uint64_t)(uint32_t)__builtin_amdgcn_readlane((int)(t_kp >> 32), (int)q) << 32;
+        if (have) ek[r] = G((const uint64_t*)kp + 64u * c)[lane];
 #pragma unroll
-        for (int mi = 0; mi < M; ++mi) ev[r][mi] = G((const V*)pvp[q * M + mi])[x];
+        for (int mi = 0; mi < M; ++mi) {
+          const uint64_t vp =
+              (uint64_t)(uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)t_vp[mi], (int)q) |
+              (uint64_t)(uint32_t)__builtin_amdgcn_readlane((int)(t_vp[mi] >> 32), (int)q) << 32;
+          if (have) ev[r][mi] = G((const V*)vp + 64u * c)[lane];
+        }
       }
     }
   };
@@ -394,7 +423,7 @@ __global__ __launch_bounds__(nt_of(kGroup), (occupancy<V, M, kGroup>())) void ti
       V t = V(0);
 #pragma unroll
       for (int r = 0; r < kCap; ++r)
-        if ((uint32_t)r < nrw && ((fl >> r) & 1u)) t += ev[r][0] + (V)(uint32_t)(ek[r] & 1u);
+        if ((uint32_t)r < nrw && ((hv >> r) & 1u)) t += ev[r][0] + (V)(uint32_t)(ek[r] & 1u);
       acc[0][s0] += t;
       done += kNW * Rw;
       if (done < U) {
@@ -405,29 +434,60 @@ __global__ __launch_bounds__(nt_of(kGroup), (occupancy<V, M, kGroup>())) void ti
       continue;
     }
 #endif
-    // ---- search every held round
+    // ---- search every held round: one bucket-table read, then a window of
+    // the 4 server keys from the bucket start, compared without branches.
+    // The bucket map is monotone, so every key past the bucket is > k (and
+    // the sentinels ~0 past the tile are >= k): c = window keys below k is
+    // the lower bound inside the bucket whenever the bucket holds <= 4 keys
+    // or c < 4, and k is present iff a window key equals it at a position
+    // inside the tile.  One bucket per slot (Poisson occupancy): c == 4 with
+    // more keys left in the bucket is ~0.4 % of keys; those finish below.
     uint32_t pos[kCap];
-    fl &= 0xffu;
+    fd = 0;
+    okb = 0;
+    uint32_t deep = 0;  // bit r: this lane's key lies past its round's window
 #pragma unroll
     for (int r = 0; r < kCap; ++r) {
       pos[r] = 0;
       if ((uint32_t)r < nrw) {
         const uint64_t k = ek[r];
         const uint32_t b = bucket(k);
-        uint32_t l = bt[b];
-        uint32_t n = (uint32_t)bt[b + 1] - l;
-        while (n > 2u) {  // crowded bucket
-          const uint32_t half = n >> 1;
-          if (dk[l + half - 1] < k) {
-            l += half;
-            n -= half;
-          } else {
-            n = half;
+        const uint32_t l = bt[b];
+        const uint32_t n = (uint32_t)bt[b + 1] - l;
+        const uint64_t* wk = dk + l;
+        const uint64_t k0 = wk[0], k1 = wk[1], k2 = wk[2], k3 = wk[3];
+        const uint32_t c = (uint32_t)(k0 < k) + (uint32_t)(k1 < k) + (uint32_t)(k2 < k) +
+                           (uint32_t)(k3 < k);
+        const uint32_t p = l + c;
+        pos[r] = p;
+        // equality as lane masks (4 compares + 3 scalar ors)
+        const uint64_t eq = __ballot(k0 == k) | __ballot(k1 == k) | __ballot(k2 == k) |
+                            __ballot(k3 == k);
+        const bool hit = ((eq >> lane) & 1ull) && p < nt;
+        fd |= (uint32_t)hit << r;
+        deep |= (uint32_t)(c == 4u && n > 4u) << r;
+      }
+    }
+    if (__ballot(deep != 0u)) {  // long buckets: bisect the rest of the bucket
+#pragma unroll
+      for (int r = 0; r < kCap; ++r) {
+        if ((deep >> r) & 1u) {
+          const uint64_t k = ek[r];
+          const uint32_t b = bucket(k);
+          uint32_t l = bt[b] + 4u;
+          uint32_t n = (uint32_t)bt[b + 1] - l;
+          while (n > 0u) {
+            const uint32_t half = n >> 1;
+            if (dk[l + half] < k) {
+              l += half + 1u;
+              n -= half + 1u;
+            } else {
+              n = half;
+            }
           }
+          pos[r] = l;
+          fd |= (uint32_t)(l < nt && dk[l] == k) << r;
         }
-        const uint64_t k0 = dk[l], k1 = dk[l + 1];
-        pos[r] = l + ((n > 0u && k0 < k) ? 1u : 0u) + ((n > 1u && k1 < k) ? 1u : 0u);
-        fl |= (uint32_t)((n > 0u && k0 == k) || (n > 1u && k1 == k)) << (8 + r);
       }
     }
     int mylast = 0;  // position held by lane 63 in this wave's last round
@@ -443,7 +503,7 @@ __global__ __launch_bounds__(nt_of(kGroup), (occupancy<V, M, kGroup>())) void ti
       V t = V(0);
 #pragma unroll
       for (int r = 0; r < kCap; ++r)
-        if ((uint32_t)r < nrw && ((fl >> (8 + r)) & 1u)) t += ev[r][0] + (V)pos[r];
+        if ((uint32_t)r < nrw && ((fd >> r) & 1u)) t += ev[r][0] + (V)pos[r];
       acc[0][s0] += t;
       done += kNW * Rw;
       if (done < U) {
@@ -464,19 +524,24 @@ __global__ __launch_bounds__(nt_of(kGroup), (occupancy<V, M, kGroup>())) void ti
         else if (r > 0) prev0 = __builtin_amdgcn_readlane((int)pos[r - 1], 63);
         else prev0 = w > 0 ? lastpos[w - 1] : pcarry;
         const int prev = __builtin_amdgcn_update_dpp(prev0, (int)pos[r], 0x138, 0xf, 0xf, false);
-        const bool ok = ((fl >> r) & 1u) && ((fl >> (8 + r)) & 1u) && (int)pos[r] > prev;
-        fl |= (uint32_t)ok << (16 + r);
+#if PSG_SKELETON == 4
+        const bool ok = ((hv & fd) >> r & 1u) && prev != 0x7fffffff;  // diagnostic: no order test
+#else
+        const bool ok = ((hv & fd) >> r & 1u) && (int)pos[r] > prev;
+#endif
+        okb |= (uint32_t)ok << r;
         if (!parallel && ok)
-          __hip_atomic_fetch_add(&cnt32[pos[r] >> 1], 1u << (16u * (pos[r] & 1u)),
+          __hip_atomic_fetch_add(kCntW ? &cnt32[pos[r]] : &cnt32[pos[r] >> 1],
+                                 kCntW ? 1u : 1u << (16u * (pos[r] & 1u)),
                                  __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
       }
     }
     // elements that exist but did not match: one ballot per pass, counts per
     // round only when there are any
-    if (__ballot((fl & ~(fl >> 16) & 0xffu) != 0u)) {
+    if (__ballot((hv & ~okb) != 0u)) {
 #pragma unroll
       for (int r = 0; r < kCap; ++r) {
-        const uint64_t bad = __ballot(((fl >> r) & ~(fl >> (16 + r)) & 1u) != 0u);
+        const uint64_t bad = __ballot(((hv & ~okb) >> r & 1u) != 0u);
         if ((uint32_t)r < nrw && bad && lane == 0)
           __hip_atomic_fetch_add(GW(T.fail) + g0 + (re[r] >> kCB),
                                  (unsigned long long)__popcll(bad), __ATOMIC_RELAXED,
@@ -487,11 +552,18 @@ __global__ __launch_bounds__(nt_of(kGroup), (occupancy<V, M, kGroup>())) void ti
     // ---- fold, wave by wave (rounds are push-major)
     const uint32_t inpass = (U - done) < kNW * Rw ? U - done : kNW * Rw;
     const uint32_t wl = (inpass - 1) / Rw;  // wave holding the pass's last round
+#if PSG_SKELETON == 3
+    // diagnostic: every wave folds at once (racy: wrong sums on shared slots),
+    // the cost of the wave-ordered fold's serialisation
+    for (uint32_t st = 0; st < 1u; ++st) {
+      {
+#else
     for (uint32_t st = 0; st < (uint32_t)kNW; ++st) {
       if (st == w) {
+#endif
 #pragma unroll
         for (int r = 0; r < kCap; ++r) {
-          if ((uint32_t)r < nrw && ((fl >> (16 + r)) & 1u)) {
+          if ((uint32_t)r < nrw && ((okb >> r) & 1u)) {
             const uint32_t q = re[r] >> kCB;
             const uint32_t s = pos[r];
             const bool first = g0 + q == 0u && !cont;
@@ -525,7 +597,8 @@ __global__ __launch_bounds__(nt_of(kGroup), (occupancy<V, M, kGroup>())) void ti
   V res[M][4];
 #pragma unroll
   for (int j = 0; j < 4; ++j) {
-    const bool gap = !parallel && (uint32_t)((const uint16_t*)cnt32)[s0 + j] != np;
+    const uint32_t ncontrib = kCntW ? cnt32[s0 + j] : (uint32_t)((const uint16_t*)cnt32)[s0 + j];
+    const bool gap = !parallel && ncontrib != np;
 #pragma unroll
     for (int mi = 0; mi < M; ++mi) {
       const V a = acc[mi][s0 + j];
@@ -626,12 +699,16 @@ __global__ __launch_bounds__(kTSl / 4) void bucket_index_kernel(
     o[tid * (kBPT / 2) + i] = (e[2 * i] + off) | (e[2 * i + 1] + off) << 16;
 }
 
+#ifndef PSG_PAD_LDS
+#define PSG_PAD_LDS 0  // diagnostic A/B builds only: dynamic LDS per workgroup that
+                       // lowers the workgroups per CU at unchanged code
+#endif
 template <typename V, int M>
 hipError_t go(const TileDesc* t, uint32_t n, int form, hipStream_t s) {
   if (form == 1)
-    hipLaunchKernelGGL((tile_kernel<V, M, 64>), dim3(n), dim3(nt_of(64)), 0, s, t, n);
+    hipLaunchKernelGGL((tile_kernel<V, M, 64>), dim3(n), dim3(nt_of(64)), PSG_PAD_LDS, s, t, n);
   else
-    hipLaunchKernelGGL((tile_kernel<V, M, 32>), dim3(n), dim3(nt_of(32)), 0, s, t, n);
+    hipLaunchKernelGGL((tile_kernel<V, M, 32>), dim3(n), dim3(nt_of(32)), PSG_PAD_LDS, s, t, n);
   return hipGetLastError();
 }
 
