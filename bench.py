@@ -48,7 +48,7 @@ WORKLOADS = {
     "cfg2": dict(batch=64, desc=(
         "cfg2: {a.npush} pushes x {a.n} sorted unique uint64 keys + {a.dtype} values, 10% shared "
         "keys (U={U:,}); {batch} such (channel,time) aggregates per GPU per step")),
-    "cfg3": dict(batch=2, desc=(
+    "cfg3": dict(batch=4, desc=(
         "cfg3 (CTR shape): 64 pushes x 131072 unique murmur-shuffled Zipf(1.1) ranks in "
         "[1,1e9] + f32 values (U={U:,}); {batch} such aggregates per step")),
     "cfg4": dict(batch=1, desc=(
@@ -60,10 +60,17 @@ WORKLOADS = {
 }
 
 
-# the aggregate kernel each workload's plan runs (the runtime picks the form:
-# dense slices, short pieces -> packed rounds, > 32 pushes -> 64-push groups)
-KERNEL = {"cfg2": "tile_kernel<float,1,32>", "cfg2_f64": "tile_kernel<double,1,32>", "cfg3": "tile_kernel<float,1,64>",
-          "cfg4": "dense_kernel<float,1>", "cfg5": "tile_packed_kernel<float,1>"}
+# the aggregate kernel a plan runs (the runtime picks the form: dense slices,
+# sorted pushes on a resident index -> per-push cursors, short pieces ->
+# packed rounds, > 32 pushes -> 64-push groups); names as rocprofv3 lists them
+def kernel_name(plan, dtype="f32"):
+    from parameter_server_amd import _lib
+    v = "double" if dtype == "f64" else "float"
+    return {_lib.PSG_KERNEL_TILE: f"tile_kernel<{v},1,32>",
+            _lib.PSG_KERNEL_TILE64: f"tile_kernel<{v},1,64>",
+            _lib.PSG_KERNEL_PACKED: f"tile_packed_kernel<{v},1>",
+            _lib.PSG_KERNEL_DENSE: f"dense_kernel<{v},1>",
+            _lib.PSG_KERNEL_CURSOR: f"cursor_kernel<{v},1,KR>"}[plan.form]
 
 
 def parse():
@@ -82,6 +89,8 @@ def parse():
                          "batch_solver.h:32); the headline is f32 (north star)")
     ap.add_argument("--no-cfg5", action="store_true",
                     help="skip the cfg5 strong-scaling block of the default line")
+    ap.add_argument("--no-f64", action="store_true",
+                    help="skip the f64 (the reference apps' double) cfg2 block of the default line")
     ap.add_argument("--cfg5-steps", type=int, default=10)
     ap.add_argument("--cfg5-unsliced-child", action="store_true",
                     help=argparse.SUPPRESS)  # internal: the unsliced leg in its own process
@@ -317,7 +326,7 @@ def main():
             "unit": "GB/s",
             "frac": achieved / HBM_PEAK_GBPS,
             "traffic": traffic.get("tile") if traffic else None,
-            "kernel": KERNEL[wl + ("_f64" if args.dtype == "f64" else "")],
+            "kernel": kernel_name(plan, args.dtype),
             "bytes_per_launch": nbytes,
             "bytes_formula": formula,
             "kernel_ms": agg_ms,
@@ -335,8 +344,12 @@ def main():
         torch.cuda.empty_cache()
         result["server_api"] = {"pinned_out": cfg4_server_api(insts[0], local),
                                 "pageable_out": cfg4_server_api(insts[0], local, pinned_out=False)}
-    if wl == "cfg2" and not args.no_cfg5 and args.dtype == "f32":
+    if wl == "cfg2" and not args.no_f64 and args.dtype == "f32":
         del plan, keep
+        torch.cuda.empty_cache()
+        result["f64"] = f64_block(args, insts, dist, dev, local, stream)
+    if wl == "cfg2" and not args.no_cfg5 and args.dtype == "f32":
+        plan = keep = None
         torch.cuda.empty_cache()
         result["cfg5"] = cfg5_block(args, rank, world, bounds, dist, dev, local, stream)
     if rank == 0 and world == 1 and not args.no_cpu_baseline and wl == "cfg2" and \
@@ -348,6 +361,40 @@ def main():
         print(json.dumps(result), flush=True)
     if dist:
         dist.destroy_process_group()
+
+
+def f64_block(args, insts, dist, dev, local, stream):
+    """The headline workload in the reference apps' value type
+    (KVVector<Key,double>, batch_solver.h:32): the same --batch cfg2
+    aggregates (same keys; the f32 values widened to f64, exact), the same
+    timed step (partition + aggregate, K steps, barrier + synchronize,
+    max over ranks).  Bytes per launch use s_V = 8."""
+    f64 = [(D, [(k, [np.asarray(v, np.float64) for v in vs]) for k, vs in pushes])
+           for D, pushes in insts]
+    plan, keep, jobs = make_plan(f64, dev, local)
+    plan.run(stream.cuda_stream)
+    want = np.array([n for jb in jobs for n in jb["push_n"]], np.uint64)
+    assert args.no_check or np.array_equal(plan.matched(), want), "f64: unmatched keys"
+    K = args.steps
+    wall, part_ms, agg_ms = timed_steps(plan, K, args.warmup, stream, dist)
+    wall_max, kv_all = reduce_over_ranks(wall, plan.kv_pairs, dist, dev)
+    nbytes = int(plan.bytes)
+    out = {
+        "dtype": "f64",
+        "value": kv_all * K / wall_max,
+        "unit": "kv-pairs/s",
+        "ms_per_step": wall_max / K * 1e3,
+        "kernel": kernel_name(plan, "f64"),
+        "kernel_ms": agg_ms,
+        "partition_ms": part_ms,
+        "bytes_per_launch": nbytes,
+        "bytes_formula": "sum_p n_p*(8+8) [pushes] + U*(8+8) [server keys + sums] (SURVEY 8d)",
+        "frac": nbytes / (agg_ms * 1e-3) / 1e9 / HBM_PEAK_GBPS,
+        "step_frac": nbytes / (wall_max / K) / 1e9 / HBM_PEAK_GBPS,
+        "data": "the f32 line's aggregates, values widened to f64",
+    }
+    del plan, keep
+    return out
 
 
 def timed_stages(stages, K, W, stream, dist):

@@ -83,6 +83,8 @@ typedef enum psg_dtype { PSG_F32 = 0, PSG_F64 = 1 } psg_dtype;
 #define PSG_NO_DENSE 0x40000u     /* never the dense (contiguous-slice) kernel */
 #define PSG_NO_ZERO_COPY 0x80000u /* context: DMA copies instead of GPU reads of pinned memory */
 #define PSG_NO_INDEX 0x100000u    /* plan: no resident bucket index (tables built per run) */
+#define PSG_FORM_CURSOR 0x400000u /* plan: cursor kernel (no partition pass) whenever it applies */
+#define PSG_NO_CURSOR 0x800000u   /* plan: never the cursor kernel (partition + tile kernel) */
 /* Plan option (psg_plan_create): the caller promises that the push KEYS at
  * the job's device pointers stay as they were at creation for the plan's
  * lifetime (values may change between runs).  Only then may the plan take
@@ -239,6 +241,14 @@ int psg_plan_run_stage(psg_plan* plan, int stage, void* stream);
 /* Synchronises the plan's last run and returns per-push matched counts,
  * jobs in order, pushes in order (sum of npush entries). */
 int psg_plan_matched(psg_plan* plan, uint64_t* matched);
+/* The aggregate kernel a plan runs (its form, chosen at creation from the
+ * shape of the jobs or by the PSG_FORM_* flags): */
+#define PSG_KERNEL_TILE 0    /* partition + push-uniform rounds, 1024-slot tiles */
+#define PSG_KERNEL_TILE64 1  /* partition + push-uniform rounds, 64-push groups */
+#define PSG_KERNEL_PACKED 2  /* partition + rounds packing several pushes */
+#define PSG_KERNEL_DENSE 3   /* contiguous slices: no key reads */
+#define PSG_KERNEL_CURSOR 4  /* no partition: per-push cursors across tile chunks */
+int psg_plan_form(psg_plan* plan, int* form);
 /* Algorithmic HBM bytes of one run (SURVEY.md 8d general form). */
 int psg_plan_bytes(psg_plan* plan, uint64_t* bytes, uint64_t* kv_pairs);
 int psg_plan_destroy(psg_plan* plan);

@@ -53,6 +53,10 @@ PSG_NO_ZERO_COPY = 0x80000
 PSG_NO_INDEX = 0x100000
 # plan option: push keys fixed for the plan's lifetime (enables the dense kernel)
 PSG_STATIC_KEYS = 0x200000
+PSG_FORM_CURSOR = 0x400000
+PSG_NO_CURSOR = 0x800000
+# psg_plan_form: the aggregate kernel a plan runs
+PSG_KERNEL_TILE, PSG_KERNEL_TILE64, PSG_KERNEL_PACKED, PSG_KERNEL_DENSE, PSG_KERNEL_CURSOR = range(5)
 MAX_VALUE_ARRAYS = 4
 
 # Every symbol include/psg.h declares, with its ctypes signature.
@@ -111,6 +115,7 @@ SIGNATURES = {
     "psg_plan_run_stage": (C.c_int, [_p, C.c_int, _p]),
     "psg_plan_matched": (C.c_int, [_p, _pu64]),
     "psg_plan_bytes": (C.c_int, [_p, _pu64, _pu64]),
+    "psg_plan_form": (C.c_int, [_p, C.POINTER(C.c_int)]),
     "psg_plan_destroy": (C.c_int, [_p]),
     "psg_gather_dev": (C.c_int, [C.c_int, _p, _u64, _p, _p, _u64, _p, _p, _p]),
     "psg_key_union_dev": (C.c_int, [_p, _u64, _p, _u64, _p, _pu64, _p]),

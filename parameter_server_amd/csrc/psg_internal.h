@@ -76,6 +76,32 @@ struct TileDesc {
   const uint32_t* bt;
 };
 
+// Cursor form (psg_tile_cursor.hip): one job of a plan as the cursor kernel
+// sees it (no partition pass: pieces are found by the element loads), and a
+// chunk = a run of consecutive tiles of one job walked by one workgroup.
+struct CursorJob {
+  const uint64_t* dkeys;          // D + lo
+  uint64_t nslots;
+  const uint64_t* const* pkeys;   // [np]
+  const void* const* pvals;       // [np * m]
+  const uint64_t* pn;             // [np]
+  void* const* out;               // [m]
+  unsigned long long* fail;       // [np] match failures
+  uint32_t* seg;                  // tile-major rows: row 0 / row ntiles = covered range
+  const uint32_t* bt;             // the resident bucket index of the job's tile 0
+  uint32_t np, ntiles, flags;
+  uint32_t kr;                    // rounds of 64 keys per push per tile (1..3, the plan's)
+};
+struct CursorChunk {
+  uint32_t job, t0, t1;           // tiles [t0, t1) of job
+};
+constexpr int kCursorPushes = 32;  // pushes per job in the cursor form (LDS cursors)
+// boundary words: (nchunks + 1) x 32 u32, zeroed before each run
+// kr: rounds per push per tile, one value for every job of the launch
+hipError_t launch_aggregate_cursor(int dtype, int m, int kr, const CursorJob* d_jobs,
+                                   const CursorChunk* d_chunks, uint32_t nchunks, uint32_t* bx,
+                                   hipStream_t stream);
+
 // dense check of one push against the server keys (psg_tile_dense.hip):
 // out[0] = lower_bound(D, keys[0]), out[1] != 0 unless keys == D[out0, +n)
 struct DenseCheck {

@@ -10,6 +10,7 @@
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <cmath>
 #include <iterator>
 #include <cstdarg>
 #include <cstdio>
@@ -149,7 +150,9 @@ int detect_dense(std::vector<JobSpec>& specs) {
 struct JobTable {
   int device = -1;
   int knob_part = -1, knob_pack = -1, knob_wide = -1;  // forced (read_knobs), -1 = chosen
+  int knob_cursor = -1;
   void read_knobs(unsigned f) {
+    knob_cursor = (f & PSG_FORM_CURSOR) ? 1 : (f & PSG_NO_CURSOR) ? 0 : -1;
     knob_part = (f & PSG_PART_SEARCH) ? (int)psg::kSearch
                 : (f & PSG_PART_STREAM) ? (int)psg::kStream : -1;
     knob_pack = (f & PSG_FORM_PACKED) ? 1 : (f & PSG_FORM_UNIFORM) ? 0 : -1;
@@ -159,6 +162,17 @@ struct JobTable {
   bool pack = false;  // rounds may hold several pushes
   bool wide = false;  // push groups of 64 in the tile kernel (a job has > 32 pushes)
   bool dense = false;  // every job dense: psg_tile_dense.hip, no partition
+  // cursor form (psg_tile_cursor.hip): plans of long pieces, no partition
+  // pass; chunks of consecutive tiles, one workgroup each
+  bool cursor = false;
+  uint32_t nchunks = 0;
+  psg::CursorJob* d_cjobs = nullptr;
+  psg::CursorChunk* d_chunks = nullptr;
+  uint32_t* d_bx = nullptr;   // chunk boundary words
+  void* d_zero = nullptr;     // fail counters of every job + boundary words: zeroed per run
+  size_t zero_bytes = 0;
+  std::vector<uint32_t> chunk0;  // per job: its first chunk
+  uint32_t ckr = 3;              // rounds per push per tile (max over the jobs)
   int dtype = 0, m = 1;
   std::vector<JobDev> h;
   // per job (host): pushes kept (non-empty) and where their matched counts go
@@ -170,6 +184,8 @@ struct JobTable {
     uint32_t* seg = nullptr;
     uint32_t segq = 1;                 // seg stride between pushes
     unsigned long long* fail = nullptr;
+    uint32_t kr = 0;                   // cursor form: rounds per push per tile
+    uint32_t nch = 0;                  // cursor form: chunks
   };
   std::vector<JobInfo> info;
   uint32_t ntiles = 0, nitems = 0, nsplit = 0;
@@ -297,6 +313,45 @@ struct JobTable {
         return fail(PSG_ERR_ARG, "batch too large (%llu tiles)", (unsigned long long)tiles);
       if (j >= (1ull << 27)) return fail(PSG_ERR_ARG, "too many jobs");
     }
+    // the cursor form: plans (resident index) of search-mode jobs of at most
+    // kCursorPushes pushes whose pieces fit kr <= 3 rounds (mean + 4 sigma
+    // keys per push per tile <= 192; longer ones would finish round by round)
+    // explicit partition / round-form flags select the partition path
+    // unless PSG_FORM_CURSOR is given too
+    cursor = index && !dense && !pack && !wide && knob_cursor != 0 && tiles > 0 &&
+             (knob_cursor == 1 || (knob_part < 0 && knob_pack < 0));
+    for (size_t j = 0; cursor && j < jobs.size(); ++j) {
+      const JobSpec& s = jobs[j];
+      JobInfo& I = info[j];
+      if (s.dense || h[j].mode != psg::kSearch || I.np > (uint32_t)psg::kCursorPushes) {
+        cursor = false;
+        break;
+      }
+      double kv = 0;
+      for (uint64_t n : I.pn) kv += (double)n;
+      const double piece = I.np && I.ntiles ? kv / ((double)I.np * I.ntiles) : 0.0;
+      const double need = piece + 4.0 * std::sqrt(piece) + 1.0;
+      if (need > 192.0 && knob_cursor != 1) cursor = false;
+      I.kr = (uint32_t)std::min(3.0, std::max(1.0, std::ceil(need / 64.0)));
+    }
+    if (cursor) {  // one kernel instance: the jobs' largest round count
+      ckr = 1;
+      for (const JobInfo& I : info) ckr = std::max(ckr, I.kr);
+      for (JobInfo& I : info) I.kr = ckr;
+    }
+    if (cursor) {
+      // about one chunk per workgroup slot of the chip (256 CUs x 8)
+      constexpr uint64_t kChunkTarget = 2048;
+      const uint64_t per = std::max<uint64_t>(1, (tiles + kChunkTarget - 1) / kChunkTarget);
+      uint64_t nc = 0;
+      for (JobInfo& I : info) {
+        I.nch = (uint32_t)((I.ntiles + per - 1) / per);
+        nc += I.nch;
+      }
+      nchunks = (uint32_t)nc;
+    } else {
+      nchunks = 0;
+    }
     size_t off = align_up(sizeof(JobDev) * jobs.size(), 256);
     const size_t tiles_off = off;
     off = align_up(off + sizeof(psg::TileDesc) * tiles, 256);
@@ -310,6 +365,22 @@ struct JobTable {
     off = align_up(off + 4 * sitems, 256);
     const size_t items_off = off;
     off = align_up(off + 8 * items, 256);
+    // the cursor form's job and chunk tables
+    const size_t cjobs_off = off;
+    if (cursor) off = align_up(off + sizeof(psg::CursorJob) * jobs.size(), 256);
+    const size_t chunks_off = off;
+    if (cursor) off = align_up(off + sizeof(psg::CursorChunk) * nchunks, 256);
+    // one zeroed region: every job's fail counters, then the boundary words
+    const size_t zero_off = off;
+    size_t fail_cur = zero_off;
+    {
+      uint64_t npall = 0;
+      for (const JobInfo& I : info) npall += I.np;
+      off = align_up(off + 8 * npall, 256);
+    }
+    const size_t bx_off = off;
+    if (cursor) off = align_up(off + 4 * 32 * ((size_t)nchunks + 1), 256);
+    const size_t zero_end = off;
     for (size_t j = 0; j < jobs.size(); ++j) {
       const size_t np = info[j].np, nt = info[j].ntiles;
       Offs& o = offs[j];
@@ -317,7 +388,7 @@ struct JobTable {
       o.pv = off; off = align_up(off + 8 * np * m, 64);
       o.pn = off; off = align_up(off + 8 * np, 64);
       o.out = off; off = align_up(off + 8 * m, 64);
-      o.fail = off; off = align_up(off + 8 * np, 64);
+      o.fail = fail_cur; fail_cur += 8 * np;
       o.seg = off; off = align_up(off + 4 * (nt + 1) * np, 256);
       o.split = off;
       if (h[j].mode == psg::kStream) off = align_up(off + 8 * (nt + 1), 256);
@@ -425,6 +496,40 @@ struct JobTable {
         T.bt = use_index ? (const uint32_t*)(base + index_off) + (size_t)(tcur - 1) * iw : nullptr;
       }
     }
+    if (cursor) {
+      psg::CursorJob* hcj = (psg::CursorJob*)(img + cjobs_off);
+      psg::CursorChunk* hch = (psg::CursorChunk*)(img + chunks_off);
+      chunk0.assign(jobs.size(), 0);
+      uint64_t tbase = 0, ccur = 0;
+      for (size_t j = 0; j < jobs.size(); ++j) {
+        const JobInfo& I = info[j];
+        const JobDev& d = h[j];
+        psg::CursorJob& c = hcj[j];
+        c.dkeys = jobs[j].keys;
+        c.nslots = jobs[j].nslots;
+        c.pkeys = d.pkeys;
+        c.pvals = (const void* const*)(base + offs[j].pv);
+        c.pn = d.pn;
+        c.out = (void* const*)(base + offs[j].out);
+        c.fail = d.fail;
+        c.seg = d.seg;
+        c.bt = (const uint32_t*)(base + index_off) + (size_t)tbase * iw;
+        c.np = I.np;
+        c.ntiles = I.ntiles;
+        c.flags = jobs[j].flags;
+        c.kr = I.kr;
+        chunk0[j] = (uint32_t)ccur;
+        for (uint32_t k = 0; k < I.nch; ++k) {
+          psg::CursorChunk& ch = hch[ccur++];
+          ch.job = (uint32_t)j;
+          ch.t0 = (uint32_t)((uint64_t)k * I.ntiles / I.nch);
+          ch.t1 = (uint32_t)((uint64_t)(k + 1) * I.ntiles / I.nch);
+        }
+        tbase += I.ntiles;
+      }
+      if (ccur != nchunks) return fail(PSG_ERR_DEVICE, "cursor chunks %llu/%u",
+                                       (unsigned long long)ccur, nchunks);
+    }
     // the fill must match the sizing pass exactly (the image regions are
     // packed back to back): a mismatch is a bug, never launched
     if (icur != items || scur != sitems || tcur != tiles)
@@ -440,6 +545,11 @@ struct JobTable {
     d_tiles = (psg::TileDesc*)(base + tiles_off);
     d_split_items = (uint32_t*)(base + sitems_off);
     d_items = (uint64_t*)(base + items_off);
+    d_cjobs = cursor ? (psg::CursorJob*)(base + cjobs_off) : nullptr;
+    d_chunks = cursor ? (psg::CursorChunk*)(base + chunks_off) : nullptr;
+    d_bx = cursor ? (uint32_t*)(base + bx_off) : nullptr;
+    d_zero = base + zero_off;
+    zero_bytes = zero_end - zero_off;
     // the image is small: a DMA copy's fixed cost exceeds its transfer time
     if (zero_copy && himg_dev[ib] && (((uintptr_t)himg_dev[ib] | (uintptr_t)blob) & 15u) == 0)
       HIP_TRY(psg::launch_host_copy(blob, himg_dev[ib], off, strm));
@@ -456,8 +566,11 @@ struct JobTable {
   int run_stage(int stage, hipStream_t s) const {
     if (h.empty()) return PSG_OK;
     if (stage == 0) {
-      if (!dense) HIP_TRY(psg::launch_partition(d_jobs, d_split_items, nsplit, d_items, nitems, s));
-    } else if (dense)
+      if (cursor) HIP_TRY(hipMemsetAsync(d_zero, 0, zero_bytes, s));  // fail counters, boundaries
+      else if (!dense) HIP_TRY(psg::launch_partition(d_jobs, d_split_items, nsplit, d_items, nitems, s));
+    } else if (cursor)
+      HIP_TRY(psg::launch_aggregate_cursor(dtype, m, (int)ckr, d_cjobs, d_chunks, nchunks, d_bx, s));
+    else if (dense)
       HIP_TRY(psg::launch_aggregate_dense(dtype, m, d_tiles, ntiles, s));
     else if (pack)
       HIP_TRY(psg::launch_aggregate_tile_packed(dtype, m, d_tiles, ntiles, s));
@@ -488,9 +601,21 @@ struct JobTable {
         HIP_TRY(hipMemcpy2D(first.data(), 4, I.seg, pitch, 4, np, hipMemcpyDeviceToHost));
         HIP_TRY(hipMemcpy2D(last.data(), 4, I.seg + (size_t)nt * segb, pitch, 4, np,
                             hipMemcpyDeviceToHost));
+        // cursor form: a chunk boundary where the chunks' cursors disagree
+        // (start != the previous chunk's end) means an unsorted push
+        std::vector<uint32_t> bxw;
+        if (cursor && I.nch > 1) {
+          bxw.resize((size_t)32 * (I.nch - 1));
+          HIP_TRY(hipMemcpy(bxw.data(), d_bx + (size_t)32 * (chunk0[j] + 1), 4 * bxw.size(),
+                            hipMemcpyDeviceToHost));
+        }
         for (uint32_t p = 0; p < np; ++p) {
           const uint64_t covered = last[p] >= first[p] ? (uint64_t)(last[p] - first[p]) : 0;
-          mt[I.slot[p]] = covered >= f[p] ? covered - f[p] : 0;
+          uint64_t v = covered >= f[p] ? covered - f[p] : 0;
+          bool torn = false;
+          for (size_t k = 0; k + 1 < I.nch && cursor; ++k) torn |= bxw[32 * k + p] != 0;
+          if (torn && v >= I.pn[p]) v = I.pn[p] - 1;
+          mt[I.slot[p]] = v;
         }
       }
       out.insert(out.end(), mt.begin(), mt.end());
@@ -1192,6 +1317,17 @@ int psg_plan_matched(psg_plan* plan, uint64_t* matched) {
   std::vector<uint64_t> mt;
   if (int rc = plan->table.matched(mt)) return rc;
   std::copy(mt.begin(), mt.end(), matched);
+  return PSG_OK;
+}
+
+int psg_plan_form(psg_plan* plan, int* form) {
+  if (!plan || !form) return fail(PSG_ERR_ARG, "null argument");
+  const JobTable& T = plan->table;
+  *form = T.cursor ? PSG_KERNEL_CURSOR
+          : T.dense ? PSG_KERNEL_DENSE
+          : T.pack  ? PSG_KERNEL_PACKED
+          : T.wide  ? PSG_KERNEL_TILE64
+                    : PSG_KERNEL_TILE;
   return PSG_OK;
 }
 

@@ -245,6 +245,9 @@ class MergePlan:
         b, kv = C.c_uint64(), C.c_uint64()
         _lib.check(self._L.psg_plan_bytes(h, C.byref(b), C.byref(kv)))
         self.bytes, self.kv_pairs = b.value, kv.value
+        f = C.c_int()
+        _lib.check(self._L.psg_plan_form(h, C.byref(f)))
+        self.form = f.value  # _lib.PSG_KERNEL_*
 
     def run(self, stream: Optional[int] = None) -> None:
         _lib.check(self._L.psg_plan_run(self._h, stream or None))

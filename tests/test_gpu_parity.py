@@ -953,3 +953,92 @@ def test_growing_value_array_list(torch_cuda, parallel, flush):
         rc, lo, hi, want, _ = O.aggregate(D, *ALL, sub, parallel, 1, dtype)
         assert rc == 0 and list(out[i][0]) == [lo, hi]
         assert_bitexact(out[i][1], want[0])
+
+
+def _cursor_check(torch, cases, parallel, flags=0, want_form=None, reps=2):
+    from parameter_server_amd._lib import PSG_KERNEL_CURSOR
+    plan, keep = plan_for(torch, cases, parallel=parallel, flags=flags)
+    assert plan.form == (PSG_KERNEL_CURSOR if want_form is None else want_form)
+    for _ in range(reps):  # a second run lands in the same buffers (bench loop)
+        plan.run()
+        mt = plan.matched().tolist()
+        want_mt = []
+        for j, (Dj, pushes) in enumerate(cases):
+            rc, _, _, want, wm = O.aggregate(Dj, *ALL, pushes, parallel=parallel)
+            want_mt += [int(x) for x in wm]
+            assert_bitexact(keep[4 * j + 3][0].cpu().numpy()[: Dj.size], want[0])
+        assert mt == want_mt
+    plan.close()
+
+
+@pytest.mark.parametrize("parallel", [False, True])
+def test_plan_cursor_form(torch_cuda, parallel):
+    """The cursor kernel (psg_tile_cursor.hip: no partition pass; each
+    workgroup walks a chunk of tiles with one cursor per push and finds a
+    piece's end with the element loads): chosen by default for plans of
+    long pieces, bit-exact with the oracle's serialSetValue /
+    parallelSetValue and matched counts, over 8, 3 and 20 pushes (groups of
+    8, idle waves), 1-3 rounds per push, one- and many-tile chunks, D ending
+    at 2^64 - 1 (the open last tile) and a second run."""
+    torch = torch_cuda
+    from parameter_server_amd import synth
+    rng = np.random.default_rng(123)
+    Dh = np.unique(np.concatenate([rng.integers(1 << 63, (1 << 64) - 1, 30000, dtype=np.uint64),
+                                   np.array([(1 << 64) - 1], np.uint64)]))
+    hp = [(np.sort(rng.choice(Dh, 3000, replace=False)),
+           [rng.standard_normal(3000).astype(np.float32)]) for _ in range(4)]
+    # the last 3 tiles whole: ~1000-key pieces, the slow path
+    hp.append((Dh[-3000:].copy(), [rng.standard_normal(3000).astype(np.float32)]))
+    hp[2][1][0][::5] = -0.0
+    cases = [synth.overlap_pushes(31, npush=8, n=40000),            # cfg2-like: 3 rounds
+             synth.overlap_pushes(33, npush=20, n=12000, overlap=0.5),  # 3 groups
+             (Dh, hp),                                                 # open end, 2^64 - 1
+             synth.overlap_pushes(34, npush=6, n=2000, overlap=0.3)]    # 9 tiles
+    _cursor_check(torch, cases, parallel)
+
+
+def test_plan_cursor_long_pieces_and_unmatched(torch_cuda):
+    """PSG_FORM_CURSOR on pieces longer than 3 rounds (3 pushes of ~365 keys
+    per tile: every group takes the slow path, which merges push after push
+    to each piece's end) and pushes holding keys outside D (below D[0],
+    between server keys, above D[-1]): matched counts equal the oracle's,
+    the sums too; PSG_NO_CURSOR gives the partition path the same bits."""
+    torch = torch_cuda
+    from parameter_server_amd import synth
+    from parameter_server_amd._lib import PSG_FORM_CURSOR, PSG_NO_CURSOR, PSG_KERNEL_TILE
+    rng = np.random.default_rng(7)
+    long_ = synth.overlap_pushes(32, npush=3, n=30000)
+    D = np.unique(rng.integers(1000, 1 << 40, 60000, dtype=np.uint64))
+    extra = np.array([1, 2, int(D[100]) + 1, int(D[-1]) + 5], np.uint64)
+    ps = []
+    for i in range(5):
+        k = np.sort(rng.choice(D, 4000, replace=False))
+        if i in (1, 3):
+            k = np.unique(np.concatenate([k, extra if i == 1 else extra[2:]]))
+        ps.append((k, [rng.standard_normal(k.size).astype(np.float32)]))
+    for parallel in (False, True):
+        _cursor_check(torch, [long_, (D, ps)], parallel, flags=PSG_FORM_CURSOR)
+        _cursor_check(torch, [long_, (D, ps)], parallel, flags=PSG_NO_CURSOR,
+                      want_form=PSG_KERNEL_TILE, reps=1)
+
+
+def test_plan_cursor_unsorted_push_is_reported(torch_cuda):
+    """An unsorted push through the cursor form: keys swapped inside one
+    tile (the order check) and across tiles far apart (the chunks' cursors
+    disagree at a chunk boundary: the boundary word reaches
+    psg_plan_matched) are both reported (matched < n) while the sorted
+    pushes of the same plan stay exact."""
+    torch = torch_cuda
+    from parameter_server_amd import synth
+    D, pushes = synth.overlap_pushes(35, npush=8, n=40000)
+    for (i, j) in ((100, 101), (500, 39000)):
+        bad = [(k.copy(), vs) for k, vs in pushes]
+        k = bad[4][0]
+        k[i], k[j] = k[j], k[i]
+        plan, keep = plan_for(torch, [(D, bad)])
+        from parameter_server_amd._lib import PSG_KERNEL_CURSOR
+        assert plan.form == PSG_KERNEL_CURSOR
+        plan.run()
+        mt = plan.matched().tolist()
+        assert mt[4] < 40000 and mt[:4] == [40000] * 4 and mt[5:] == [40000] * 3
+        plan.close()

@@ -1,6 +1,13 @@
 # scratch GPU command of the current step (overwritten per gpurun call)
 set -o pipefail
 export TMPDIR=/tmp
-O=gpurun_out/r04d; mkdir -p $O
-bash tools/ab_run.sh "base sk1 sk2 sk3 sk4 o6 o4 sk1o4" "cfg2" 2>&1 | tee $O/ab_phases.txt
+O=gpurun_out/r04e; mkdir -p $O
+timeout -k 10 400 python3 -u -m pytest tests/test_gpu_parity.py -x -q -m gpu --timeout 200 --timeout-method thread -k "cursor or cfg2 or batched or partition or round_forms or nan or ieee" > $O/gputest_cursor.log 2>&1 || { echo TESTFAIL; tail -40 $O/gputest_cursor.log; exit 1; }
+tail -2 $O/gputest_cursor.log
+for rep in 1 2; do
+for f in 0 0x800000; do
+  timeout -k 10 300 python3 bench.py --no-cpu-baseline --no-cfg5 --no-f64 --steps 20 --plan-flags $f > $O/b.json 2> $O/b.err || { echo "bench failed $f"; tail -5 $O/b.err; exit 1; }
+  python3 -c "import json;d=json.load(open('$O/b.json'));r=d['roofline'];print('$rep flags $f value %.3e ms/step %.4f kern %.4f part %.4f frac %.3f step %.3f'%(d['value'],d['ms_per_step'],r['kernel_ms'],r['partition_ms'],r['frac'],r['step_frac']))"
+done
+done
 echo done
