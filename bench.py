@@ -70,7 +70,8 @@ def kernel_name(plan, dtype="f32"):
             _lib.PSG_KERNEL_TILE64: f"tile_kernel<{v},1,64>",
             _lib.PSG_KERNEL_PACKED: f"tile_packed_kernel<{v},1>",
             _lib.PSG_KERNEL_DENSE: f"dense_kernel<{v},1>",
-            _lib.PSG_KERNEL_CURSOR: f"cursor_kernel<{v},1,KR>"}[plan.form]
+            _lib.PSG_KERNEL_CURSOR: f"cursor_kernel<{v},1,KR>",
+            _lib.PSG_KERNEL_PACKED_CURSOR: f"tile_packed_kernel<{v},1,true>"}[plan.form]
 
 
 def parse():
@@ -355,7 +356,7 @@ def main():
     if rank == 0 and world == 1 and not args.no_cpu_baseline and wl == "cfg2" and \
             args.dtype == "f32":
         result["end_to_end"] = end_to_end(insts[0], local)
-        result["rows"] = bench_rows(local)
+        result["rows"] = bench_rows(local, insts=insts)
         result["cpu_baseline"] = cpu_baseline(insts[0], args.cpu_seconds)
     if rank == 0:
         print(json.dumps(result), flush=True)
@@ -894,7 +895,7 @@ def load_traffic(bytes_per_launch, workload):
             "source": d.get("source")}
 
 
-def bench_rows(device, reps=5):
+def bench_rows(device, reps=5, insts=None):
     """The SURVEY 8(f) rows beside the merge, each on device-resident input
     with its own HBM roofline: algorithmic bytes / mean kernel time (HIP
     events on the stream the kernel runs on).  Shapes: the N-way merge of
@@ -939,7 +940,7 @@ def bench_rows(device, reps=5):
     tot = sum(k.size for k, _ in pushes)
     ok = torch.empty(tot, dtype=torch.int64, device=dev)
     ov = torch.empty(tot, dtype=torch.float32, device=dev)
-    for name, m in (("key_union", 0), ("nway_merge", 1)):
+    for name, m in (("key_union", 0), ("nway_merge_1agg", 1)):
         u = NWayMerge(device, _lib.PSG_F32, [t.data_ptr() for t in dk], [k.size for k, _ in pushes],
                       [[t.data_ptr()] for t in dv] if m else [[] for _ in dk], ok.data_ptr(),
                       [ov.data_ptr()] if m else [])
@@ -954,6 +955,35 @@ def bench_rows(device, reps=5):
                               (" + f32 sums" if m else ""))
     assert np.array_equal(ok[:D.size].cpu().numpy().view(np.uint64), D)
     del dk, dv, ok, ov
+    if insts:
+        # the N-way merge at the headline's scale: its --batch cfg2
+        # aggregates (keys + f32 values) as one pipeline (psg_nway_create_batch:
+        # one launch per stage over every aggregate)
+        from parameter_server_amd.kv_vector import NWayMergeBatch
+        keepb, merges, nb, kvb = [], [], 0, 0
+        for Dj, ps in insts:
+            dkb = [torch.from_numpy(k.view(np.int64)).to(dev) for k, _ in ps]
+            dvb = [torch.from_numpy(vs[0]).to(dev) for _, vs in ps]
+            totb = sum(k.size for k, _ in ps)
+            okb = torch.empty(totb, dtype=torch.int64, device=dev)
+            ovb = torch.empty(totb, dtype=torch.float32, device=dev)
+            keepb.append((dkb, dvb, okb, ovb))
+            merges.append(dict(push_keys=[t.data_ptr() for t in dkb],
+                               push_n=[k.size for k, _ in ps],
+                               push_vals=[[t.data_ptr()] for t in dvb],
+                               out_keys=okb.data_ptr(), out_vals=[ovb.data_ptr()]))
+            nb += totb * 12 + Dj.size * 12
+            kvb += totb
+        u = NWayMergeBatch(device, _lib.PSG_F32, merges)
+        u.run()
+        assert u.result() == [Dj.size for Dj, _ in insts], "batched N-way union sizes"
+        ms = timed(lambda: u.run(st.cuda_stream))
+        u.result()
+        u.close()
+        row("nway_merge", ms, nb, kvb, "keys/s")
+        out["nway_merge"]["shape"] = (f"{len(insts)} cfg2 aggregates (8 pushes x 131,072 keys + "
+                                      "f32 values each -> U = 956,827 keys + sums), one pipeline")
+        del keepb, merges
     # pull gather (getValue) of 1 M sorted request keys from a cfg2 shard
     req = np.sort(np.concatenate([k for k, _ in pushes[:8]]))[::1]
     dD = torch.from_numpy(D.view(np.int64)).to(dev)

@@ -83,8 +83,8 @@ typedef enum psg_dtype { PSG_F32 = 0, PSG_F64 = 1 } psg_dtype;
 #define PSG_NO_DENSE 0x40000u     /* never the dense (contiguous-slice) kernel */
 #define PSG_NO_ZERO_COPY 0x80000u /* context: DMA copies instead of GPU reads of pinned memory */
 #define PSG_NO_INDEX 0x100000u    /* plan: no resident bucket index (tables built per run) */
-#define PSG_FORM_CURSOR 0x400000u /* plan: cursor kernel (no partition pass) whenever it applies */
-#define PSG_NO_CURSOR 0x800000u   /* plan: never the cursor kernel (partition + tile kernel) */
+#define PSG_FORM_CURSOR 0x400000u /* plan: a cursor form (no partition pass) whenever it applies */
+#define PSG_NO_CURSOR 0x800000u   /* plan: never a cursor form (partition + aggregate kernel) */
 /* Plan option (psg_plan_create): the caller promises that the push KEYS at
  * the job's device pointers stay as they were at creation for the plan's
  * lifetime (values may change between runs).  Only then may the plan take
@@ -172,7 +172,10 @@ int psg_push_compressed(psg_ctx* ctx, int chl, int time, uint64_t kb, uint64_t k
  * Each cache is indexed by (chl, [kb, ke)).  No signature: the entry is
  * dropped and the message's keys are used.  Signature + keys: the keys'
  * crc32c over their first PSG_MAX_SIG_LEN bytes (computed on the GPU) must
- * equal `sig` (else PSG_ERR_SIGNATURE), and the resident copy is cached.
+ * equal `sig`, and the resident copy is cached under `sig`.  With values
+ * (m > 0) the check runs on the device without a host wait and a mismatch
+ * is reported by psg_received for `time` (PSG_ERR_SIGNATURE); a key-only
+ * message (m == 0) is checked before its union and fails here.
  * Signature without keys: the cached keys are used in place (no key bytes
  * cross PCIe); a missing entry or another signature is PSG_ERR_SIGNATURE
  * (sig 0 against a missing entry restores no keys: the message is
@@ -248,6 +251,7 @@ int psg_plan_matched(psg_plan* plan, uint64_t* matched);
 #define PSG_KERNEL_PACKED 2  /* partition + rounds packing several pushes */
 #define PSG_KERNEL_DENSE 3   /* contiguous slices: no key reads */
 #define PSG_KERNEL_CURSOR 4  /* no partition: per-push cursors across tile chunks */
+#define PSG_KERNEL_PACKED_CURSOR 5  /* no partition: packed rounds, cursors across tile chunks */
 int psg_plan_form(psg_plan* plan, int* form);
 /* Algorithmic HBM bytes of one run (SURVEY.md 8d general form). */
 int psg_plan_bytes(psg_plan* plan, uint64_t* bytes, uint64_t* kv_pairs);
@@ -287,8 +291,19 @@ int psg_nway_max_push(void);
 int psg_nway_create(int device, int dtype, int m, unsigned flags, int npush,
                     const uint64_t* const* keys, const uint64_t* n, const void* const* vals,
                     uint64_t* out_keys, void* const* out_vals, psg_nway** out);
+/* A batch of nmerge independent merges run as one pipeline (one launch per
+ * stage over all of them: e.g. the 64 aggregates of a bench step).  Merge j
+ * has npush[j] pushes; keys / n / vals list the merges' pushes back to back
+ * (vals: m per push); out_keys[j] and out_vals[j * m + i] are merge j's
+ * outputs.  psg_nway_create is the batch of one. */
+int psg_nway_create_batch(int device, int dtype, int m, unsigned flags, int nmerge,
+                          const int* npush, const uint64_t* const* keys, const uint64_t* n,
+                          const void* const* vals, uint64_t* const* out_keys,
+                          void* const* out_vals, psg_nway** out);
 int psg_nway_run(psg_nway* u, void* stream);
+/* the first merge's merged-count word (device) */
 int psg_nway_count_dev(psg_nway* u, unsigned long long** nout);
+/* nout (host, nullable): one merged count per merge */
 int psg_nway_result(psg_nway* u, uint64_t* nout);
 /* Algorithmic bytes read by a run (sum(n) * (8 + m s_V)) and keys read;
  * the merged output adds |union| * (8 + m s_V). */

@@ -56,7 +56,8 @@ PSG_STATIC_KEYS = 0x200000
 PSG_FORM_CURSOR = 0x400000
 PSG_NO_CURSOR = 0x800000
 # psg_plan_form: the aggregate kernel a plan runs
-PSG_KERNEL_TILE, PSG_KERNEL_TILE64, PSG_KERNEL_PACKED, PSG_KERNEL_DENSE, PSG_KERNEL_CURSOR = range(5)
+(PSG_KERNEL_TILE, PSG_KERNEL_TILE64, PSG_KERNEL_PACKED, PSG_KERNEL_DENSE, PSG_KERNEL_CURSOR,
+ PSG_KERNEL_PACKED_CURSOR) = range(6)
 MAX_VALUE_ARRAYS = 4
 
 # Every symbol include/psg.h declares, with its ctypes signature.
@@ -150,6 +151,8 @@ SIGNATURES = {
     "psg_nway_max_push": (C.c_int, []),
     "psg_nway_create": (C.c_int, [C.c_int, C.c_int, C.c_int, C.c_uint, C.c_int, _p, _p, _p, _p,
                                   _p, C.POINTER(_p)]),
+    "psg_nway_create_batch": (C.c_int, [C.c_int, C.c_int, C.c_int, C.c_uint, C.c_int, _p, _p, _p,
+                                         _p, _p, _p, C.POINTER(_p)]),
     "psg_nway_run": (C.c_int, [_p, _p]),
     "psg_nway_count_dev": (C.c_int, [_p, C.POINTER(_p)]),
     "psg_nway_result": (C.c_int, [_p, _pu64]),

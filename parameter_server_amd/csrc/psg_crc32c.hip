@@ -89,6 +89,52 @@ __device__ uint32_t shift_bytes(uint32_t c, uint64_t n) {
   return c;
 }
 
+// raw CRC (state 0, no inversion) of one chunk of <= kChunk bytes, the
+// whole wave (every lane gets the result)
+__device__ __forceinline__ uint32_t chunk_raw(const uint8_t* p, uint32_t clen, uint32_t lane,
+                                              const uint32_t (*t)[256], const uint32_t (*sh)[256],
+                                              const uint32_t* x8) {
+  const bool a16 = ((uintptr_t)p & 15u) == 0;
+  uint32_t r = 0;     // this lane's register
+  uint32_t last = 0;  // end of this lane's last block (0: none)
+  for (uint32_t base = 0; base < clen; base += 1024u) {
+    const uint32_t bs = base + lane * 16u;
+    if (bs >= clen) break;  // this lane has no block here (nor later)
+    // advance over the 1008 bytes since this lane's previous block
+    if (base)
+      r = sh[0][r & 255u] ^ sh[1][(r >> 8) & 255u] ^ sh[2][(r >> 16) & 255u] ^ sh[3][r >> 24];
+    const uint32_t bl = clen - bs < 16u ? clen - bs : 16u;
+    if (bl == 16u) {
+      uint32_t w0, w1, w2, w3;
+      if (a16) {
+        const uint4 v = *(const uint4*)(p + bs);
+        w0 = v.x; w1 = v.y; w2 = v.z; w3 = v.w;
+      } else {
+        const uint8_t* q = p + bs;
+        uint32_t w[4];
+#pragma unroll
+        for (int j = 0; j < 4; ++j)
+          w[j] = (uint32_t)q[4 * j] | (uint32_t)q[4 * j + 1] << 8 |
+                 (uint32_t)q[4 * j + 2] << 16 | (uint32_t)q[4 * j + 3] << 24;
+        w0 = w[0]; w1 = w[1]; w2 = w[2]; w3 = w[3];
+      }
+      w0 ^= r;
+      r = t[15][w0 & 255u] ^ t[14][(w0 >> 8) & 255u] ^ t[13][(w0 >> 16) & 255u] ^ t[12][w0 >> 24] ^
+          t[11][w1 & 255u] ^ t[10][(w1 >> 8) & 255u] ^ t[9][(w1 >> 16) & 255u] ^ t[8][w1 >> 24] ^
+          t[7][w2 & 255u] ^ t[6][(w2 >> 8) & 255u] ^ t[5][(w2 >> 16) & 255u] ^ t[4][w2 >> 24] ^
+          t[3][w3 & 255u] ^ t[2][(w3 >> 8) & 255u] ^ t[1][(w3 >> 16) & 255u] ^ t[0][w3 >> 24];
+    } else {  // the segment's last, partial block
+      for (uint32_t j = 0; j < bl; ++j) r = t[0][(r ^ p[bs + j]) & 255u] ^ (r >> 8);
+    }
+    last = bs + bl;
+  }
+  // shift over the bytes after this lane's last block (< 1024), reduce
+  uint32_t v = last ? mulmodp(x8[clen - last], r) : 0u;
+#pragma unroll
+  for (int d = 32; d >= 1; d >>= 1) v ^= (uint32_t)__shfl_xor((int)v, d, 64);
+  return v;
+}
+
 __global__ __launch_bounds__(kNT) void crc_kernel(const uint8_t* __restrict__ data,
                                                   const uint64_t* __restrict__ off,
                                                   uint64_t nseg, uint64_t max_len,
@@ -117,46 +163,7 @@ __global__ __launch_bounds__(kNT) void crc_kernel(const uint8_t* __restrict__ da
     uint32_t acc = 0;  // this item's chunks, each shifted to the segment's end
     for (uint64_t cb = c * kChunk; cb < len; cb += per_seg * kChunk) {
       const uint32_t clen = (uint32_t)(len - cb < kChunk ? len - cb : kChunk);
-      const uint8_t* p = data + b0 + cb;
-      const bool a16 = ((uintptr_t)p & 15u) == 0;
-      uint32_t r = 0;     // this lane's register
-      uint32_t last = 0;  // end of this lane's last block (0: none)
-      for (uint32_t base = 0; base < clen; base += 1024u) {
-        const uint32_t bs = base + lane * 16u;
-        if (bs >= clen) break;  // this lane has no block here (nor later)
-        // advance over the 1008 bytes since this lane's previous block
-        if (base)
-          r = sh[0][r & 255u] ^ sh[1][(r >> 8) & 255u] ^ sh[2][(r >> 16) & 255u] ^ sh[3][r >> 24];
-        const uint32_t bl = clen - bs < 16u ? clen - bs : 16u;
-        if (bl == 16u) {
-          uint32_t w0, w1, w2, w3;
-          if (a16) {
-            const uint4 v = *(const uint4*)(p + bs);
-            w0 = v.x; w1 = v.y; w2 = v.z; w3 = v.w;
-          } else {
-            const uint8_t* q = p + bs;
-            uint32_t w[4];
-#pragma unroll
-            for (int j = 0; j < 4; ++j)
-              w[j] = (uint32_t)q[4 * j] | (uint32_t)q[4 * j + 1] << 8 |
-                     (uint32_t)q[4 * j + 2] << 16 | (uint32_t)q[4 * j + 3] << 24;
-            w0 = w[0]; w1 = w[1]; w2 = w[2]; w3 = w[3];
-          }
-          w0 ^= r;
-          r = t[15][w0 & 255u] ^ t[14][(w0 >> 8) & 255u] ^ t[13][(w0 >> 16) & 255u] ^ t[12][w0 >> 24] ^
-              t[11][w1 & 255u] ^ t[10][(w1 >> 8) & 255u] ^ t[9][(w1 >> 16) & 255u] ^ t[8][w1 >> 24] ^
-              t[7][w2 & 255u] ^ t[6][(w2 >> 8) & 255u] ^ t[5][(w2 >> 16) & 255u] ^ t[4][w2 >> 24] ^
-              t[3][w3 & 255u] ^ t[2][(w3 >> 8) & 255u] ^ t[1][(w3 >> 16) & 255u] ^ t[0][w3 >> 24];
-        } else {  // the segment's last, partial block
-          for (uint32_t j = 0; j < bl; ++j) r = t[0][(r ^ p[bs + j]) & 255u] ^ (r >> 8);
-        }
-        last = bs + bl;
-      }
-      // shift over the bytes after this lane's last block (< 1024), reduce
-      uint32_t v = last ? mulmodp(x8[clen - last], r) : 0u;
-#pragma unroll
-      for (int d = 32; d >= 1; d >>= 1) v ^= (uint32_t)__shfl_xor((int)v, d, 64);
-      acc ^= shift_bytes(v, len - cb - clen);
+      acc ^= shift_bytes(chunk_raw(data + b0 + cb, clen, lane, t, sh, x8), len - cb - clen);
     }
     if (lane == 0) {
       // ~(raw ^ (~init) x^(8 len)): the init term and the final inversion
@@ -170,7 +177,33 @@ __global__ __launch_bounds__(kNT) void crc_kernel(const uint8_t* __restrict__ da
   }
 }
 
+// the key signature check of a message that carries keys (cacheKeyRecver,
+// remote_node.cc:161-163): crc32c::Value of the first min(len, max) bytes
+// against the carried signature; a mismatch counts into *bad (reported by
+// psg_received), so the host does not wait for it.  One wave.
+__global__ __launch_bounds__(64) void sig_kernel(const uint8_t* __restrict__ data, uint32_t len,
+                                                 uint32_t want, unsigned long long* bad) {
+  __shared__ uint32_t t[16][256];
+  __shared__ uint32_t sh[4][256];
+  __shared__ uint32_t x8[1024];
+  for (int i = threadIdx.x; i < 16 * 256; i += 64) (&t[0][0])[i] = (&kTab.t[0][0])[i];
+  for (int i = threadIdx.x; i < 4 * 256; i += 64) (&sh[0][0])[i] = (&kTab.sh[0][0])[i];
+  for (int i = threadIdx.x; i < 1024; i += 64) x8[i] = kTab.x8[i];
+  __syncthreads();
+  const uint32_t raw = chunk_raw(data, len, threadIdx.x, t, sh, x8);
+  const uint32_t got = raw ^ ~shift_bytes(~0u, len);  // Extend(0, data, len)
+  if (threadIdx.x == 0 && got != want) atomicAdd(bad, 1ull);
+}
+
 }  // namespace
+
+hipError_t launch_sig_check(const uint8_t* data, uint64_t len, uint64_t max_len, uint32_t want,
+                            unsigned long long* bad, hipStream_t s) {
+  const uint64_t l = len < max_len ? len : max_len;
+  if (l > kChunk) return hipErrorInvalidValue;
+  hipLaunchKernelGGL(sig_kernel, dim3(1), dim3(64), 0, s, data, (uint32_t)l, want, bad);
+  return hipGetLastError();
+}
 
 // items per segment: one per 64 KB chunk up to kMaxPer (an item then takes
 // every kMaxPer-th chunk), so any max_len gives a bounded grid

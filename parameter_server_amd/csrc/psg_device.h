@@ -40,6 +40,49 @@ __device__ __forceinline__ uint64_t wave_search(const uint64_t* __restrict__ S,
   return lo;
 }
 
+// lower_bound(S, xl) inside a bracket with S[a] < xl <= S[c]: interpolation
+// probes (pushes of murmur-hashed keys are near-uniform), bisection, then
+// the last <= 15 candidates in one round trip.  One lane per search.
+__device__ __forceinline__ uint64_t bracket_lower_bound(const uint64_t* S, uint64_t xl,
+                                                        uint64_t a, uint64_t c, uint64_t ka,
+                                                        uint64_t kc) {
+  for (int it = 0; it < 6 && c - a > 16u; ++it) {
+    const double f = (double)(xl - ka) / (double)(kc - ka);
+    uint64_t mid = a + 1 + (uint64_t)(f * (double)(c - a - 1));
+    mid = mid < c ? mid : c - 1;
+    const uint64_t km = S[mid];
+    if (km < xl) {
+      a = mid;
+      ka = km;
+    } else {
+      c = mid;
+      kc = km;
+    }
+  }
+  while (c - a > 16u) {
+    const uint64_t mid = a + ((c - a) >> 1);
+    if (S[mid] < xl) a = mid; else c = mid;
+  }
+  // independent loads of S[a+1 .. c-1] (indices clamped to c, where
+  // S[c] >= xl counts 0)
+  uint32_t below = 0;
+#pragma unroll
+  for (uint32_t i = 1; i < 16u; ++i) {
+    const uint64_t idx = a + i < c ? a + i : c;
+    below += S[idx] < xl ? 1u : 0u;
+  }
+  return a + 1u + below;
+}
+
+// lower_bound(S[0, n), x) by bracket_lower_bound: in [0, n] whatever S holds
+__device__ __forceinline__ uint64_t interp_lower_bound(const uint64_t* S, uint64_t n, uint64_t x) {
+  if (n == 0) return 0;
+  const uint64_t k0 = S[0], kn = S[n - 1];
+  if (x <= k0) return 0;
+  if (x > kn) return n;
+  return bracket_lower_bound(S, x, 0, n - 1, k0, kn);
+}
+
 // lower_bound over a sorted LDS array of n <= 2*TILE-1 keys: fixed trip
 // count (log2(TILE)+1 probes), so the wave never diverges on the loop.
 template <int TILE>

@@ -22,6 +22,7 @@ constexpr int kWideSlots = 2048;
 
 constexpr uint32_t kFlagParallel = 1u;  // PSG_PARALLEL_MATCH
 constexpr uint32_t kFlagCont = 2u;      // continue an aggregate of an earlier launch
+constexpr uint32_t kFlagLastTile = 4u;  // TileDesc: the job's last tile
 
 // How the partition finds a job's (push, tile) pieces:
 // kSearch: one lane per (push, tile boundary), interpolation search -- cost
@@ -132,8 +133,14 @@ uint32_t bucket_index_words(uint32_t tile_slots);
 hipError_t launch_bucket_index(const TileDesc* d_tiles, uint32_t ntiles, uint32_t tile_slots,
                                uint32_t* out,
                                hipStream_t stream);
+// cursor form (d_chunks non-null): one workgroup per chunk of consecutive
+// tiles (t0, t1 index d_tiles), boundary words (nchunks + 1) x kPackCursorPushes
+// u32, zeroed before each run
+constexpr int kPackCursorPushes = 256;
 hipError_t launch_aggregate_tile_packed(int dtype, int m, const TileDesc* d_tiles,
-                                        uint32_t ntiles, hipStream_t stream);
+                                        uint32_t ntiles, hipStream_t stream,
+                                        const CursorChunk* d_chunks = nullptr,
+                                        uint32_t nchunks = 0, uint32_t* bx = nullptr);
 // psg_tile_dense.hip: every push of every job a contiguous slice of D
 hipError_t launch_aggregate_dense(int dtype, int m, const TileDesc* d_tiles, uint32_t ntiles,
                                   hipStream_t stream);
@@ -231,5 +238,9 @@ uint64_t crc32c_chunks_per_segment(uint64_t max_len);
 hipError_t launch_crc32c(const uint8_t* data, const uint64_t* off, uint64_t nseg,
                          uint64_t max_len, const uint32_t* init, uint32_t* out,
                          hipStream_t stream);
+// *bad += 1 unless crc32c::Value(data, min(len, max_len)) == want (one
+// wave; max_len <= 64 KB)
+hipError_t launch_sig_check(const uint8_t* data, uint64_t len, uint64_t max_len, uint32_t want,
+                            unsigned long long* bad, hipStream_t stream);
 
 }  // namespace psg

@@ -60,22 +60,6 @@ constexpr int kMaxRuns = 64;        // pushes per merge (runs per tile)
 
 __device__ __forceinline__ uint32_t uni(uint32_t v) { return __builtin_amdgcn_readfirstlane(v); }
 
-// lower_bound over a sorted global array
-__device__ __forceinline__ uint64_t lb_global(const uint64_t* __restrict__ a, uint64_t n,
-                                              uint64_t k) {
-  uint64_t lo = 0, len = n;
-  while (len > 0) {
-    const uint64_t half = len >> 1;
-    if (a[lo + half] < k) {
-      lo += half + 1;
-      len -= half + 1;
-    } else {
-      len = half;
-    }
-  }
-  return lo;
-}
-
 struct NwArgs {
   const uint64_t* const* keys;  // [K] push keys
   const void* const* vals;      // [K * M] push values (M > 0)
@@ -85,7 +69,6 @@ struct NwArgs {
   uint64_t* split;              // [B] splitter keys
   uint32_t* seg;                // [(T + 1) * K] piece starts, tile-major
   unsigned long long* state;    // [T] look-back words
-  unsigned int* ticket;         // tile tickets
   unsigned long long* bad;      // order violations / overflow
   unsigned long long* nout;     // merged key count
   uint64_t* out_keys;
@@ -95,36 +78,90 @@ struct NwArgs {
   uint32_t flags;
 };
 
-// 1. R(c) for every candidate c: one thread per (candidate, push)
-__global__ __launch_bounds__(256) void nw_cand_kernel(NwArgs a) {
-  const uint64_t id = (uint64_t)blockIdx.x * 256u + threadIdx.x;
-  if (id >= a.ncand * a.K) return;
-  const uint64_t c = id / a.K;
-  const uint32_t r = (uint32_t)(id - c * a.K);
-  // the push that owns candidate c (K <= 64: linear)
-  uint32_t q = 0;
-  while (q + 1 < a.K && a.cbase[q + 1] <= c) ++q;
-  const uint64_t key = a.keys[q][(c - a.cbase[q]) * a.s + a.s - 1];
-  const uint64_t l = lb_global(a.keys[r], a.n[r], key);
-  atomicAdd(a.rank + c, (uint32_t)l);
+// A batch of independent merges (psg_nway_create_batch: e.g. the 64
+// aggregates of a bench step) runs as ONE pipeline: each stage is one launch
+// over the work items of every merge, which find their merge by a binary
+// search over the stage's prefix counts.  The tile stage deals tiles by a
+// global ticket, so a tile's look-back only waits on tiles of its merge
+// that are already running.
+struct NwBatch {
+  const NwArgs* args;       // [nm]
+  const uint64_t* wpre;     // [nm + 1] candidate waves before merge j
+  const uint64_t* cpre;     // [nm + 1] candidates before merge j
+  const uint64_t* spre;     // [nm + 1] seg entries ((T + 1) K) before merge j
+  const uint64_t* tpre;     // [nm + 1] tiles before merge j
+  unsigned int* ticket;     // tile tickets
+  uint32_t nm;
+};
+
+// merge j of item x: the last j with pre[j] <= x (pre non-decreasing)
+__device__ __forceinline__ uint32_t merge_of(const uint64_t* pre, uint32_t nm, uint64_t x) {
+  uint32_t lo = 0, hi = nm;  // pre[lo] <= x < pre[hi]
+  while (hi - lo > 1) {
+    const uint32_t mid = (lo + hi) >> 1;
+    if (pre[mid] <= x) lo = mid; else hi = mid;
+  }
+  return lo;
+}
+
+// the push owning candidate c: the last q with cbase[q] <= c
+__device__ __forceinline__ uint32_t owner(const NwArgs& a, uint64_t c) {
+  uint32_t lo = 0, hi = a.K;
+  while (hi - lo > 1) {
+    const uint32_t mid = (lo + hi) >> 1;
+    if (a.cbase[mid] <= c) lo = mid; else hi = mid;
+  }
+  return lo;
+}
+
+// lanes per candidate in the rank stage: K rounded up to a power of two
+__host__ __device__ __forceinline__ uint32_t cand_lanes(uint32_t K) {
+  uint32_t p = 1;
+  while (p < K) p <<= 1;
+  return p;
+}
+
+// 1. R(c) for every candidate c: a wave holds 64 / kp candidates, lane r of
+// a candidate's kp lanes takes lower_bound(push r, c) (interpolation probes,
+// the pushes being near-uniform hashed keys, then a bisection: any key
+// distribution is exact), and the kp lanes sum them: no atomics
+__global__ __launch_bounds__(256) void nw_cand_kernel(NwBatch b, uint64_t nwaves) {
+  const uint64_t wv = ((uint64_t)blockIdx.x * 256u + threadIdx.x) >> 6;
+  if (wv >= nwaves) return;
+  const uint32_t j = uni(merge_of(b.wpre, b.nm, wv));
+  const NwArgs& a = b.args[j];
+  const uint32_t K = a.K, kp = cand_lanes(K), lane = threadIdx.x & 63u;
+  const uint64_t c = (wv - b.wpre[j]) * (64u / kp) + lane / kp;
+  const uint32_t r = lane % kp;
+  uint32_t l = 0;
+  if (c < a.ncand && r < K) {
+    const uint32_t q = owner(a, c);
+    const uint64_t key = a.keys[q][(c - a.cbase[q]) * a.s + a.s - 1];
+    l = (uint32_t)dev::interp_lower_bound(a.keys[r], a.n[r], key);
+  }
+  for (uint32_t d = 1; d < kp; d <<= 1) l += (uint32_t)__shfl_xor((int)l, (int)d, 64);
+  if (c < a.ncand && r == 0) a.rank[c] = l;
 }
 
 // 2. splitter of bucket floor(R / C') = its largest candidate key
-__global__ __launch_bounds__(256) void nw_bucket_kernel(NwArgs a) {
-  const uint64_t c = (uint64_t)blockIdx.x * 256u + threadIdx.x;
-  if (c >= a.ncand) return;
-  uint32_t q = 0;
-  while (q + 1 < a.K && a.cbase[q + 1] <= c) ++q;
+__global__ __launch_bounds__(256) void nw_bucket_kernel(NwBatch b, uint64_t ncand) {
+  const uint64_t g = (uint64_t)blockIdx.x * 256u + threadIdx.x;
+  if (g >= ncand) return;
+  const uint32_t j = merge_of(b.cpre, b.nm, g);
+  const NwArgs& a = b.args[j];
+  const uint64_t c = g - b.cpre[j];
+  const uint32_t q = owner(a, c);
   const uint64_t key = a.keys[q][(c - a.cbase[q]) * a.s + a.s - 1];
-  const uint32_t b = a.rank[c] / a.cw;
-  if (b < a.B) atomicMax((unsigned long long*)a.split + b, (unsigned long long)key);
+  const uint32_t bk = a.rank[c] / a.cw;
+  if (bk < a.B) atomicMax((unsigned long long*)a.split + bk, (unsigned long long)key);
 }
 
-// 3. prefix max (one workgroup): splitters non-decreasing, empty buckets
-// repeat the previous splitter (an empty tile)
-__global__ __launch_bounds__(256) void nw_split_kernel(NwArgs a) {
+// 3. prefix max (one workgroup per merge): splitters non-decreasing, empty
+// buckets repeat the previous splitter (an empty tile)
+__global__ __launch_bounds__(256) void nw_split_kernel(NwBatch bt) {
   __shared__ uint64_t wmax[4];
   __shared__ uint64_t carry;
+  const NwArgs& a = bt.args[blockIdx.x];
   if (threadIdx.x == 0) carry = 0;
   __syncthreads();
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
@@ -150,15 +187,17 @@ __global__ __launch_bounds__(256) void nw_split_kernel(NwArgs a) {
 
 // 4. seg[t * K + q] = first index of push q in tile t: 0 (t = 0),
 // lower_bound(push q, split[t - 1]) (0 < t < T), n_q (t = T)
-__global__ __launch_bounds__(256) void nw_seg_kernel(NwArgs a) {
-  const uint64_t id = (uint64_t)blockIdx.x * 256u + threadIdx.x;
-  const uint64_t tot = (uint64_t)(a.T + 1) * a.K;
-  if (id >= tot) return;
+__global__ __launch_bounds__(256) void nw_seg_kernel(NwBatch b, uint64_t nseg) {
+  const uint64_t g = (uint64_t)blockIdx.x * 256u + threadIdx.x;
+  if (g >= nseg) return;
+  const uint32_t j = merge_of(b.spre, b.nm, g);
+  const NwArgs& a = b.args[j];
+  const uint64_t id = g - b.spre[j];
   const uint32_t t = (uint32_t)(id / a.K), q = (uint32_t)(id - (uint64_t)t * a.K);
   uint64_t v;
   if (t == 0) v = 0;
   else if (t == a.T) v = a.n[q];
-  else v = lb_global(a.keys[q], a.n[q], a.split[t - 1]);
+  else v = dev::interp_lower_bound(a.keys[q], a.n[q], a.split[t - 1]);
   a.seg[id] = (uint32_t)v;
 }
 
@@ -167,7 +206,7 @@ constexpr uint64_t kValMask = (1ull << 62) - 1;
 
 // 5. the tile merge
 template <typename V, int M>
-__global__ __launch_bounds__(kNT) void nw_tile_kernel(NwArgs a) {
+__global__ __launch_bounds__(kNT) void nw_tile_kernel(NwBatch bt) {
   constexpr int kM = M > 0 ? M : 1;
   constexpr int kVC = M > 0 ? kCap : 1;
   __shared__ __attribute__((aligned(16))) uint64_t sk[kCap];  // keys (merged in place)
@@ -179,17 +218,20 @@ __global__ __launch_bounds__(kNT) void nw_tile_kernel(NwArgs a) {
   __shared__ uint32_t sh_t, sh_err;
   __shared__ unsigned long long sh_base;
   const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
-  const uint32_t K = a.K;
-  const bool parallel = (a.flags & kFlagParallel) != 0;
 
   // ---- ticket: tiles in dispatch order (the look-back waits only on
-  // tickets taken by workgroups that are already running)
+  // tickets taken by workgroups that are already running), then its merge
   if (tid == 0) {
-    sh_t = atomicAdd(a.ticket, 1u);
+    sh_t = atomicAdd(bt.ticket, 1u);
     sh_err = 0;
   }
   __syncthreads();
-  const uint32_t t = sh_t;
+  const uint32_t g = uni(sh_t);
+  const uint32_t jm = uni(merge_of(bt.tpre, bt.nm, g));
+  const NwArgs& a = bt.args[jm];
+  const uint32_t t = (uint32_t)(g - bt.tpre[jm]);
+  const uint32_t K = a.K;
+  const bool parallel = (a.flags & kFlagParallel) != 0;
 
   // ---- piece table: wave 0, one lane per push
   if (w == 0) {
@@ -432,19 +474,19 @@ __global__ __launch_bounds__(kNT) void nw_tile_kernel(NwArgs a) {
 }
 
 template <typename V, int M>
-hipError_t launch_tile(const NwArgs& a, hipStream_t s) {
-  hipLaunchKernelGGL((nw_tile_kernel<V, M>), dim3(a.T), dim3(kNT), 0, s, a);
+hipError_t launch_tile(const NwBatch& b, uint64_t tiles, hipStream_t s) {
+  hipLaunchKernelGGL((nw_tile_kernel<V, M>), dim3((uint32_t)tiles), dim3(kNT), 0, s, b);
   return hipGetLastError();
 }
 
 template <typename V>
-hipError_t launch_tile_m(int m, const NwArgs& a, hipStream_t s) {
+hipError_t launch_tile_m(int m, const NwBatch& b, uint64_t tiles, hipStream_t s) {
   switch (m) {
-    case 0: return launch_tile<V, 0>(a, s);
-    case 1: return launch_tile<V, 1>(a, s);
-    case 2: return launch_tile<V, 2>(a, s);
-    case 3: return launch_tile<V, 3>(a, s);
-    case 4: return launch_tile<V, 4>(a, s);
+    case 0: return launch_tile<V, 0>(b, tiles, s);
+    case 1: return launch_tile<V, 1>(b, tiles, s);
+    case 2: return launch_tile<V, 2>(b, tiles, s);
+    case 3: return launch_tile<V, 3>(b, tiles, s);
+    case 4: return launch_tile<V, 4>(b, tiles, s);
     default: return hipErrorInvalidValue;
   }
 }
@@ -453,20 +495,16 @@ size_t al256(size_t x) { return (x + 255) / 256 * 256; }
 
 }  // namespace
 
-// Layout of one merge's device scratch (tables, per-run cleared region,
-// piece starts) for K non-empty pushes of ntot keys, m value arrays.
-struct NwLayout {
+// One merge's shape: sample stride s and bucket width C' (header: a tile
+// holds <= C' + K s + K elements), candidates, buckets, tiles.
+struct NwShape {
   uint32_t K = 0, s = 1, cw = 1, B = 1, T = 2;
   uint64_t ncand = 0;
-  size_t o_k = 0, o_v = 0, o_n = 0, o_cb = 0, o_ov = 0, o_zero = 0, o_rank = 0, o_split = 0,
-         o_state = 0, o_misc = 0, zero_len = 0, o_seg = 0, bytes = 0;
   std::vector<uint64_t> cbase;
-
-  void plan(uint32_t k, const uint64_t* pn, int m) {
+  void plan(uint32_t k, const uint64_t* pn) {
     K = k;
     uint64_t ntot = 0;
     for (uint32_t q = 0; q < K; ++q) ntot += pn[q];
-    // sample stride s and bucket width C' (header: a tile holds <= C' + K s)
     s = K <= 16 ? std::max<uint32_t>(1, kCap / (8 * std::max<uint32_t>(K, 1))) : 16u;
     cw = kCap - K * s - K;
     cbase.assign(K + 1, 0);
@@ -474,79 +512,156 @@ struct NwLayout {
     ncand = cbase[K];
     B = (uint32_t)(ntot / cw + 1);
     T = B + 1;
-    size_t off = 0;
-    o_k = off; off = al256(off + 8 * K);
-    o_v = off; off = al256(off + 8 * (size_t)K * m);
-    o_n = off; off = al256(off + 8 * K);
-    o_cb = off; off = al256(off + 8 * (K + 1));
-    o_ov = off; off = al256(off + 8 * (size_t)std::max(m, 1));
-    o_zero = off;
-    o_rank = off; off = al256(off + 4 * ncand);
-    o_split = off; off = al256(off + 8 * (size_t)B);
-    o_state = off; off = al256(off + 8 * (size_t)T);
-    o_misc = off; off = al256(off + 32);  // ticket, bad, nout
-    zero_len = off - o_zero;
-    o_seg = off; off = al256(off + 4 * (size_t)(T + 1) * K);
-    bytes = off;
+  }
+  uint64_t waves() const { return (ncand + 64 / cand_lanes(K) - 1) / (64 / cand_lanes(K)); }
+};
+
+// Device scratch of a batch of nm merges: [tables: per merge key / value /
+// length / candidate-base / output pointer arrays; NwArgs[nm]; prefix
+// counts][zeroed per run: per merge rank, splitters, look-back words; the
+// ticket; per merge (bad, nout)][per merge piece starts].  The tables are
+// written once (upload); a run clears one region and enqueues 5 launches.
+struct NwLayout {
+  uint32_t nm = 0;
+  int m = 0;
+  std::vector<NwShape> sh;
+  struct Off { size_t k, v, n, cb, ov, rank, split, state, seg; };
+  std::vector<Off> off;
+  size_t o_args = 0, o_pre = 0, o_zero = 0, o_ticket = 0, o_misc = 0, zero_len = 0, bytes = 0;
+  uint64_t nwaves = 0, ncand = 0, nseg = 0, ntiles = 0;
+
+  // pn: the merges' push lengths back to back, npush[j] per merge
+  void plan(uint32_t nmerge, const uint32_t* npush, const uint64_t* pn, int mm) {
+    nm = nmerge;
+    m = mm;
+    sh.assign(nm, NwShape{});
+    off.assign(nm, Off{});
+    size_t o = 0, pcur = 0;
+    for (uint32_t j = 0; j < nm; ++j) {
+      sh[j].plan(npush[j], pn + pcur);
+      pcur += npush[j];
+      const uint32_t K = npush[j];
+      Off& f = off[j];
+      f.k = o; o = al256(o + 8 * (size_t)K);
+      f.v = o; o = al256(o + 8 * (size_t)K * m);
+      f.n = o; o = al256(o + 8 * (size_t)K);
+      f.cb = o; o = al256(o + 8 * (size_t)(K + 1));
+      f.ov = o; o = al256(o + 8 * (size_t)std::max(m, 1));
+    }
+    o_args = o; o = al256(o + sizeof(NwArgs) * (size_t)nm);
+    o_pre = o; o = al256(o + 8 * 4 * (size_t)(nm + 1));
+    o_zero = o;
+    for (uint32_t j = 0; j < nm; ++j) {
+      Off& f = off[j];
+      f.rank = o; o = al256(o + 4 * sh[j].ncand);
+      f.split = o; o = al256(o + 8 * (size_t)sh[j].B);
+      f.state = o; o = al256(o + 8 * (size_t)sh[j].T);
+    }
+    o_ticket = o; o = al256(o + 8);
+    o_misc = o; o = al256(o + 16 * (size_t)nm);  // per merge: bad, nout
+    zero_len = o - o_zero;
+    for (uint32_t j = 0; j < nm; ++j) {
+      off[j].seg = o;
+      o = al256(o + 4 * (size_t)(sh[j].T + 1) * sh[j].K);
+    }
+    bytes = o;
+    nwaves = ncand = nseg = ntiles = 0;
+    for (const NwShape& x : sh) {
+      nwaves += x.waves();
+      ncand += x.ncand;
+      nseg += (uint64_t)(x.T + 1) * x.K;
+      ntiles += x.T;
+    }
   }
 
-  NwArgs args(char* b, uint64_t* out_keys, uint32_t flags) const {
-    NwArgs A{};
-    A.keys = (const uint64_t* const*)(b + o_k);
-    A.vals = (const void* const*)(b + o_v);
-    A.n = (const uint64_t*)(b + o_n);
-    A.cbase = (const uint64_t*)(b + o_cb);
-    A.out_vals = (void* const*)(b + o_ov);
-    A.rank = (uint32_t*)(b + o_rank);
-    A.split = (uint64_t*)(b + o_split);
-    A.state = (unsigned long long*)(b + o_state);
-    A.ticket = (unsigned int*)(b + o_misc);
-    A.bad = (unsigned long long*)(b + o_misc + 8);
-    A.nout = (unsigned long long*)(b + o_misc + 16);
-    A.seg = (uint32_t*)(b + o_seg);
-    A.out_keys = out_keys;
-    A.ncand = ncand;
-    A.K = K;
-    A.B = B;
-    A.T = T;
-    A.s = s;
-    A.cw = cw;
-    A.flags = flags;
-    return A;
+  unsigned long long* misc(char* b, uint32_t j) const {
+    return (unsigned long long*)(b + o_misc) + 2 * (size_t)j;
   }
 
-  // the tables (pointer arrays, lengths, candidate bases) into the scratch
-  hipError_t upload(char* b, const uint64_t* const* pk, const void* const* pv, const uint64_t* pn,
-                    const void* const* ov, int m, hipStream_t st, bool sync) const {
-    std::vector<char> h(o_zero);
-    if (K) memcpy(h.data() + o_k, pk, 8 * K);
-    if (K && m) memcpy(h.data() + o_v, pv, 8 * (size_t)K * m);
-    if (K) memcpy(h.data() + o_n, pn, 8 * K);
-    memcpy(h.data() + o_cb, cbase.data(), 8 * (K + 1));
-    if (m) memcpy(h.data() + o_ov, ov, 8 * (size_t)m);
+  NwBatch batch(char* b) const {
+    NwBatch B{};
+    B.args = (const NwArgs*)(b + o_args);
+    const uint64_t* pre = (const uint64_t*)(b + o_pre);
+    B.wpre = pre;
+    B.cpre = pre + (nm + 1);
+    B.spre = pre + 2 * (size_t)(nm + 1);
+    B.tpre = pre + 3 * (size_t)(nm + 1);
+    B.ticket = (unsigned int*)(b + o_ticket);
+    B.nm = nm;
+    return B;
+  }
+
+  // the tables into the scratch b (one copy on st; synchronous: the host
+  // image is freed on return).  Arrays as plan(): pk / pn / pv back to back
+  // over the merges, out_keys[j], out_vals[j * m + i].
+  hipError_t upload(char* b, const uint64_t* const* pk, const void* const* pv,
+                    const uint64_t* pn, uint64_t* const* out_keys, const void* const* ov,
+                    uint32_t flags, hipStream_t st) const {
+    std::vector<char> h(o_zero, 0);
+    std::vector<NwArgs> args(nm);
+    std::vector<uint64_t> pre(4 * (size_t)(nm + 1), 0);
+    size_t pcur = 0;
+    for (uint32_t j = 0; j < nm; ++j) {
+      const NwShape& x = sh[j];
+      const Off& f = off[j];
+      const uint32_t K = x.K;
+      if (K) memcpy(h.data() + f.k, pk + pcur, 8 * (size_t)K);
+      if (K && m) memcpy(h.data() + f.v, pv + pcur * m, 8 * (size_t)K * m);
+      if (K) memcpy(h.data() + f.n, pn + pcur, 8 * (size_t)K);
+      memcpy(h.data() + f.cb, x.cbase.data(), 8 * (size_t)(K + 1));
+      if (m) memcpy(h.data() + f.ov, ov + (size_t)j * m, 8 * (size_t)m);
+      pcur += K;
+      NwArgs& A = args[j];
+      A.keys = (const uint64_t* const*)(b + f.k);
+      A.vals = (const void* const*)(b + f.v);
+      A.n = (const uint64_t*)(b + f.n);
+      A.cbase = (const uint64_t*)(b + f.cb);
+      A.out_vals = (void* const*)(b + f.ov);
+      A.rank = (uint32_t*)(b + f.rank);
+      A.split = (uint64_t*)(b + f.split);
+      A.state = (unsigned long long*)(b + f.state);
+      A.bad = misc(b, j);
+      A.nout = misc(b, j) + 1;
+      A.seg = (uint32_t*)(b + f.seg);
+      A.out_keys = out_keys[j];
+      A.ncand = x.ncand;
+      A.K = K;
+      A.B = x.B;
+      A.T = x.T;
+      A.s = x.s;
+      A.cw = x.cw;
+      A.flags = flags;
+      pre[j + 1] = pre[j] + x.waves();
+      pre[(nm + 1) + j + 1] = pre[(nm + 1) + j] + x.ncand;
+      pre[2 * (nm + 1) + j + 1] = pre[2 * (nm + 1) + j] + (uint64_t)(x.T + 1) * K;
+      pre[3 * (nm + 1) + j + 1] = pre[3 * (nm + 1) + j] + x.T;
+    }
+    memcpy(h.data() + o_args, args.data(), sizeof(NwArgs) * nm);
+    memcpy(h.data() + o_pre, pre.data(), 8 * pre.size());
     hipError_t e = hipMemcpyAsync(b, h.data(), o_zero, hipMemcpyHostToDevice, st);
-    // the host vector is freed on return: wait for the copy
     if (e == hipSuccess) e = hipStreamSynchronize(st);
-    (void)sync;
     return e;
   }
 };
 
-hipError_t nway_enqueue(const NwArgs& A, char* b, const NwLayout& L, int dtype, int m,
-                        hipStream_t st) {
+// one run of the batch: clear, then the 5 stages, each one launch over every
+// merge (merges of no pushes have no work items; their count stays 0)
+hipError_t nway_enqueue(char* b, const NwLayout& L, int dtype, hipStream_t st) {
   hipError_t e = hipMemsetAsync(b + L.o_zero, 0, L.zero_len, st);
-  if (e != hipSuccess || A.K == 0) return e;
-  if (A.ncand) {
-    const uint64_t th = A.ncand * A.K;
-    hipLaunchKernelGGL(nw_cand_kernel, dim3((uint32_t)((th + 255) / 256)), dim3(256), 0, st, A);
-    hipLaunchKernelGGL(nw_bucket_kernel, dim3((uint32_t)((A.ncand + 255) / 256)), dim3(256), 0, st,
-                       A);
+  if (e != hipSuccess || L.ntiles == 0) return e;
+  const NwBatch B = L.batch(b);
+  if (L.ncand) {
+    hipLaunchKernelGGL(nw_cand_kernel, dim3((uint32_t)((L.nwaves + 3) / 4)), dim3(256), 0, st, B,
+                       L.nwaves);
+    hipLaunchKernelGGL(nw_bucket_kernel, dim3((uint32_t)((L.ncand + 255) / 256)), dim3(256), 0, st,
+                       B, L.ncand);
   }
-  hipLaunchKernelGGL(nw_split_kernel, dim3(1), dim3(256), 0, st, A);
-  const uint64_t ns = (uint64_t)(A.T + 1) * A.K;
-  hipLaunchKernelGGL(nw_seg_kernel, dim3((uint32_t)((ns + 255) / 256)), dim3(256), 0, st, A);
+  hipLaunchKernelGGL(nw_split_kernel, dim3(L.nm), dim3(256), 0, st, B);
+  hipLaunchKernelGGL(nw_seg_kernel, dim3((uint32_t)((L.nseg + 255) / 256)), dim3(256), 0, st, B,
+                     L.nseg);
   if ((e = hipGetLastError()) != hipSuccess) return e;
-  return dtype == PSG_F32 ? launch_tile_m<float>(m, A, st) : launch_tile_m<double>(m, A, st);
+  return dtype == PSG_F32 ? launch_tile_m<float>(L.m, B, L.ntiles, st)
+                          : launch_tile_m<double>(L.m, B, L.ntiles, st);
 }
 
 // One keys-only union on `st` into out_keys (>= sum(n) entries), scratch
@@ -554,7 +669,7 @@ hipError_t nway_enqueue(const NwArgs& A, char* b, const NwLayout& L, int dtype, 
 // (psg_key_union*).  *d_bad / *d_nout: the device words psg_nway_result reads.
 size_t nway_scratch_bytes(uint32_t K, const uint64_t* pn) {
   NwLayout L;
-  L.plan(K, pn, 0);
+  L.plan(1, &K, pn, 0);
   return L.bytes;
 }
 
@@ -562,13 +677,13 @@ hipError_t nway_union_enqueue(uint32_t K, const uint64_t* const* pk, const uint6
                               uint64_t* out_keys, void* scratch, unsigned long long** d_bad,
                               hipStream_t st) {
   NwLayout L;
-  L.plan(K, pn, 0);
+  L.plan(1, &K, pn, 0);
   char* b = (char*)scratch;
-  hipError_t e = L.upload(b, pk, nullptr, pn, nullptr, 0, st, true);
+  uint64_t* ok[1] = {out_keys};
+  hipError_t e = L.upload(b, pk, nullptr, pn, ok, nullptr, 0, st);
   if (e != hipSuccess) return e;
-  const NwArgs A = L.args(b, out_keys, 0);
-  *d_bad = A.bad;  // [bad, nout]
-  return nway_enqueue(A, b, L, PSG_F32, 0, st);
+  *d_bad = L.misc(b, 0);  // [bad, nout]
+  return nway_enqueue(b, L, PSG_F32, st);
 }
 
 }  // namespace psg
@@ -577,13 +692,90 @@ using psg::fail;
 
 struct psg_nway {
   int device = 0, dtype = 0, m = 0;
+  uint32_t nm = 0;
   uint64_t ntot = 0;              // keys over all pushes
   uint64_t bytes = 0;             // algorithmic bytes read by a run
   void* blob = nullptr;
   psg::NwLayout layout;
-  psg::NwArgs args{};
   hipStream_t last = nullptr;
 };
+
+namespace {
+
+int nway_create(int device, int dtype, int m, unsigned flags, int nmerge, const int* npush,
+                const uint64_t* const* keys, const uint64_t* n, const void* const* vals,
+                uint64_t* const* out_keys, void* const* out_vals, psg_nway** out) {
+  using namespace psg;
+  if (!out || nmerge < 1 || !npush || !out_keys) return fail(PSG_ERR_ARG, "null argument");
+  if (dtype != PSG_F32 && dtype != PSG_F64) return fail(PSG_ERR_ARG, "dtype %d", dtype);
+  if (m < 0 || m > PSG_MAX_VALUE_ARRAYS || (m > 0 && !out_vals))
+    return fail(PSG_ERR_ARG, "m=%d", m);
+  size_t tot_push = 0;
+  for (int j = 0; j < nmerge; ++j) {
+    if (npush[j] < 0) return fail(PSG_ERR_ARG, "merge %d: %d pushes", j, npush[j]);
+    if (!out_keys[j]) return fail(PSG_ERR_ARG, "merge %d: null out_keys", j);
+    for (int i = 0; i < m; ++i)
+      if (!out_vals[(size_t)j * m + i]) return fail(PSG_ERR_ARG, "merge %d: null out_vals", j);
+    tot_push += (size_t)npush[j];
+  }
+  if (tot_push && (!keys || !n || (m > 0 && !vals))) return fail(PSG_ERR_ARG, "null argument");
+  HIP_TRY(hipSetDevice(device));
+  // empty pushes are ignored (kv_vector.h:90,177): push 0 of a merge is its
+  // first non-empty one
+  std::vector<const uint64_t*> pk;
+  std::vector<const void*> pv;
+  std::vector<uint64_t> pn;
+  std::vector<uint32_t> kept(nmerge, 0);
+  uint64_t ntot = 0;
+  size_t p = 0;
+  for (int j = 0; j < nmerge; ++j) {
+    uint64_t mt = 0;
+    for (int e = 0; e < npush[j]; ++e, ++p) {
+      if (n[p] == 0) continue;
+      if (!keys[p]) return fail(PSG_ERR_ARG, "merge %d push %d: null keys", j, e);
+      pk.push_back(keys[p]);
+      for (int i = 0; i < m; ++i) {
+        if (!vals[p * m + i]) return fail(PSG_ERR_ARG, "merge %d push %d: null values", j, e);
+        pv.push_back(vals[p * m + i]);
+      }
+      pn.push_back(n[p]);
+      ++kept[j];
+      mt += n[p];
+    }
+    if (kept[j] > (uint32_t)kMaxRuns)
+      return fail(PSG_ERR_ARG, "merge %d: %u pushes > %d per merge", j, kept[j], kMaxRuns);
+    if (mt >= (1ull << 32))
+      return fail(PSG_ERR_ARG, "merge %d: %llu keys >= 2^32", j, (unsigned long long)mt);
+    ntot += mt;
+  }
+  psg_nway* u = new psg_nway();
+  u->device = device;
+  u->dtype = dtype;
+  u->m = m;
+  u->nm = (uint32_t)nmerge;
+  u->ntot = ntot;
+  u->layout.plan((uint32_t)nmerge, kept.data(), pn.data(), m);
+  if (hipMalloc(&u->blob, u->layout.bytes) != hipSuccess) {
+    const size_t want = u->layout.bytes;
+    delete u;
+    return fail(PSG_ERR_OOM, "nway: %zu bytes", want);
+  }
+  const hipError_t e = u->layout.upload(
+      (char*)u->blob, pk.data(), pv.data(), pn.data(), out_keys, (const void* const*)out_vals,
+      (flags & PSG_PARALLEL_MATCH) ? kFlagParallel : 0u, nullptr);
+  if (e != hipSuccess) {
+    (void)hipFree(u->blob);
+    delete u;
+    return fail(PSG_ERR_DEVICE, "nway set-up: %s", hipGetErrorString(e));
+  }
+  // SURVEY 8d general form, the read side: every push's keys and values
+  // (the merged output adds |union| * (8 + m s_V), known after a run)
+  u->bytes = ntot * (8 + (uint64_t)m * (dtype == PSG_F32 ? 4 : 8));
+  *out = u;
+  return PSG_OK;
+}
+
+}  // namespace
 
 extern "C" {
 
@@ -592,57 +784,17 @@ int psg_nway_max_push(void) { return psg::kMaxRuns; }
 int psg_nway_create(int device, int dtype, int m, unsigned flags, int npush,
                     const uint64_t* const* keys, const uint64_t* n, const void* const* vals,
                     uint64_t* out_keys, void* const* out_vals, psg_nway** out) {
-  using namespace psg;
-  if (!out || npush < 0 || (npush && (!keys || !n)) || !out_keys)
-    return fail(PSG_ERR_ARG, "null argument");
-  if (dtype != PSG_F32 && dtype != PSG_F64) return fail(PSG_ERR_ARG, "dtype %d", dtype);
-  if (m < 0 || m > PSG_MAX_VALUE_ARRAYS || (m > 0 && (!vals || !out_vals)))
-    return fail(PSG_ERR_ARG, "m=%d", m);
-  HIP_TRY(hipSetDevice(device));
-  // empty pushes are ignored (kv_vector.h:90,177): push 0 is the first non-empty one
-  std::vector<const uint64_t*> pk;
-  std::vector<const void*> pv;
-  std::vector<uint64_t> pn;
-  uint64_t ntot = 0;
-  for (int p = 0; p < npush; ++p) {
-    if (n[p] == 0) continue;
-    if (!keys[p]) return fail(PSG_ERR_ARG, "push %d: null keys", p);
-    pk.push_back(keys[p]);
-    for (int i = 0; i < m; ++i) {
-      if (!vals[(size_t)p * m + i]) return fail(PSG_ERR_ARG, "push %d: null values", p);
-      pv.push_back(vals[(size_t)p * m + i]);
-    }
-    pn.push_back(n[p]);
-    ntot += n[p];
-  }
-  const uint32_t K = (uint32_t)pk.size();
-  if (K > (uint32_t)kMaxRuns) return fail(PSG_ERR_ARG, "%u pushes > %d per merge", K, kMaxRuns);
-  if (ntot >= (1ull << 32)) return fail(PSG_ERR_ARG, "%llu keys >= 2^32", (unsigned long long)ntot);
-  psg_nway* u = new psg_nway();
-  u->device = device;
-  u->dtype = dtype;
-  u->m = m;
-  u->ntot = ntot;
-  u->layout.plan(K, pn.data(), m);
-  if (hipMalloc(&u->blob, u->layout.bytes) != hipSuccess) {
-    const size_t want = u->layout.bytes;
-    delete u;
-    return fail(PSG_ERR_OOM, "nway: %zu bytes", want);
-  }
-  const hipError_t e = u->layout.upload((char*)u->blob, pk.data(), pv.data(), pn.data(),
-                                        (const void* const*)out_vals, m, nullptr, true);
-  if (e != hipSuccess) {
-    (void)hipFree(u->blob);
-    delete u;
-    return fail(PSG_ERR_DEVICE, "nway set-up: %s", hipGetErrorString(e));
-  }
-  u->args = u->layout.args((char*)u->blob, out_keys,
-                           (flags & PSG_PARALLEL_MATCH) ? kFlagParallel : 0u);
-  // SURVEY 8d general form, the read side: every push's keys and values
-  // (the merged output adds |union| * (8 + m s_V), known after a run)
-  u->bytes = ntot * (8 + (uint64_t)m * (dtype == PSG_F32 ? 4 : 8));
-  *out = u;
-  return PSG_OK;
+  if (npush < 0) return fail(PSG_ERR_ARG, "npush %d", npush);
+  uint64_t* ok[1] = {out_keys};
+  return nway_create(device, dtype, m, flags, 1, &npush, keys, n, vals, ok, out_vals, out);
+}
+
+int psg_nway_create_batch(int device, int dtype, int m, unsigned flags, int nmerge,
+                          const int* npush, const uint64_t* const* keys, const uint64_t* n,
+                          const void* const* vals, uint64_t* const* out_keys,
+                          void* const* out_vals, psg_nway** out) {
+  return nway_create(device, dtype, m, flags, nmerge, npush, keys, n, vals, out_keys, out_vals,
+                     out);
 }
 
 int psg_nway_run(psg_nway* u, void* stream) {
@@ -650,13 +802,13 @@ int psg_nway_run(psg_nway* u, void* stream) {
   HIP_TRY(hipSetDevice(u->device));
   hipStream_t st = (hipStream_t)stream;
   u->last = st;
-  HIP_TRY(psg::nway_enqueue(u->args, (char*)u->blob, u->layout, u->dtype, u->m, st));
+  HIP_TRY(psg::nway_enqueue((char*)u->blob, u->layout, u->dtype, st));
   return PSG_OK;
 }
 
 int psg_nway_count_dev(psg_nway* u, unsigned long long** nout) {
   if (!u || !nout) return fail(PSG_ERR_ARG, "null argument");
-  *nout = u->args.nout;
+  *nout = u->layout.misc((char*)u->blob, 0) + 1;
   return PSG_OK;
 }
 
@@ -664,14 +816,19 @@ int psg_nway_result(psg_nway* u, uint64_t* nout) {
   if (!u) return fail(PSG_ERR_ARG, "null merge");
   HIP_TRY(hipSetDevice(u->device));
   if (u->last) HIP_TRY(hipStreamSynchronize(u->last));
-  unsigned long long h[2] = {0, 0};
-  HIP_TRY(hipMemcpy(h, u->args.bad, 16, hipMemcpyDeviceToHost));  // bad, nout
-  if (nout) *nout = h[1];
-  if (h[0] >> 32)
-    return fail(PSG_ERR_DEVICE, "nway: tile overflow / look-back timeout (%llx)", h[0]);
-  if (h[0])
+  std::vector<unsigned long long> h(2 * (size_t)u->nm);  // per merge: bad, nout
+  HIP_TRY(hipMemcpy(h.data(), u->layout.misc((char*)u->blob, 0), 8 * h.size(),
+                    hipMemcpyDeviceToHost));
+  unsigned long long dev = 0, bad = 0;
+  for (uint32_t j = 0; j < u->nm; ++j) {
+    if (nout) nout[j] = h[2 * j + 1];
+    dev |= h[2 * j] >> 32;
+    bad += h[2 * j] & 0xffffffffull;
+  }
+  if (dev) return fail(PSG_ERR_DEVICE, "nway: tile overflow / look-back timeout (%llx)", dev);
+  if (bad)
     return fail(PSG_ERR_UNSORTED, "nway: %llu keys out of order (pushes must be strictly "
-                "increasing)", h[0]);
+                "increasing)", bad);
   return PSG_OK;
 }
 

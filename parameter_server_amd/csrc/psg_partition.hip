@@ -53,38 +53,9 @@ __global__ __launch_bounds__(256) void splitter_kernel(const JobDev* __restrict_
 }
 
 // ---- kSearch: one lane per (push, tile boundary) ----
-// lower_bound(S, xl) inside a bracket with S[a] < xl <= S[c]: interpolation
-// probes (pushes of murmur-hashed keys are near-uniform), bisection, then
-// the last <= 15 candidates in one round trip
-__device__ __forceinline__ uint64_t bracket_search(const uint64_t* S, uint64_t xl, uint64_t a,
-                                                   uint64_t c, uint64_t ka, uint64_t kc) {
-  for (int it = 0; it < 6 && c - a > 16u; ++it) {
-    const double f = (double)(xl - ka) / (double)(kc - ka);
-    uint64_t mid = a + 1 + (uint64_t)(f * (double)(c - a - 1));
-    mid = mid < c ? mid : c - 1;
-    const uint64_t km = S[mid];
-    if (km < xl) {
-      a = mid;
-      ka = km;
-    } else {
-      c = mid;
-      kc = km;
-    }
-  }
-  while (c - a > 16u) {
-    const uint64_t mid = a + ((c - a) >> 1);
-    if (S[mid] < xl) a = mid; else c = mid;
-  }
-  // independent loads of S[a+1 .. c-1] (indices clamped to c, where
-  // S[c] >= xl counts 0)
-  uint32_t below = 0;
-#pragma unroll
-  for (uint32_t i = 1; i < 16u; ++i) {
-    const uint64_t idx = a + i < c ? a + i : c;
-    below += S[idx] < xl ? 1u : 0u;
-  }
-  return a + 1u + below;
-}
+// (dev::bracket_lower_bound: interpolation probes, bisection, one batch of
+// the last <= 15 candidates)
+using dev::bracket_lower_bound;
 
 // A wave holds 64 consecutive boundaries of one push.  Every 16th lane and
 // the last search the whole push; the lanes between start from the bracket
@@ -111,7 +82,7 @@ __device__ __forceinline__ void search_item(const JobDev& J, uint32_t p, uint32_
   const int hi_l = lo_l + 16 < last ? lo_l + 16 : last;
   uint64_t res = 0;
   if (edge) {
-    res = xl <= k0 ? 0 : (xl > kn ? n : bracket_search(S, xl, 0, n - 1, k0, kn));
+    res = xl <= k0 ? 0 : (xl > kn ? n : bracket_lower_bound(S, xl, 0, n - 1, k0, kn));
   }
   const uint64_t r0 = (uint64_t)__shfl((long long)res, lo_l, 64);
   const uint64_t r1 = (uint64_t)__shfl((long long)res, hi_l, 64);
@@ -129,7 +100,7 @@ __device__ __forceinline__ void search_item(const JobDev& J, uint32_t p, uint32_
         kc = S[c];
         ok = ka < xl && xl <= kc;
       }
-      res = ok ? bracket_search(S, xl, a, c, ka, kc) : bracket_search(S, xl, 0, n - 1, k0, kn);
+      res = ok ? bracket_lower_bound(S, xl, a, c, ka, kc) : bracket_lower_bound(S, xl, 0, n - 1, k0, kn);
     }
   }
   if (valid) {

@@ -165,6 +165,10 @@ struct JobTable {
   // cursor form (psg_tile_cursor.hip): plans of long pieces, no partition
   // pass; chunks of consecutive tiles, one workgroup each
   bool cursor = false;
+  // packed cursor form (psg_tile_packed.hip CUR): short pieces of <= 256
+  // pushes, no partition pass either
+  bool pcursor = false;
+  uint32_t bxs = 32;          // boundary words per chunk boundary (pushes per job at most)
   uint32_t nchunks = 0;
   psg::CursorJob* d_cjobs = nullptr;
   psg::CursorChunk* d_chunks = nullptr;
@@ -339,9 +343,34 @@ struct JobTable {
       for (const JobInfo& I : info) ckr = std::max(ckr, I.kr);
       for (JobInfo& I : info) I.kr = ckr;
     }
-    if (cursor) {
-      // about one chunk per workgroup slot of the chip (256 CUs x 8)
-      constexpr uint64_t kChunkTarget = 2048;
+    // the packed cursor form: plans (resident index) of packed-round jobs of
+    // at most 256 pushes whose pointers leave the top 16 bits free (the
+    // kernel keeps a piece's length there) and whose tiles' elements fit one
+    // pass (mean + 6 sigma <= 2,560; larger ones take more groups per tile)
+    pcursor = index && !dense && pack && knob_cursor != 0 && tiles > 0 &&
+              (knob_cursor == 1 || (knob_part < 0 && knob_pack < 0));
+    for (size_t j = 0; pcursor && j < jobs.size(); ++j) {
+      const JobSpec& s = jobs[j];
+      const JobInfo& I = info[j];
+      if (s.dense || I.np > (uint32_t)psg::kPackCursorPushes) {
+        pcursor = false;
+        break;
+      }
+      for (size_t p = 0; p < s.pkeys.size(); ++p) {
+        bool hi = ((uint64_t)s.pkeys[p] >> 48) != 0;
+        for (int i = 0; i < m; ++i) hi |= ((uint64_t)s.pvals[p * m + i] >> 48) != 0;
+        if (hi) pcursor = false;
+      }
+      double kv = 0;
+      for (uint64_t n : I.pn) kv += (double)n;
+      const double per_tile = I.ntiles ? kv / I.ntiles : 0.0;
+      if (per_tile + 6.0 * std::sqrt(per_tile) > 2560.0 && knob_cursor != 1) pcursor = false;
+    }
+    bxs = pcursor ? (uint32_t)psg::kPackCursorPushes : 32u;
+    if (cursor || pcursor) {
+      // about one chunk per workgroup slot of the chip (256 CUs x 8
+      // workgroups of the cursor kernel, x 4 of the packed one)
+      const uint64_t kChunkTarget = cursor ? 2048 : 1024;
       const uint64_t per = std::max<uint64_t>(1, (tiles + kChunkTarget - 1) / kChunkTarget);
       uint64_t nc = 0;
       for (JobInfo& I : info) {
@@ -369,7 +398,7 @@ struct JobTable {
     const size_t cjobs_off = off;
     if (cursor) off = align_up(off + sizeof(psg::CursorJob) * jobs.size(), 256);
     const size_t chunks_off = off;
-    if (cursor) off = align_up(off + sizeof(psg::CursorChunk) * nchunks, 256);
+    if (cursor || pcursor) off = align_up(off + sizeof(psg::CursorChunk) * nchunks, 256);
     // one zeroed region: every job's fail counters, then the boundary words
     const size_t zero_off = off;
     size_t fail_cur = zero_off;
@@ -379,7 +408,7 @@ struct JobTable {
       off = align_up(off + 8 * npall, 256);
     }
     const size_t bx_off = off;
-    if (cursor) off = align_up(off + 4 * 32 * ((size_t)nchunks + 1), 256);
+    if (cursor || pcursor) off = align_up(off + 4 * (size_t)bxs * ((size_t)nchunks + 1), 256);
     const size_t zero_end = off;
     for (size_t j = 0; j < jobs.size(); ++j) {
       const size_t np = info[j].np, nt = info[j].ntiles;
@@ -491,7 +520,7 @@ struct JobTable {
         T.np = np;
         T.stride = d.segq;
         T.segb = d.segb;
-        T.flags = s.flags;
+        T.flags = s.flags | (t + 1 == nt ? psg::kFlagLastTile : 0u);
         T.dpos = s.dense ? (const uint64_t*)(base + o.dpos) : nullptr;
         T.bt = use_index ? (const uint32_t*)(base + index_off) + (size_t)(tcur - 1) * iw : nullptr;
       }
@@ -530,6 +559,24 @@ struct JobTable {
       if (ccur != nchunks) return fail(PSG_ERR_DEVICE, "cursor chunks %llu/%u",
                                        (unsigned long long)ccur, nchunks);
     }
+    if (pcursor) {  // chunks index the tile descriptors
+      psg::CursorChunk* hch = (psg::CursorChunk*)(img + chunks_off);
+      chunk0.assign(jobs.size(), 0);
+      uint64_t tbase = 0, ccur = 0;
+      for (size_t j = 0; j < jobs.size(); ++j) {
+        const JobInfo& I = info[j];
+        chunk0[j] = (uint32_t)ccur;
+        for (uint32_t k = 0; k < I.nch; ++k) {
+          psg::CursorChunk& ch = hch[ccur++];
+          ch.job = (uint32_t)j;
+          ch.t0 = (uint32_t)(tbase + (uint64_t)k * I.ntiles / I.nch);
+          ch.t1 = (uint32_t)(tbase + (uint64_t)(k + 1) * I.ntiles / I.nch);
+        }
+        tbase += I.ntiles;
+      }
+      if (ccur != nchunks) return fail(PSG_ERR_DEVICE, "cursor chunks %llu/%u",
+                                       (unsigned long long)ccur, nchunks);
+    }
     // the fill must match the sizing pass exactly (the image regions are
     // packed back to back): a mismatch is a bug, never launched
     if (icur != items || scur != sitems || tcur != tiles)
@@ -546,8 +593,8 @@ struct JobTable {
     d_split_items = (uint32_t*)(base + sitems_off);
     d_items = (uint64_t*)(base + items_off);
     d_cjobs = cursor ? (psg::CursorJob*)(base + cjobs_off) : nullptr;
-    d_chunks = cursor ? (psg::CursorChunk*)(base + chunks_off) : nullptr;
-    d_bx = cursor ? (uint32_t*)(base + bx_off) : nullptr;
+    d_chunks = cursor || pcursor ? (psg::CursorChunk*)(base + chunks_off) : nullptr;
+    d_bx = cursor || pcursor ? (uint32_t*)(base + bx_off) : nullptr;
     d_zero = base + zero_off;
     zero_bytes = zero_end - zero_off;
     // the image is small: a DMA copy's fixed cost exceeds its transfer time
@@ -566,14 +613,16 @@ struct JobTable {
   int run_stage(int stage, hipStream_t s) const {
     if (h.empty()) return PSG_OK;
     if (stage == 0) {
-      if (cursor) HIP_TRY(hipMemsetAsync(d_zero, 0, zero_bytes, s));  // fail counters, boundaries
+      if (cursor || pcursor)  // fail counters, boundaries
+        HIP_TRY(hipMemsetAsync(d_zero, 0, zero_bytes, s));
       else if (!dense) HIP_TRY(psg::launch_partition(d_jobs, d_split_items, nsplit, d_items, nitems, s));
     } else if (cursor)
       HIP_TRY(psg::launch_aggregate_cursor(dtype, m, (int)ckr, d_cjobs, d_chunks, nchunks, d_bx, s));
     else if (dense)
       HIP_TRY(psg::launch_aggregate_dense(dtype, m, d_tiles, ntiles, s));
     else if (pack)
-      HIP_TRY(psg::launch_aggregate_tile_packed(dtype, m, d_tiles, ntiles, s));
+      HIP_TRY(psg::launch_aggregate_tile_packed(dtype, m, d_tiles, ntiles, s,
+                                                pcursor ? d_chunks : nullptr, nchunks, d_bx));
     else
       HIP_TRY(psg::launch_aggregate_tile(dtype, m, d_tiles, ntiles, wide ? 1 : 0, s));
     return PSG_OK;
@@ -604,16 +653,17 @@ struct JobTable {
         // cursor form: a chunk boundary where the chunks' cursors disagree
         // (start != the previous chunk's end) means an unsorted push
         std::vector<uint32_t> bxw;
-        if (cursor && I.nch > 1) {
-          bxw.resize((size_t)32 * (I.nch - 1));
-          HIP_TRY(hipMemcpy(bxw.data(), d_bx + (size_t)32 * (chunk0[j] + 1), 4 * bxw.size(),
+        const bool cur = cursor || pcursor;
+        if (cur && I.nch > 1) {
+          bxw.resize((size_t)bxs * (I.nch - 1));
+          HIP_TRY(hipMemcpy(bxw.data(), d_bx + (size_t)bxs * (chunk0[j] + 1), 4 * bxw.size(),
                             hipMemcpyDeviceToHost));
         }
         for (uint32_t p = 0; p < np; ++p) {
           const uint64_t covered = last[p] >= first[p] ? (uint64_t)(last[p] - first[p]) : 0;
           uint64_t v = covered >= f[p] ? covered - f[p] : 0;
           bool torn = false;
-          for (size_t k = 0; k + 1 < I.nch && cursor; ++k) torn |= bxw[32 * k + p] != 0;
+          for (size_t k = 0; k + 1 < I.nch && cur; ++k) torn |= bxw[(size_t)bxs * k + p] != 0;
           if (torn && v >= I.pn[p]) v = I.pn[p] - 1;
           mt[I.slot[p]] = v;
         }
@@ -705,6 +755,10 @@ struct PendingPush {
 // grows when a push brings more arrays than the earlier ones; array i is
 // assigned by the first push holding an i-th array and added to by the later
 // ones that hold one (a push without it leaves it alone)
+// an aggregate's device counters: unmatched keys, compressed parts that failed
+// to decode, pushes whose keys do not match their carried signature
+constexpr size_t kBadBytes = 32;
+
 struct Aggregate {
   int chl = 0, m = 0;                // m: arrays so far (the largest push's)
   size_t lo = 0, hi = 0;
@@ -714,7 +768,8 @@ struct Aggregate {
   uint64_t folded_arr[psg::kMaxM] = {};  // of them, those holding array i
   uint64_t expected_total = 0;
   // device: [0] pushed keys not matched so far, [1] compressed parts that
-  // failed to decode (psg_push_compressed reports them here, asynchronously)
+  // failed to decode (psg_push_compressed reports them here, asynchronously),
+  // [2] pushes whose keys do not match their carried signature
   unsigned long long* d_bad = nullptr;
 };
 
@@ -1174,7 +1229,7 @@ struct psg_ctx {
       if (int rc = table.run(stream)) return rc;
       HIP_TRY(psg::launch_unmatched(table.d_jobs, 0, table.info[0].np, a.d_bad, stream));
       if (bad_host && take == a.pending.size())
-        if (int rc = d2h(bad_host, a.d_bad, 16)) return rc;
+        if (int rc = d2h(bad_host, a.d_bad, kBadBytes)) return rc;
       for (size_t p = 0; p < take; ++p) {
         for (int i = 0; i < a.pending[p].m; ++i) ++a.folded_arr[i];
         release_push(a.pending[p]);
@@ -1191,7 +1246,7 @@ struct psg_ctx {
     for (auto& pp : a.pending) release_push(pp);
     a.pending.clear();
     for (int i = 0; i < a.m; ++i) dev_put(a.d_out[i], (a.hi - a.lo) * sv);
-    dev_put(a.d_bad, 16);
+    dev_put(a.d_bad, kBadBytes);
   }
 
   // the value push behind psg_push / psg_push_cached / psg_push_compressed:
@@ -1324,6 +1379,7 @@ int psg_plan_form(psg_plan* plan, int* form) {
   if (!plan || !form) return fail(PSG_ERR_ARG, "null argument");
   const JobTable& T = plan->table;
   *form = T.cursor ? PSG_KERNEL_CURSOR
+          : T.pcursor ? PSG_KERNEL_PACKED_CURSOR
           : T.dense ? PSG_KERNEL_DENSE
           : T.pack  ? PSG_KERNEL_PACKED
           : T.wide  ? PSG_KERNEL_TILE64
@@ -1710,8 +1766,8 @@ int psg_ctx::aggregate_for(int chl, int time, uint64_t kb, uint64_t ke, int m,
     // zeroed on `copy`: the dense pushes' order checks and the compressed
     // pushes' decodes add to it there; every reader on `stream` runs after
     // a join_copy
-    if (int rc = dev_get(16, (void**)&A.d_bad, copy)) return rc;
-    HIP_TRY(hipMemsetAsync(A.d_bad, 0, 16, copy));
+    if (int rc = dev_get(kBadBytes, (void**)&A.d_bad, copy)) return rc;
+    HIP_TRY(hipMemsetAsync(A.d_bad, 0, kBadBytes, copy));
     ait = agg.emplace(time, A).first;
   }
   Aggregate& A = ait->second;
@@ -2025,6 +2081,7 @@ int push_cached_impl(psg_ctx* c, int sender, int chl, int time, uint64_t kb, uin
   if (int rc = set_dev(c->device)) return rc;
   const CacheKey ck{sender, chl, kb, ke};
   KeyRef k;  // the message's keys, resident
+  bool sigcheck = false;  // the carried signature checked on the device
   if (!(kc & PSG_KC_SIG)) {
     // no signature: the cache entry of (channel, range) is dropped
     // (remote_node.cc:143-156) and the message's own keys are used
@@ -2040,7 +2097,13 @@ int push_cached_impl(psg_ctx* c, int sender, int chl, int time, uint64_t kb, uin
       if (int rc = c->h2d(k->d, keys, 8 * nkeys)) return rc;
     }
     uint32_t got = 0;  // crc32c::Value of no bytes
-    if (nkeys) {
+    // with values (m > 0) the check runs on the device and a mismatch is
+    // reported by psg_received (no host wait); a key-only message merges
+    // into the channel's keys at once, so it is checked before that
+    if (nkeys && m > 0) {
+      sigcheck = true;
+      got = sig;
+    } else if (nkeys) {
       c->h_small[8] = 0;
       c->h_small[9] = 8 * nkeys;
       HIP_TRY(hipMemcpyAsync(c->d_small + 8, c->h_small + 8, 16, hipMemcpyHostToDevice, c->copy));
@@ -2075,6 +2138,12 @@ int push_cached_impl(psg_ctx* c, int sender, int chl, int time, uint64_t kb, uin
     return fail(PSG_ERR_SIZE, "%zu values for %zu keys", nvals, n);
   size_t lo, hi;
   if (int rc = check_push(c, chl, time, kb, ke, n, m, &lo, &hi)) return rc;
+  if (sigcheck) {  // into the aggregate's counters, on `copy` after the key copy
+    Aggregate* A = nullptr;
+    if (int rc = c->aggregate_for(chl, time, kb, ke, m, &A)) return rc;
+    HIP_TRY(psg::launch_sig_check((const uint8_t*)k->d, 8 * n, PSG_MAX_SIG_LEN, sig, A->d_bad + 2,
+                                  c->copy));
+  }
   return c->push_values(chl, time, kb, ke, k, m, vals);
 }
 
@@ -2133,13 +2202,14 @@ int psg_received(psg_ctx* c, int time, int m, void* const* out) {
   for (int i = 0; !direct && rc == PSG_OK && i < A.m && len; ++i)
     rc = c->d2h(out[i], A.d_out[i], len * sv);
   unsigned long long bad = 0;
-  unsigned long long corrupt = 0;
-  if (rc == PSG_OK && !(direct && pend)) rc = c->d2h(c->h_small, A.d_bad, 16);
+  unsigned long long corrupt = 0, badsig = 0;
+  if (rc == PSG_OK && !(direct && pend)) rc = c->d2h(c->h_small, A.d_bad, kBadBytes);
   if (rc == PSG_OK) {
     hipError_t e = hipStreamSynchronize(c->stream);
     if (e != hipSuccess) rc = fail(PSG_ERR_DEVICE, "received: %s", hipGetErrorString(e));
     bad = c->h_small[0];
     corrupt = c->h_small[1];
+    badsig = c->h_small[2];
   }
   const unsigned long long want = A.expected_total;
   c->drop(A);
@@ -2147,6 +2217,9 @@ int psg_received(psg_ctx* c, int time, int m, void* const* out) {
   if (rc) return rc;
   if (corrupt)  // Van::recv's CHECK on uncompressFrom (shared_array_inl.h:236)
     return fail(PSG_ERR_ARG, "time %d: %llu compressed parts failed to decode", time, corrupt);
+  if (badsig)  // cacheKeyRecver's CHECK_EQ(crc32c(key), sig) (remote_node.cc:163)
+    return fail(PSG_ERR_SIGNATURE, "time %d: %llu pushes' keys do not match their signature",
+                time, badsig);
   if (bad)
     return fail(PSG_ERR_UNMATCHED, "time %d: matched %llu of %llu pushed keys", time,
                 want - bad, want);

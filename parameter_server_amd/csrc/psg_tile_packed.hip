@@ -41,6 +41,22 @@
 // strictly and every key must be found; the piece boundaries come from the
 // tile's key bounds, so this is the reference's matched == n <=> sorted,
 // unique, inside the range.
+//
+// Cursor form (CUR, plans of <= 256 pushes on a resident index): no
+// partition pass.  A workgroup walks a CHUNK of consecutive tiles of one job
+// and keeps each push's cursor (the first key not merged yet) in LDS as the
+// piece pointer itself; two lanes per push (all 8 waves) load the 16 keys at
+// the cursor, and the piece is the keys before the first one >= the next
+// tile's first server key (lower_bound, message.h:96-99).  The same lanes
+// touch the piece's value lines, so the pass's element loads that follow hit
+// L2: each push key is read from HBM once per run (the partition read every
+// key once more, cfg5: 0.58 GB).  Piece pointers then point at the piece's
+// END with its length in the top 16 bits (device addresses are < 2^48), so
+// the next tile starts there; pieces are cut at kTS keys (keys past it can
+// only fail, and do so in the next tile).  Chunk boundaries: each chunk
+// starts from lower_bound(push, its first key) and xors its start and end
+// cursors into the word it shares with its neighbour (a nonzero word = an
+// unsorted push); the job's first and last chunks write the covered range.
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
@@ -79,6 +95,12 @@ static_assert(kSPT == 4 && kBPT == 4, "layout");
 static_assert(kTS <= 0x7ffe, "u16 positions");
 static_assert(kG <= 256, "u8 element -> push map, 8-bit push field of a round entry");
 static_assert(kECap >= kTS, "a piece (<= kTS keys) always fits a group");
+static_assert(kNT / 2 == kG, "cursor form: two lanes per push");
+static_assert(kTS < 65536, "cursor form: a piece length in 16 bits");
+constexpr uint64_t kPtrMask = (1ull << 48) - 1;  // cursor form: pointer bits of a piece word
+#ifndef PSG_PC_TOUCH
+#define PSG_PC_TOUCH 1  // A/B builds: 0 = the cursor phase does not touch the value lines
+#endif
 
 typedef unsigned long long u64x2 __attribute__((ext_vector_type(2)));
 typedef uint32_t u32x2 __attribute__((ext_vector_type(2)));
@@ -129,9 +151,10 @@ constexpr int occupancy() {
 
 // rounds of 64 consecutive elements of the concatenated pieces: a round
 // can hold several pushes
-template <typename V, int M>
+template <typename V, int M, bool CUR>
 __global__ __launch_bounds__(kNT, (occupancy<V, M>())) void tile_packed_kernel(
-    const TileDesc* __restrict__ tiles, uint32_t ntiles) {
+    const TileDesc* __restrict__ tiles, uint32_t ntiles, const CursorChunk* __restrict__ chunks,
+    uint32_t nchunks, uint32_t* __restrict__ bx) {
   __shared__ __attribute__((aligned(16))) uint64_t dk[kTS + 8];
   // bucket starts (u16); the histogram counts in it as packed pairs by 32-bit atomics
   __shared__ __attribute__((aligned(16))) uint32_t bt32[(kNB + 8) / 2];
@@ -157,9 +180,51 @@ __global__ __launch_bounds__(kNT, (occupancy<V, M>())) void tile_packed_kernel(
 
   const uint32_t w = uni((uint32_t)threadIdx.x >> 6);
   const int tid = threadIdx.x;
+  // the tiles of this workgroup: one (partition form), or a chunk (cursor form)
+  uint32_t tb, te, ci = 0;
+  if constexpr (CUR) {
+    ci = xcd_tile(blockIdx.x, gridDim.x);
+    if (ci >= nchunks) return;
+    tb = chunks[ci].t0;
+    te = chunks[ci].t1;
+  } else {
+    tb = xcd_tile(blockIdx.x, gridDim.x);
+    if (tb >= ntiles) return;
+    te = tb + 1u;
+  }
+  // cursor form: keys of push tid >> 1 not merged yet (both lanes of the pair)
+  uint32_t rem = 0;
+  if constexpr (CUR) {
+    // start cursors: lower_bound(push q, the chunk's first server key)
+    const TileDesc& T0 = tiles[tb];
+    const uint32_t q = (uint32_t)tid >> 1;
+    if (q < T0.np) {
+      const uint64_t* S = G(T0.pkeys)[q];
+      const uint64_t n = G(T0.pn)[q];
+      const uint64_t c = dev::interp_lower_bound(S, n, G(T0.dk)[0]);
+      rem = (uint32_t)(n - c);
+      if ((tid & 1) == 0) {
+        pkp[q] = (uint64_t)(S + c);
+        if (T0.slot0 == 0) GW(const_cast<uint32_t*>(T0.seg))[(size_t)q * T0.stride] = (uint32_t)c;
+        else atomicXor(bx + (size_t)ci * kG + q, (uint32_t)c);
+      } else {
+#pragma unroll
+        for (int mi = 0; mi < M; ++mi)
+          pvp[q * M + mi] = (uint64_t)((const V*)G(T0.pvals)[(size_t)q * M + mi] + c);
+      }
+    }
+    // the pair's other lane reads pkp[q] next: LDS accesses of one wave are
+    // in order, the fences keep the compiler from moving them
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+  }
+  for (uint32_t ti = tb;; ++ti) {  // the partition form: one tile, no loop
+  // the thread id afresh per tile (opaque): values derived from it are
+  // recomputed in the loop instead of held (and spilled) across it
+  int tid = threadIdx.x;
+  if constexpr (CUR) asm volatile("" : "+v"(tid));
   const int lane = tid & 63;
-  const uint32_t ti = xcd_tile(blockIdx.x, gridDim.x);
-  if (ti >= ntiles) return;
   const TileDesc& T = tiles[ti];
   const uint32_t np = T.np;
   const uint32_t nt = T.nt;
@@ -281,7 +346,128 @@ __global__ __launch_bounds__(kNT, (occupancy<V, M>())) void tile_packed_kernel(
       }
     }
   };
-  if (np) tables_a(0);
+  // ---- cursor form: the tables of the group at g0 from the cursors, all 8
+  // waves, push g0 + (t >> 1) on lanes t (h = 0) and t + 1 (h = 1).  Phase A
+  // (`first`: the tile's first group) finds each piece: the pair loads the
+  // 16 keys at the cursor (8 each), the piece ends before the first key >=
+  // the next tile's first key (16 more at a time for a longer piece), and
+  // moves the piece words to the piece's end.  A later group of the same
+  // tile reads the lengths back from the words.  Returns the push's piece
+  // length (h = 0 lanes) and its wave-inclusive prefix in *x; the wave
+  // totals go to wsum.
+  const bool lastt = CUR && (T.flags & kFlagLastTile) != 0u;
+  const uint64_t dlast = lastt ? G(Dg)[nt - 1] : 0ull;
+  // the piece bound: keys < the next tile's first key; the job's last tile
+  // takes every key <= D[nslots - 1] (open: D ends at 2^64 - 1)
+  const bool open = lastt && dlast == ~0ull;
+  const uint64_t nxt = !CUR ? 0ull : lastt ? dlast + 1ull : G(Dg)[kTS];
+  auto cur_a = [&](uint32_t g0, bool first, uint32_t* x) -> uint32_t {
+    uint32_t t = (uint32_t)threadIdx.x;
+    asm volatile("" : "+v"(t));
+    const uint32_t h = t & 1u, q = g0 + (t >> 1);
+    const bool own = q < np;
+    uint32_t len = 0;
+    if (first) {
+      uint64_t st = 0;
+      auto piece8 = [&](uint32_t b) -> uint32_t {  // keys [b + 8h, b + 8h + 8): leading keys < nxt
+        const uint32_t o = b + 8u * h;
+        const uint32_t avail = rem > o ? rem - o : 0u;
+        const AS1 uint64_t* S = G((const uint64_t*)st) + o;
+        uint32_t lt = 0;
+#pragma unroll
+        for (int j = 0; j < 8; ++j) {
+          const uint64_t k = (uint32_t)j < avail ? S[j] : ~0ull;
+          lt |= (uint32_t)((uint32_t)j < avail && (open || k < nxt)) << j;
+        }
+        return (uint32_t)__builtin_ctz(~lt);
+      };
+      uint32_t f = 8;
+      if (own) {
+        st = pkp[q] & kPtrMask;
+        f = piece8(0);
+#if PSG_PC_TOUCH
+        // the piece's value lines (its first 16 values), so the pass's
+        // element loads find them in L2
+        const uint32_t o = 8u * h;
+        if (rem > o) {
+          const uint32_t e = rem - o < 8u ? rem - o - 1u : 7u;
+#pragma unroll
+          for (int mi = 0; mi < M; ++mi) {
+            const AS1 V* pv = G((const V*)pvp[q * M + mi]) + o;
+            const V v0 = pv[0], v1 = pv[e];
+            asm volatile("" ::"v"(v0), "v"(v1));
+          }
+        }
+#endif
+      }
+      const uint32_t fo = (uint32_t)__shfl_xor((int)f, 1, 64);
+      len = (h ? fo : f) < 8u ? (h ? fo : f) : 8u + (h ? f : fo);
+      if (own && len == 16u && rem > 16u) {  // a longer piece (rare): 16 keys a step
+        for (uint32_t b = 16;; b += 16) {
+          const uint32_t g = piece8(b);
+          const uint32_t go = (uint32_t)__shfl_xor((int)g, 1, 64);
+          const uint32_t l = (h ? go : g) < 8u ? (h ? go : g) : 8u + (h ? g : go);
+          len = b + l;
+          if (l < 16u || b + 16u >= rem || len >= (uint32_t)kTS) break;
+        }
+      }
+      len = len < (uint32_t)kTS ? len : (uint32_t)kTS;
+      if (own) {
+        if (h == 0u) {
+          pkp[q] = (st + 8ull * len) | (uint64_t)len << 48;
+        } else {
+#pragma unroll
+          for (int mi = 0; mi < M; ++mi) pvp[q * M + mi] += (uint64_t)len * sizeof(V);
+        }
+        rem -= len;
+      }
+    } else {
+      len = own ? (uint32_t)(pkp[q] >> 48) : 0u;
+    }
+    const uint32_t lv = own && h == 0u ? len : 0u;
+    *x = wave_scan_incl(lv);
+    if (lane_id() == 63u) wsum[w] = *x;
+    if (t == 0u) {
+      uint32_t z = 0;  // opaque zero (as in tables_a)
+      asm volatile("" : "+v"(z));
+      gsh[0] = z;
+      gsh[1] = z;
+    }
+    return lv;
+  };
+  // phase B (after a barrier): the group's prefix, the pushes whose elements
+  // fit one pass (a prefix of them), the element -> push map
+  auto cur_b = [&](uint32_t g0, uint32_t lv, uint32_t x) {
+    uint32_t t = (uint32_t)threadIdx.x;
+    asm volatile("" : "+v"(t));
+    const uint32_t ql = t >> 1;
+    uint32_t base = 0;
+#pragma unroll
+    for (uint32_t v = 0; v < (uint32_t)kNW - 1u; ++v) base += v < w ? wsum[v] : 0u;
+    const uint32_t X = x + base;  // elements of the group through push ql
+    // X grows with ql, so the pushes that fit are a prefix
+    const bool in = (t & 1u) == 0u && g0 + ql < np && X <= (uint32_t)kECap;
+    const uint32_t fit = (uint32_t)__popcll(__ballot(in));
+    uint32_t emax = in ? X : 0u;
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) {
+      const uint32_t y = (uint32_t)__shfl_xor((int)emax, o, 64);
+      emax = y > emax ? y : emax;
+    }
+    if (in) {
+      pre[ql + 1] = X;
+#pragma nounroll
+      for (uint32_t e = X - lv; e < X; ++e) ep[e] = (uint8_t)ql;
+    }
+    if (lane_id() == 0u) {
+      __hip_atomic_fetch_add(&gsh[0], fit, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+      __hip_atomic_fetch_max(&gsh[1], emax, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+    }
+    if (t == 0u) pre[0] = 0;
+  };
+  if (np) {
+    if constexpr (!CUR) tables_a(0);
+  }
 
 
   // ---- D keys, continued sums: thread t owns slots 4t..4t+3
@@ -306,6 +492,11 @@ __global__ __launch_bounds__(kNT, (occupancy<V, M>())) void tile_packed_kernel(
 #pragma unroll
     for (int j = 0; j < 4; ++j)
       a0[mi][j] = (cont && s0i + j < nt) ? G((const V*)T.out[mi] + T.slot0)[s0i + j] : V(0);
+  // cursor form: the pieces, while D and the index are in flight
+  uint32_t cx = 0, clv = 0;
+  if constexpr (CUR) {
+    if (np) clv = cur_a(0, true, &cx);
+  }
 
   // bucket of a key: the tile's key range [klo, khi] scaled onto [0, kNB) by
   // one 32x32 high multiply; keys outside the range land in an end bucket
@@ -323,23 +514,30 @@ __global__ __launch_bounds__(kNT, (occupancy<V, M>())) void tile_packed_kernel(
   };
 
   // ---- install D, sums, lastl; clear the histogram and the bitmaps
+  // (constants as opaque values: hoisted out of the cursor form's tile loop
+  // they would hold VGPRs across it, and spill)
+  uint32_t ones = ~0u, one = 1u;
+  if constexpr (CUR) asm volatile("" : "+v"(ones), "+v"(one));
 #pragma unroll
   for (int j = 0; j < 4; ++j) {
     dk[s0i + j] = d[j];
 #pragma unroll
     for (int mi = 0; mi < M; ++mi) acc[mi][s0i + j] = a0[mi][j];
-    lastl[s0i + j] = 1;  // last = -1 = g0 - 1
+    lastl[s0i + j] = (uint16_t)one;  // last = -1 = g0 - 1
   }
-  if (tid < 8) dk[kTS + tid] = ~0ull;
+  if (tid < 8) dk[kTS + tid] = (uint64_t)ones << 32 | ones;
   {
     uint32_t z = 0;  // opaque zero: not a hoisted (and spilled) constant vector
     asm volatile("" : "+v"(z));
     *(u32x2*)&bt[tid * kBPT] = Bg ? btw : u32x2{z, z};  // resident table, or a cleared histogram
     if (Bg && tid == 0) bt[kNB] = (uint16_t)nt;
   }
-  if (tid == 0) pcarry = -1;
+  if (tid == 0) pcarry = (int)ones;
   __syncthreads();  // (1) pieces scanned, D, cleared histogram (or the resident bucket table)
-  if (np) tables_b(0);
+  if (np) {
+    if constexpr (CUR) cur_b(0, clv, cx);
+    else tables_b(0);
+  }
   __syncthreads();  // (1b) the group's tables
 
   // ---- a pass: this wave's run of rounds, loaded into registers
@@ -374,12 +572,23 @@ __global__ __launch_bounds__(kNT, (occupancy<V, M>())) void tile_packed_kernel(
         // exists, so its push is a safe address for the lanes past the end
         uint32_t q = ep[have ? e : R * 64u];
         const uint32_t qlo = uni(q);
-        const uint32_t i = have ? e - pre[q] : 0u;
         mmask |= (__ballot(have && q != qlo) != 0 ? 1u : 0u) << r;
-        rp[r / 3] |= (q | (uint32_t)(have && i == 0u) << 8 | (uint32_t)have << 9) << (10 * (r % 3));
-        ek[r] = G((const uint64_t*)pkp[q])[i];
+        if constexpr (CUR) {
+          // piece words point at the piece's end: element e is `back` before it
+          const uint64_t pw = pkp[g0 + q];
+          const uint32_t back = have ? pre[q + 1] - e : 1u;
+          const bool head = have && back == (uint32_t)(pw >> 48);
+          rp[r / 3] |= (q | (uint32_t)head << 8 | (uint32_t)have << 9) << (10 * (r % 3));
+          ek[r] = *(G((const uint64_t*)(pw & kPtrMask)) - back);
 #pragma unroll
-        for (int mi = 0; mi < M; ++mi) ev[r][mi] = G((const V*)pvp[q * M + mi])[i];
+          for (int mi = 0; mi < M; ++mi) ev[r][mi] = *(G((const V*)pvp[(g0 + q) * M + mi]) - back);
+        } else {
+          const uint32_t i = have ? e - pre[q] : 0u;
+          rp[r / 3] |= (q | (uint32_t)(have && i == 0u) << 8 | (uint32_t)have << 9) << (10 * (r % 3));
+          ek[r] = G((const uint64_t*)pkp[q])[i];
+#pragma unroll
+          for (int mi = 0; mi < M; ++mi) ev[r][mi] = G((const V*)pvp[q * M + mi])[i];
+        }
       }
     }
   };
@@ -442,9 +651,16 @@ __global__ __launch_bounds__(kNT, (occupancy<V, M>())) void tile_packed_kernel(
       // rebase lastl on the new group: last == g0 - 1 -> 1, older -> 0
 #pragma unroll
       for (int j = 0; j < 4; ++j) lastl[s0i + j] = lastl[s0i + j] == gp + 1u ? 1 : 0;
-      tables_a(g0);
-      __syncthreads();
-      tables_b(g0);
+      if constexpr (CUR) {
+        uint32_t x;
+        const uint32_t lv = cur_a(g0, false, &x);
+        __syncthreads();
+        cur_b(g0, lv, x);
+      } else {
+        tables_a(g0);
+        __syncthreads();
+        tables_b(g0);
+      }
       __syncthreads();
       gp = uni(gsh[0]);
       Et = uni(gsh[1]);
@@ -705,12 +921,38 @@ __global__ __launch_bounds__(kNT, (occupancy<V, M>())) void tile_packed_kernel(
         if (s0 + j < nt) GW(o)[j] = res[mi][j];
     }
   }
+  if constexpr (!CUR) {
+    break;
+  } else {
+    if (ti + 1u >= te) break;
+    __syncthreads();  // the next tile's installs overwrite what the stores read
+  }
+  }  // tiles of the chunk
+  if constexpr (CUR) {
+    // end cursors: into the boundary word shared with the next chunk, or the
+    // covered range's end (the job's last tile)
+    const TileDesc& T1 = tiles[te - 1u];
+    uint32_t t = (uint32_t)threadIdx.x;  // fresh: the loop's ids are dead
+    asm volatile("" : "+v"(t));
+    const uint32_t q = t >> 1;
+    if (q < T1.np && (t & 1u) == 0u) {
+      const uint32_t c = (uint32_t)(((pkp[q] & kPtrMask) - (uint64_t)G(T1.pkeys)[q]) / 8u);
+      if (T1.flags & kFlagLastTile) GW(const_cast<uint32_t*>(T1.seg))[(size_t)q * T1.stride + T1.segb] = c;
+      else atomicXor(bx + (size_t)(ci + 1u) * kG + q, c);
+    }
+  }
 }
 
 template <typename V, int M>
-hipError_t go(const TileDesc* t, uint32_t n, hipStream_t s) {
+hipError_t go(const TileDesc* t, uint32_t n, const CursorChunk* ch, uint32_t nch, uint32_t* bx,
+              hipStream_t s) {
   if constexpr (lds_bytes<V, M>() <= 163840) {
-    hipLaunchKernelGGL((tile_packed_kernel<V, M>), dim3(n), dim3(kNT), 0, s, t, n);
+    if (ch)
+      hipLaunchKernelGGL((tile_packed_kernel<V, M, true>), dim3(nch), dim3(kNT), 0, s, t, n, ch,
+                         nch, bx);
+    else
+      hipLaunchKernelGGL((tile_packed_kernel<V, M, false>), dim3(n), dim3(kNT), 0, s, t, n, ch,
+                         nch, bx);
     return hipGetLastError();
   } else {
     return hipErrorInvalidValue;  // larger tiles (A/B builds) hold fewer value arrays
@@ -718,12 +960,13 @@ hipError_t go(const TileDesc* t, uint32_t n, hipStream_t s) {
 }
 
 template <typename V>
-hipError_t launch_m(int m, const TileDesc* t, uint32_t n, hipStream_t s) {
+hipError_t launch_m(int m, const TileDesc* t, uint32_t n, const CursorChunk* ch, uint32_t nch,
+                    uint32_t* bx, hipStream_t s) {
   switch (m) {
-    case 1: return go<V, 1>(t, n, s);
-    case 2: return go<V, 2>(t, n, s);
-    case 3: return go<V, 3>(t, n, s);
-    case 4: return go<V, 4>(t, n, s);
+    case 1: return go<V, 1>(t, n, ch, nch, bx, s);
+    case 2: return go<V, 2>(t, n, ch, nch, bx, s);
+    case 3: return go<V, 3>(t, n, ch, nch, bx, s);
+    case 4: return go<V, 4>(t, n, ch, nch, bx, s);
     default: return hipErrorInvalidValue;
   }
 }
@@ -731,10 +974,12 @@ hipError_t launch_m(int m, const TileDesc* t, uint32_t n, hipStream_t s) {
 }  // namespace
 
 hipError_t launch_aggregate_tile_packed(int dtype, int m, const TileDesc* d_tiles,
-                                        uint32_t ntiles, hipStream_t stream) {
-  if (ntiles == 0) return hipSuccess;
-  return dtype == 0 ? launch_m<float>(m, d_tiles, ntiles, stream)
-                    : launch_m<double>(m, d_tiles, ntiles, stream);
+                                        uint32_t ntiles, hipStream_t stream,
+                                        const CursorChunk* d_chunks, uint32_t nchunks,
+                                        uint32_t* bx) {
+  if (ntiles == 0 || (d_chunks && nchunks == 0)) return hipSuccess;
+  return dtype == 0 ? launch_m<float>(m, d_tiles, ntiles, d_chunks, nchunks, bx, stream)
+                    : launch_m<double>(m, d_tiles, ntiles, d_chunks, nchunks, bx, stream);
 }
 
 }  // namespace psg

@@ -274,6 +274,58 @@ class MergePlan:
             pass
 
 
+class NWayMergeBatch:
+    """A batch of independent N-way merges run as one pipeline
+    (psg_nway_create_batch: one launch per stage over every merge).
+
+    merges: [dict(push_keys=[ptr], push_n=[n], push_vals=[[ptr] * m],
+    out_keys=ptr, out_vals=[ptr] * m)]; all device pointers."""
+
+    def __init__(self, device: int, dtype: int, merges, parallel_match: bool = False):
+        self._L = _lib.lib()
+        m = len(merges[0]["out_vals"]) if merges else 0
+        npush = [len(x["push_keys"]) for x in merges]
+        keys = [k for x in merges for k in x["push_keys"]]
+        ns = [n for x in merges for n in x["push_n"]]
+        vals = [v for x in merges for vs in x["push_vals"] for v in vs]
+        np_ = (C.c_int * max(1, len(npush)))(*npush)
+        pk = _lib.ptr_array(keys) if keys else None
+        pn = (C.c_uint64 * max(1, len(ns)))(*ns)
+        pv = _lib.ptr_array(vals) if m and vals else None
+        ok = _lib.ptr_array([x["out_keys"] for x in merges])
+        ov = _lib.ptr_array([v for x in merges for v in x["out_vals"]]) if m else None
+        self._keep = [np_, pk, pn, pv, ok, ov]
+        self.nmerge = len(merges)
+        h = C.c_void_p()
+        flags = PSG_PARALLEL_MATCH if parallel_match else PSG_SERIAL_MATCH
+        _lib.check(self._L.psg_nway_create_batch(device, dtype, m, flags, len(merges), np_, pk, pn,
+                                                 pv, ok, ov, C.byref(h)))
+        self._h = h
+        b, kv = C.c_uint64(), C.c_uint64()
+        _lib.check(self._L.psg_nway_bytes(h, C.byref(b), C.byref(kv)))
+        self.bytes_in, self.kv_pairs = b.value, kv.value
+
+    def run(self, stream: Optional[int] = None) -> None:
+        _lib.check(self._L.psg_nway_run(self._h, stream or None))
+
+    def result(self) -> List[int]:
+        """Synchronises; the merged key count of each merge."""
+        n = (C.c_uint64 * self.nmerge)()
+        _lib.check(self._L.psg_nway_result(self._h, n))
+        return list(n)
+
+    def close(self):
+        if getattr(self, "_h", None):
+            self._L.psg_nway_destroy(self._h)
+            self._h = None
+
+    def __del__(self):  # pragma: no cover
+        try:
+            self.close()
+        except Exception:
+            pass
+
+
 class NWayMerge:
     """A prepared N-way merge (psg_nway_*): the union of sorted device
     pushes and, with values, their per-key sums in arrival order.

@@ -1042,3 +1042,102 @@ def test_plan_cursor_unsorted_push_is_reported(torch_cuda):
         mt = plan.matched().tolist()
         assert mt[4] < 40000 and mt[:4] == [40000] * 4 and mt[5:] == [40000] * 3
         plan.close()
+
+
+def _pcursor_check(torch, cases, parallel, dtype=np.float32, flags=0, reps=2):
+    """Plan over `cases` in the packed cursor form: every value array and
+    matched count against the oracle, `reps` runs into the same buffers."""
+    from parameter_server_amd._lib import PSG_KERNEL_PACKED_CURSOR
+    m = len(cases[0][1][0][1])
+    plan, keep = plan_for(torch, cases, dtype=dtype, parallel=parallel, flags=flags)
+    assert plan.form == PSG_KERNEL_PACKED_CURSOR
+    for _ in range(reps):
+        plan.run()
+        mt = plan.matched().tolist()
+        want_mt = []
+        for j, (Dj, pushes) in enumerate(cases):
+            _, _, _, want, wm = O.aggregate(Dj, *ALL, pushes, parallel, m, dtype)
+            want_mt += [int(x) for x in wm]
+            for i in range(m):
+                assert_bitexact(keep[4 * j + 3][i].cpu().numpy()[: Dj.size], want[i])
+        assert mt == want_mt
+    plan.close()
+
+
+def _open_end_case(seed, npush, density, nD, dtype, m):
+    """Sparse pushes over a D whose last key is 2^64 - 1 (the open last tile)."""
+    rng = np.random.default_rng(seed)
+    D = np.unique(np.concatenate([rng.integers(1 << 63, (1 << 64) - 1, nD, dtype=np.uint64),
+                                  np.array([(1 << 64) - 1], np.uint64)]))
+    pushes = []
+    for p in range(npush):
+        k = np.sort(rng.choice(D, int(rng.binomial(D.size, density)), replace=False))
+        if p == 1:
+            k = np.unique(np.concatenate([k, D[-3:]]))
+        pushes.append((k, [rng.standard_normal(k.size).astype(dtype) for _ in range(m)]))
+    return D, pushes
+
+
+@pytest.mark.parametrize("parallel", [False, True])
+@pytest.mark.parametrize("dtype,m", [(np.float32, 1), (np.float64, 2)])
+def test_plan_packed_cursor_form(torch_cuda, parallel, dtype, m):
+    """The packed kernel's cursor form (psg_tile_packed.hip, CUR: no
+    partition pass; a workgroup walks a chunk of 2048-slot tiles and two
+    lanes per push find each piece from the push's cursor), chosen by
+    default for packed plans of <= 256 pushes: bit-exact with the oracle's
+    serialSetValue / parallelSetValue and matched counts over three jobs of
+    one plan (chunk seams inside and between jobs): 256 sparse pushes with
+    one dense push among them (pieces past 16 keys: the 16-key steps) and
+    an empty one; 20 pushes; a D ending at 2^64 - 1 (the open last tile);
+    a second run into the same buffers."""
+    torch = torch_cuda
+    D1, p1 = random_case(4101, dtype, m, 256, 0.004, 300_000)
+    rng = np.random.default_rng(5)
+    k = np.sort(rng.choice(D1, D1.size // 20, replace=False))
+    p1[17] = (k, [rng.standard_normal(k.size).astype(dtype) for _ in range(m)])
+    p1[40] = (np.zeros(0, np.uint64), [np.zeros(0, dtype) for _ in range(m)])
+    D2, p2 = random_case(4102, dtype, m, 20, 0.005, 120_000)
+    D3, p3 = _open_end_case(4103, 12, 0.006, 50_000, dtype, m)
+    _pcursor_check(torch_cuda, [(D1, p1), (D2, p2), (D3, p3)], parallel, dtype)
+
+
+def test_plan_packed_cursor_groups_and_unmatched(torch_cuda):
+    """PSG_FORM_PACKED | PSG_FORM_CURSOR on tiles whose elements exceed one
+    pass (256 pushes x ~20 keys per tile: the cursor form's later groups
+    read the piece lengths back from the piece words), and pushes holding
+    keys outside D (below D[0], between server keys, above D[-1]): matched
+    counts and sums equal the oracle's, serial and parallel."""
+    from parameter_server_amd._lib import PSG_FORM_CURSOR, PSG_FORM_PACKED
+    D, pushes = random_case(4104, np.float32, 1, 256, 0.01, 200_000)
+    D2, p2 = random_case(4105, np.float32, 1, 30, 0.004, 150_000)
+    extra = np.array([1, 2, int(D2[100]) + 1, int(D2[-1]) + 3], np.uint64)
+    for i in (3, 11):
+        k, vs = p2[i]
+        k2 = np.unique(np.concatenate([k, extra if i == 3 else extra[2:]]))
+        p2[i] = (k2, [np.random.default_rng(i).standard_normal(k2.size).astype(np.float32)])
+    for parallel in (False, True):
+        _pcursor_check(torch_cuda, [(D, pushes), (D2, p2)], parallel,
+                       flags=PSG_FORM_PACKED | PSG_FORM_CURSOR, reps=1)
+
+
+def test_plan_packed_cursor_unsorted_push_is_reported(torch_cuda):
+    """An unsorted push through the packed cursor form: two keys swapped
+    inside one tile (the order check) and across far-apart tiles (the
+    chunks' cursors disagree at a seam) are both reported (matched < n)
+    while the other pushes of the plan stay exact."""
+    torch = torch_cuda
+    from parameter_server_amd import synth
+    from parameter_server_amd._lib import PSG_KERNEL_PACKED_CURSOR
+    D, pushes = synth.cfg5_shard(1, 8)
+    n = [k.size for k, _ in pushes]
+    for (i, j) in ((100, 101), (50, n[9] - 50)):
+        bad = list(pushes)
+        k = bad[9][0].copy()
+        k[i], k[j] = k[j], k[i]
+        bad[9] = (k, bad[9][1])
+        plan, keep = plan_for(torch, [(D, bad)])
+        assert plan.form == PSG_KERNEL_PACKED_CURSOR
+        plan.run()
+        mt = plan.matched().tolist()
+        assert mt[9] < n[9] and mt[:9] == n[:9] and mt[10:] == n[10:]
+        plan.close()

@@ -222,3 +222,62 @@ def test_key_union_batch_fails_in_later_chunk():
     assert np.array_equal(v.key(0), O.set_union(D, extra))
     assert v.value(0).size == 0
     v.close()
+
+
+def test_nway_batch_of_merges_vs_oracle():
+    """psg_nway_create_batch: independent merges as one pipeline (one
+    launch per stage over all of them): cfg2-shaped merges of different
+    sizes and push counts (8, 3, 64 pushes, one with an empty push, one of
+    keys past 2^63), f64 m = 2, serial and parallel; every merge's union and
+    sums bit-exact against the oracle, its count from psg_nway_result; an
+    unsorted push in one merge of a batch is reported."""
+    import torch
+    from parameter_server_amd import synth
+    from parameter_server_amd._lib import PSG_F64, PSGError, PSG_ERR_UNSORTED
+    from parameter_server_amd.kv_vector import NWayMergeBatch
+    dev = torch.device("cuda", 0)
+    rng = np.random.default_rng(11)
+    cases = [synth.overlap_pushes(41, npush=8, n=40000, dtype=np.float64, m=2)[1],
+             synth.overlap_pushes(42, npush=3, n=70000, overlap=0.5, dtype=np.float64, m=2)[1],
+             synth.overlap_pushes(43, npush=64, n=3000, overlap=0.2, dtype=np.float64, m=2)[1]]
+    hi = [(np.unique(rng.integers(1 << 63, (1 << 64) - 1, 20000, dtype=np.uint64)),) for _ in range(5)]
+    cases.append([(k, [rng.standard_normal(k.size), rng.standard_normal(k.size)]) for (k,) in hi])
+    cases[0][5] = (np.zeros(0, np.uint64), [np.zeros(0), np.zeros(0)])
+    keep, merges = [], []
+    for pushes in cases:
+        dk = [torch.from_numpy(np.ascontiguousarray(k).view(np.int64)).to(dev) for k, _ in pushes]
+        dv = [[torch.from_numpy(np.ascontiguousarray(v, np.float64)).to(dev) for v in vs]
+              for _, vs in pushes]
+        tot = max(1, sum(k.size for k, _ in pushes))
+        ok = torch.full((tot,), -1, dtype=torch.int64, device=dev)
+        ov = [torch.empty(tot, dtype=torch.float64, device=dev) for _ in range(2)]
+        keep += [dk, dv, ok, ov]
+        merges.append(dict(push_keys=[t.data_ptr() for t in dk], push_n=[k.size for k, _ in pushes],
+                           push_vals=[[t.data_ptr() for t in vs] for vs in dv],
+                           out_keys=ok.data_ptr(), out_vals=[t.data_ptr() for t in ov]))
+    for parallel in (False, True):
+        u = NWayMergeBatch(0, PSG_F64, merges, parallel)
+        for _ in range(2):
+            u.run()
+            counts = u.result()
+            for j, pushes in enumerate(cases):
+                D = _union(pushes)
+                assert counts[j] == D.size
+                ok, ov = keep[4 * j + 2], keep[4 * j + 3]
+                assert np.array_equal(ok.cpu().numpy()[: D.size].view(np.uint64), D)
+                rc, lo, hi_, want, _ = O.aggregate(D, *ALL, pushes, parallel, 2, np.float64)
+                assert rc == 0
+                for i in range(2):
+                    assert np.array_equal(_bits(ov[i].cpu().numpy()[lo:hi_]), _bits(want[i]))
+        u.close()
+    # one unsorted push in the second merge: reported by the batch's result
+    bad = np.ascontiguousarray(cases[1][1][0].copy())
+    bad[[10, 11]] = bad[[11, 10]]
+    keep.append(torch.from_numpy(bad.view(np.int64)).to(dev))
+    merges[1]["push_keys"][1] = keep[-1].data_ptr()
+    u = NWayMergeBatch(0, PSG_F64, merges)
+    u.run()
+    with pytest.raises(PSGError) as e:
+        u.result()
+    assert e.value.status == PSG_ERR_UNSORTED
+    u.close()

@@ -218,10 +218,20 @@ def test_key_cache_signature_errors_and_erase():
     v = _kvv()
     v.setValue(_msg(D))
     sig = O.key_signature(k)
-    # carried keys whose crc32c differs from the carried signature: CHECK_EQ (:163)
+    # carried keys whose crc32c differs from the carried signature: CHECK_EQ
+    # (:163), checked on the device (no host wait per message) and reported
+    # by received(t); a key-only message is checked before its union
+    v.setValue(_msg(k, [x], t=1, sig=sig ^ 1))
     with pytest.raises(PSGError) as e:
-        v.setValue(_msg(k, [x], t=1, sig=sig ^ 1))
+        v.received(1)
     assert e.value.status == PSG_ERR_SIGNATURE
+    with pytest.raises(PSGError) as e:
+        v.setValue(_msg(k, [], t=1, sig=sig ^ 1))
+    assert e.value.status == PSG_ERR_SIGNATURE
+    v.setValue(_msg(k, [x], t=1, sig=sig))  # a good one at the same time: clean
+    (_, got), = v.received(1)
+    assert np.array_equal(_bits(got), _bits(O.aggregate(D, 0, (1 << 64) - 1, [(k, [x])])[3][0]))
+    v.clear_key_cache()
     # restore without an entry, signature != 0: CHECK_EQ(sig, cache.first) (:174)
     with pytest.raises(PSGError) as e:
         v.setValue(_msg(None, [x], t=1, sig=sig, has_key=False))
