@@ -608,6 +608,7 @@ def cfg5_unsliced(args, rank, world, bounds, dist, dev, local, stream, pushes, D
         plan = MergePlan(local, PSG_F32, 1, [job])
         x.run(sh)
         plan.run(sh)
+        ref_bits = res.view(torch.int32).clone()
         if not args.no_check:
             assert np.array_equal(plan.matched(), np.array([c for _, c in pcs], np.uint64))
             assert x.status() == 0
@@ -622,6 +623,16 @@ def cfg5_unsliced(args, rank, world, bounds, dist, dev, local, stream, pushes, D
         wall_max, kv_all = reduce_over_ranks(wall, plan.kv_pairs, dist, dev)
         assert int(kv_all) == kv_total
         assert args.no_check or x.status() == 0
+        # A/B of the transport: peer-bound pieces sent straight from the push
+        # arrays (psg_exchange_set_direct) instead of packed first; the same
+        # received bytes, checked against the packed run's merge
+        x.set_direct(True)
+        x.run(sh)
+        plan.run(sh)
+        if not args.no_check:
+            assert torch.equal(res.view(torch.int32), ref_bits), "direct exchange differs"
+        wall_d, (x_ms_direct,) = timed_stages([lambda: x.run(sh)], K, 2, stream, dist)
+        x.set_direct(False)
         _, _, send_cnt = x.send_layout()
         per_dest = send_cnt.sum(axis=1) * 12  # keys + f32 values
         peers = [s for s in range(world) if s != rank]
@@ -631,7 +642,8 @@ def cfg5_unsliced(args, rank, world, bounds, dist, dev, local, stream, pushes, D
         res_out = {
             "value": kv_total * K / wall_max,
             "ms_per_step": wall_max / K * 1e3,
-            "rank0": {"exchange_ms": x_ms, "partition_ms": part_ms, "kernel_ms": agg_ms,
+            "rank0": {"exchange_ms": x_ms, "exchange_ms_direct": x_ms_direct,
+                      "partition_ms": part_ms, "kernel_ms": agg_ms,
                       "pushes_held": b - a, "bytes_sent_to_peers": to_peers,
                       "bytes_kept_local": int(per_dest[rank]),
                       "max_bytes_to_one_peer": peer_max,

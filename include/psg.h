@@ -83,8 +83,8 @@ typedef enum psg_dtype { PSG_F32 = 0, PSG_F64 = 1 } psg_dtype;
 #define PSG_NO_DENSE 0x40000u     /* never the dense (contiguous-slice) kernel */
 #define PSG_NO_ZERO_COPY 0x80000u /* context: DMA copies instead of GPU reads of pinned memory */
 #define PSG_NO_INDEX 0x100000u    /* plan: no resident bucket index (tables built per run) */
-#define PSG_FORM_CURSOR 0x400000u /* plan: a cursor form (no partition pass) whenever it applies */
-#define PSG_NO_CURSOR 0x800000u   /* plan: never a cursor form (partition + aggregate kernel) */
+#define PSG_FORM_CURSOR 0x400000u /* plan: a cursor form (no partition pass) where it applies */
+#define PSG_NO_CURSOR 0x800000u   /* plan: never a cursor form (the default) */
 /* Plan option (psg_plan_create): the caller promises that the push KEYS at
  * the job's device pointers stay as they were at creation for the plan's
  * lifetime (values may change between runs).  Only then may the plan take
@@ -358,6 +358,12 @@ int psg_exchange_destroy(psg_exchange* x);
  * run's stream and returns PSG_ERR_SIZE (*changed = that count) if any run
  * saw one.  The run's pieces are then those of the create-time cut. */
 int psg_exchange_status(psg_exchange* x, uint64_t* changed);
+/* Direct mode (on != 0; communicator exchanges only): a run sends every
+ * peer-bound piece straight from the push arrays (one send per piece and
+ * array, the receiver posts the matching receives in the same order) instead
+ * of packing them into the send buffer first; own pieces are still packed
+ * into the receive buffers.  Same received layout and bytes either way. */
+int psg_exchange_set_direct(psg_exchange* x, int on);
 /* The same slice-and-pack for nshards virtual shards on one device with no
  * communicator ("8 shards on 1 device"): a run re-cuts and packs
  * only; psg_exchange_send_layout gives the packed buffers (device) and

@@ -146,6 +146,7 @@ SIGNATURES = {
     "psg_exchange_status": (C.c_int, [_p, _pu64]),
     "psg_exchange_create_local": (C.c_int, [C.c_int, C.c_int, C.c_int, C.c_int, C.c_int, _p,
                                             _p, _p, C.POINTER(_p)]),
+    "psg_exchange_set_direct": (C.c_int, [_p, C.c_int]),
     "psg_exchange_send_layout": (C.c_int, [_p, C.POINTER(_p), _p, _p]),
     "psg_key_union_batch": (C.c_int, [_p, C.c_int, _p, _p, C.c_int]),
     "psg_nway_max_push": (C.c_int, []),

@@ -339,6 +339,15 @@ struct psg_exchange {
   const uint64_t* d_pos = nullptr;     // the layout's cut positions [p][S + 1]
   unsigned long long* d_bad = nullptr; // positions that differed in a run's re-cut
   uint64_t nchunks = 0, nsend = 0, nrecv = 0;
+  // direct mode (psg_exchange_set_direct): peer-bound pieces go to the
+  // transport straight from the push arrays (one send per piece and array),
+  // only this rank's own pieces are packed
+  bool direct = false;
+  std::vector<const uint64_t*> hkeys;  // the pushes (host copies of the tables)
+  std::vector<const void*> hvals;
+  std::vector<uint64_t> hpos;          // cut positions [p][S + 1]
+  uint64_t* d_chunks_own = nullptr;    // chunks of the own pieces
+  uint64_t nchunks_own = 0;
   hipStream_t last = nullptr;          // stream of the last run
 };
 
@@ -494,7 +503,7 @@ int exchange_create(psg_comm* comm, int device, int S, int dtype, int m, int npu
   x->send_tot.assign(S, 0);
   x->send_off.assign(S, 0);
   std::vector<Piece> pieces;
-  std::vector<uint64_t> chunks;
+  std::vector<uint64_t> chunks, chunks_own;
   uint64_t off = 0;
   // this rank's own pieces (a communicator's rank) go straight to the
   // receive buffers: their offsets there (push order, from recv_off[rank])
@@ -512,8 +521,11 @@ int exchange_create(psg_comm* comm, int device, int S, int dtype, int m, int npu
           err = fail(PSG_ERR_ARG, "too many pieces (> 2^24)");
           break;
         }
-        for (uint64_t q = 0; q * kChunk < c; ++q) chunks.push_back((uint64_t)pieces.size() << 24 | q);
         const bool mine = s == self;
+        for (uint64_t q = 0; q * kChunk < c; ++q) {
+          chunks.push_back((uint64_t)pieces.size() << 24 | q);
+          if (mine) chunks_own.push_back((uint64_t)pieces.size() << 24 | q);
+        }
         pieces.push_back(Piece{a, mine ? own : off, c, (uint32_t)p, mine ? 1u : 0u});
       }
       if (s == self) own += c;  // own pieces take no send-buffer space
@@ -592,6 +604,7 @@ int exchange_create(psg_comm* comm, int device, int S, int dtype, int m, int npu
   const size_t b_rvp = b; b += al(8 * (size_t)m);
   const size_t b_pc = b; b += al(sizeof(Piece) * pieces.size());
   const size_t b_ch = b; b += al(8 * chunks.size());
+  const size_t b_cho = b; b += al(8 * chunks_own.size());
   const size_t b_n = b; b += al(8 * (size_t)P);
   const size_t b_bd = b; b += al(8 * (size_t)S1);
   const size_t b_pos = b; b += al(8 * (size_t)P * S1);
@@ -613,6 +626,11 @@ int exchange_create(psg_comm* comm, int device, int S, int dtype, int m, int npu
   x->d_rvals = (void* const*)(d + b_rvp);
   x->d_pieces = (Piece*)(d + b_pc);
   x->d_chunks = (uint64_t*)(d + b_ch);
+  x->d_chunks_own = (uint64_t*)(d + b_cho);
+  x->nchunks_own = chunks_own.size();
+  x->hkeys.assign(push_keys, push_keys + P);
+  x->hvals.assign(push_vals, push_vals + (size_t)P * m);
+  x->hpos = pos;
   x->d_n = (const uint64_t*)(d + b_n);
   x->d_bounds = (const uint64_t*)(d + b_bd);
   x->d_pos = (const uint64_t*)(d + b_pos);
@@ -632,6 +650,9 @@ int exchange_create(psg_comm* comm, int device, int S, int dtype, int m, int npu
                          hipMemcpyHostToDevice, st));
   if (!chunks.empty())
     X_TRY(hipMemcpyAsync(d + b_ch, chunks.data(), 8 * chunks.size(), hipMemcpyHostToDevice, st));
+  if (!chunks_own.empty())
+    X_TRY(hipMemcpyAsync(d + b_cho, chunks_own.data(), 8 * chunks_own.size(),
+                         hipMemcpyHostToDevice, st));
 #undef X_TRY
   *out = x;
   return done(PSG_OK);
@@ -669,17 +690,42 @@ int psg_exchange_run(psg_exchange* x, void* stream) {
                        x->d_n, x->d_bounds, S1, x->P, nullptr, x->d_pos, x->d_bad);
     HIP_TRY(hipGetLastError());
   }
-  if (x->nchunks) {
-    const uint64_t blocks = x->nchunks < 4096 ? x->nchunks : 4096;
+  const bool direct = x->direct && x->comm;
+  const uint64_t nch = direct ? x->nchunks_own : x->nchunks;
+  if (nch) {
+    const uint64_t blocks = nch < 4096 ? nch : 4096;
     hipLaunchKernelGGL(pack_kernel, dim3((uint32_t)blocks), dim3(256), 0, st, x->d_pieces,
-                       x->d_chunks, x->nchunks, x->d_keys, x->d_vals, x->m, vb, x->skeys,
-                       x->d_svals, x->rkeys, x->d_rvals);
+                       direct ? x->d_chunks_own : x->d_chunks, nch, x->d_keys, x->d_vals, x->m,
+                       vb, x->skeys, x->d_svals, x->rkeys, x->d_rvals);
     HIP_TRY(hipGetLastError());
   }
   if (!x->comm) return PSG_OK;  // local shards: the packed buffers are the result
   std::vector<XOp> ops;
+  const int S1 = x->S + 1;
   for (int s = 0; s < x->S; ++s) {
     if (s == x->comm->rank) continue;  // own pieces were packed into the receive buffers
+    if (direct) {
+      // per push in order: its keys, then its m value arrays -- the
+      // receiver posts the same sequence (the count round told it the
+      // sizes), so RCCL pairs them one to one
+      for (int p = 0; p < x->P; ++p) {
+        const uint64_t a = x->hpos[(size_t)p * S1 + s], c = x->send_cnt[(size_t)s * x->P + p];
+        if (!c) continue;
+        ops.push_back(XOp{true, s, (void*)(x->hkeys[p] + a), 8 * c});
+        for (int i = 0; i < x->m; ++i)
+          ops.push_back(XOp{true, s, (char*)x->hvals[(size_t)p * x->m + i] + a * vb, (size_t)vb * c});
+      }
+      uint64_t o = x->recv_off[s];
+      for (int p = 0; p < x->P; ++p) {
+        const uint64_t c = x->recv_cnt[(size_t)s * x->P + p];
+        if (!c) continue;
+        ops.push_back(XOp{false, s, x->rkeys + o, 8 * c});
+        for (int i = 0; i < x->m; ++i)
+          ops.push_back(XOp{false, s, (char*)x->rvals[i] + o * vb, (size_t)vb * c});
+        o += c;
+      }
+      continue;
+    }
     if (x->send_tot[s]) {
       ops.push_back(XOp{true, s, x->skeys + x->send_off[s], 8 * x->send_tot[s]});
       for (int a = 0; a < x->m; ++a)
@@ -694,6 +740,13 @@ int psg_exchange_run(psg_exchange* x, void* stream) {
     }
   }
   return xport_group(x->comm, st, ops);
+}
+
+int psg_exchange_set_direct(psg_exchange* x, int on) {
+  if (!x) return fail(PSG_ERR_ARG, "null exchange");
+  if (!x->comm) return fail(PSG_ERR_ARG, "direct mode needs a communicator");
+  x->direct = on != 0;
+  return PSG_OK;
 }
 
 int psg_exchange_status(psg_exchange* x, uint64_t* changed) {

@@ -13,11 +13,15 @@
 //         arrival order, and the serial path adds one +0.0 when some push
 //         lacked the key (the dense `+=` of absent pushes).
 //
-// Pipeline (one stream, no host wait; psg_union_run):
-//   1. candidates: every s-th key of every push; its global rank
-//      R(c) = sum_q lower_bound(push q, c)                     (nw_cand)
+// Pipeline (one stream, no host wait; psg_nway_run):
+//   0. candidates: every s-th key of every push, gathered into one array
+//                                                              (nw_gather)
+//   1. its rank estimate A(c) = s * sum_q (candidates of push q below c):
+//      searches of the small, cached candidate lists instead of the pushes
+//      (R(c) = sum_q lower_bound(push q, c) lies in [A, A + K(s - 1)])
+//                                                              (nw_cand)
 //   2. splitter of rank bucket b = the largest candidate with
-//      floor(R / C') == b (atomic max on the key: R is monotone in the key)
+//      floor(A / C') == b (atomic max on the key: A is monotone in the key)
 //                                                              (nw_bucket)
 //   3. prefix max over the buckets (empty buckets: empty tiles) (nw_split)
 //   4. per (tile, push) the piece bounds: lower_bound of the splitters
@@ -33,11 +37,12 @@
 //        in ticket order) for the global offset;
 //      - segmented sum of each run in push order; the merged keys and sums
 //        staged compacted in LDS and written coalesced.
-// Tile size: a candidate every s keys of each push puts consecutive
-// candidates at most K*s ranks apart, so every rank bucket of width C' has a
-// candidate and a tile spans at most C' + K*s + K elements (equal keys of K
-// pushes at its start) <= kCap: no tile overflows, whatever the key
-// distribution.
+// Tile size: tile t holds R(split[t]) - R(split[t-1]) elements.
+// R(split[t]) <= A(split[t]) + K(s-1) < (t+1) C' + K(s-1); the candidate
+// after split[t-1] in key order lies in bucket >= t and at most K
+// candidates (one per push) equal split[t-1], so A(split[t-1]) >= t C' - K s;
+// hence a tile spans at most C' + 2 K s - K elements <= kCap (C' = kCap -
+// 2 K s): no tile overflows, whatever the key distribution.
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
@@ -65,7 +70,8 @@ struct NwArgs {
   const void* const* vals;      // [K * M] push values (M > 0)
   const uint64_t* n;            // [K]
   const uint64_t* cbase;        // [K + 1] first candidate of each push
-  uint32_t* rank;               // [ncand] R(c)
+  uint64_t* candk;              // [ncand] candidate keys, push by push
+  uint32_t* rank;               // [ncand] A(c)
   uint64_t* split;              // [B] splitter keys
   uint32_t* seg;                // [(T + 1) * K] piece starts, tile-major
   unsigned long long* state;    // [T] look-back words
@@ -121,10 +127,21 @@ __host__ __device__ __forceinline__ uint32_t cand_lanes(uint32_t K) {
   return p;
 }
 
-// 1. R(c) for every candidate c: a wave holds 64 / kp candidates, lane r of
-// a candidate's kp lanes takes lower_bound(push r, c) (interpolation probes,
-// the pushes being near-uniform hashed keys, then a bisection: any key
-// distribution is exact), and the kp lanes sum them: no atomics
+// 0. the candidates: candidate i of push q is its key (i + 1) s - 1
+__global__ __launch_bounds__(256) void nw_gather_kernel(NwBatch b, uint64_t ncand) {
+  const uint64_t g = (uint64_t)blockIdx.x * 256u + threadIdx.x;
+  if (g >= ncand) return;
+  const uint32_t j = merge_of(b.cpre, b.nm, g);
+  const NwArgs& a = b.args[j];
+  const uint64_t c = g - b.cpre[j];
+  const uint32_t q = owner(a, c);
+  a.candk[c] = a.keys[q][(c - a.cbase[q]) * a.s + a.s - 1];
+}
+
+// 1. A(c) for every candidate c: a wave holds 64 / kp candidates, lane r of
+// a candidate's kp lanes counts push r's candidates below it (interpolation
+// probes -- pushes of hashed keys are near-uniform -- then a bisection:
+// exact for any key distribution) and the kp lanes sum them: no atomics
 __global__ __launch_bounds__(256) void nw_cand_kernel(NwBatch b, uint64_t nwaves) {
   const uint64_t wv = ((uint64_t)blockIdx.x * 256u + threadIdx.x) >> 6;
   if (wv >= nwaves) return;
@@ -135,9 +152,8 @@ __global__ __launch_bounds__(256) void nw_cand_kernel(NwBatch b, uint64_t nwaves
   const uint32_t r = lane % kp;
   uint32_t l = 0;
   if (c < a.ncand && r < K) {
-    const uint32_t q = owner(a, c);
-    const uint64_t key = a.keys[q][(c - a.cbase[q]) * a.s + a.s - 1];
-    l = (uint32_t)dev::interp_lower_bound(a.keys[r], a.n[r], key);
+    const uint64_t c0 = a.cbase[r];
+    l = a.s * (uint32_t)dev::interp_lower_bound(a.candk + c0, a.cbase[r + 1] - c0, a.candk[c]);
   }
   for (uint32_t d = 1; d < kp; d <<= 1) l += (uint32_t)__shfl_xor((int)l, (int)d, 64);
   if (c < a.ncand && r == 0) a.rank[c] = l;
@@ -150,8 +166,7 @@ __global__ __launch_bounds__(256) void nw_bucket_kernel(NwBatch b, uint64_t ncan
   const uint32_t j = merge_of(b.cpre, b.nm, g);
   const NwArgs& a = b.args[j];
   const uint64_t c = g - b.cpre[j];
-  const uint32_t q = owner(a, c);
-  const uint64_t key = a.keys[q][(c - a.cbase[q]) * a.s + a.s - 1];
+  const uint64_t key = a.candk[c];
   const uint32_t bk = a.rank[c] / a.cw;
   if (bk < a.B) atomicMax((unsigned long long*)a.split + bk, (unsigned long long)key);
 }
@@ -213,7 +228,8 @@ __global__ __launch_bounds__(kNT) void nw_tile_kernel(NwBatch bt) {
   __shared__ uint16_t si[kCap];                               // source position of each key
   __shared__ __attribute__((aligned(16))) V sv[kM][kVC];      // values by source position
   __shared__ uint32_t roff[kMaxRuns + 1];                     // run offsets (never changed)
-  __shared__ uint32_t pstart[kMaxRuns];                       // piece start in its push
+  __shared__ const uint64_t* pkey[kMaxRuns];                  // piece starts (keys)
+  __shared__ const V* pval[kMaxRuns * kM];                    // piece starts (values)
   __shared__ uint32_t wsum[kNT / 64];
   __shared__ uint32_t sh_t, sh_err;
   __shared__ unsigned long long sh_base;
@@ -239,7 +255,10 @@ __global__ __launch_bounds__(kNT) void nw_tile_kernel(NwBatch bt) {
     if ((uint32_t)lane < K) {
       const uint32_t s0 = a.seg[(size_t)t * K + lane], s1 = a.seg[(size_t)(t + 1) * K + lane];
       len = s1 > s0 ? s1 - s0 : 0u;
-      pstart[lane] = s0;
+      pkey[lane] = a.keys[lane] + s0;
+#pragma unroll
+      for (int mi = 0; mi < M; ++mi)
+        pval[lane * M + mi] = (const V*)a.vals[(size_t)lane * M + mi] + s0;
     }
     uint32_t x = len;
 #pragma unroll
@@ -264,37 +283,64 @@ __global__ __launch_bounds__(kNT) void nw_tile_kernel(NwBatch bt) {
   }
   const uint32_t E = uni(roff[K]);
 
-  // ---- load the pieces: keys, source positions, values
-  for (uint32_t q = 0; q < K; ++q) {
-    const uint32_t o = roff[q], len = roff[q + 1] - o;
-    const uint64_t* kp = a.keys[q] + pstart[q];
-    for (uint32_t e = tid; e < len; e += kNT) {
-      sk[o + e] = kp[e];
-      si[o + e] = (uint16_t)(o + e);
-#pragma unroll
-      for (int mi = 0; mi < M; ++mi)
-        sv[mi][o + e] = ((const V*)a.vals[(size_t)q * M + mi] + pstart[q])[e];
-    }
-  }
-  __syncthreads();
-  // order check: each piece strictly increasing and inside the tile's key
-  // range [split[t-1], split[t]), so the pieces concatenate to the sorted
-  // pushes (std::set_union's precondition)
+  // ---- load the pieces: thread tid takes elements [8 tid, 8 tid + 8) of
+  // the concatenated pieces (one search of the run offsets, then a walk), so
+  // every load of the tile is in flight at once; then keys, source
+  // positions and values into LDS, and the order check: each piece strictly
+  // increasing and inside the tile's key range [split[t-1], split[t]), so
+  // the pieces concatenate to the sorted pushes (std::set_union's
+  // precondition)
   uint32_t viol = 0;
   {
+    const uint32_t e0 = (uint32_t)tid * kPer;
+    uint32_t q = 0;
+    {
+      uint32_t hi = K;  // the last q with roff[q] <= e0
+      while (hi - q > 1) {
+        const uint32_t mid = (q + hi) >> 1;
+        if (roff[mid] <= e0) q = mid; else hi = mid;
+      }
+    }
+    uint64_t kk[kPer];
+    V vv[kPer][kM];
+    uint32_t qs = 0;  // bit x: element e0 + x starts a piece
+#pragma unroll
+    for (int x = 0; x < kPer; ++x) {
+      const uint32_t e = e0 + x;
+      kk[x] = 0;
+#pragma unroll
+      for (int mi = 0; mi < kM; ++mi) vv[x][mi] = V(0);
+      if (e < E) {
+        while (roff[q + 1] <= e) ++q;
+        const uint32_t i = e - roff[q];
+        qs |= (uint32_t)(i == 0u) << x;
+        kk[x] = pkey[q][i];
+#pragma unroll
+        for (int mi = 0; mi < M; ++mi) vv[x][mi] = pval[q * M + mi][i];
+      }
+    }
     const uint64_t klo = t > 0 ? a.split[t - 1] : 0ull;
     const bool open = t + 1 >= a.T;
     const uint64_t khi = open ? ~0ull : a.split[t];
-    for (uint32_t q = 0; q < K; ++q) {
-      const uint32_t o = roff[q], len = roff[q + 1] - o;
-      for (uint32_t e = tid; e < len; e += kNT) {
-        const uint64_t k = sk[o + e];
-        const bool ok = k >= klo && (open || k < khi) && (e == 0 || sk[o + e - 1] < k);
-        viol += ok ? 0u : 1u;
+#pragma unroll
+    for (int x = 0; x < kPer; ++x) {
+      const uint32_t e = e0 + x;
+      if (e < E) {
+        sk[e] = kk[x];
+        si[e] = (uint16_t)e;
+#pragma unroll
+        for (int mi = 0; mi < M; ++mi) sv[mi][e] = vv[x][mi];
+        // within the thread's run: the previous element from registers; at
+        // a piece start only the range; the run's first element against the
+        // previous thread's last, after the barrier
+        const bool inr = kk[x] >= klo && (open || kk[x] < khi);
+        const bool ord = x == 0 || ((qs >> x) & 1u) || kk[x - 1] < kk[x];
+        viol += inr && ord ? 0u : 1u;
       }
     }
+    __syncthreads();
+    if (e0 < E && e0 > 0 && !(qs & 1u) && !(sk[e0 - 1] < kk[0])) ++viol;
   }
-
   // ---- merge-path tree: round `width` merges runs [r0, r0 + width) and
   // [r0 + width, r0 + 2 width) (original run indices; the offsets of merged
   // runs are original run offsets); stable, so equal keys keep push order
@@ -505,13 +551,14 @@ struct NwShape {
     K = k;
     uint64_t ntot = 0;
     for (uint32_t q = 0; q < K; ++q) ntot += pn[q];
-    s = K <= 16 ? std::max<uint32_t>(1, kCap / (8 * std::max<uint32_t>(K, 1))) : 16u;
-    cw = kCap - K * s - K;
+    s = std::max<uint32_t>(1, kCap / (8 * std::max<uint32_t>(K, 1)));
+    cw = kCap - 2 * K * s;
     cbase.assign(K + 1, 0);
     for (uint32_t q = 0; q < K; ++q) cbase[q + 1] = cbase[q] + pn[q] / s;
     ncand = cbase[K];
     B = (uint32_t)(ntot / cw + 1);
     T = B + 1;
+    if (K == 0) B = T = 0;  // no pushes: no work, the merged count stays 0
   }
   uint64_t waves() const { return (ncand + 64 / cand_lanes(K) - 1) / (64 / cand_lanes(K)); }
 };
@@ -525,7 +572,7 @@ struct NwLayout {
   uint32_t nm = 0;
   int m = 0;
   std::vector<NwShape> sh;
-  struct Off { size_t k, v, n, cb, ov, rank, split, state, seg; };
+  struct Off { size_t k, v, n, cb, ov, rank, split, state, seg, candk; };
   std::vector<Off> off;
   size_t o_args = 0, o_pre = 0, o_zero = 0, o_ticket = 0, o_misc = 0, zero_len = 0, bytes = 0;
   uint64_t nwaves = 0, ncand = 0, nseg = 0, ntiles = 0;
@@ -563,6 +610,8 @@ struct NwLayout {
     for (uint32_t j = 0; j < nm; ++j) {
       off[j].seg = o;
       o = al256(o + 4 * (size_t)(sh[j].T + 1) * sh[j].K);
+      off[j].candk = o;
+      o = al256(o + 8 * sh[j].ncand);
     }
     bytes = o;
     nwaves = ncand = nseg = ntiles = 0;
@@ -616,6 +665,7 @@ struct NwLayout {
       A.vals = (const void* const*)(b + f.v);
       A.n = (const uint64_t*)(b + f.n);
       A.cbase = (const uint64_t*)(b + f.cb);
+      A.candk = (uint64_t*)(b + f.candk);
       A.out_vals = (void* const*)(b + f.ov);
       A.rank = (uint32_t*)(b + f.rank);
       A.split = (uint64_t*)(b + f.split);
@@ -651,14 +701,17 @@ hipError_t nway_enqueue(char* b, const NwLayout& L, int dtype, hipStream_t st) {
   if (e != hipSuccess || L.ntiles == 0) return e;
   const NwBatch B = L.batch(b);
   if (L.ncand) {
+    hipLaunchKernelGGL(nw_gather_kernel, dim3((uint32_t)((L.ncand + 255) / 256)), dim3(256), 0, st,
+                       B, L.ncand);
     hipLaunchKernelGGL(nw_cand_kernel, dim3((uint32_t)((L.nwaves + 3) / 4)), dim3(256), 0, st, B,
                        L.nwaves);
     hipLaunchKernelGGL(nw_bucket_kernel, dim3((uint32_t)((L.ncand + 255) / 256)), dim3(256), 0, st,
                        B, L.ncand);
   }
   hipLaunchKernelGGL(nw_split_kernel, dim3(L.nm), dim3(256), 0, st, B);
-  hipLaunchKernelGGL(nw_seg_kernel, dim3((uint32_t)((L.nseg + 255) / 256)), dim3(256), 0, st, B,
-                     L.nseg);
+  if (L.nseg)
+    hipLaunchKernelGGL(nw_seg_kernel, dim3((uint32_t)((L.nseg + 255) / 256)), dim3(256), 0, st, B,
+                       L.nseg);
   if ((e = hipGetLastError()) != hipSuccess) return e;
   return dtype == PSG_F32 ? launch_tile_m<float>(L.m, B, L.ntiles, st)
                           : launch_tile_m<double>(L.m, B, L.ntiles, st);

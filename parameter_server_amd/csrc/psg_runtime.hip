@@ -320,10 +320,9 @@ struct JobTable {
     // the cursor form: plans (resident index) of search-mode jobs of at most
     // kCursorPushes pushes whose pieces fit kr <= 3 rounds (mean + 4 sigma
     // keys per push per tile <= 192; longer ones would finish round by round)
-    // explicit partition / round-form flags select the partition path
-    // unless PSG_FORM_CURSOR is given too
-    cursor = index && !dense && !pack && !wide && knob_cursor != 0 && tiles > 0 &&
-             (knob_cursor == 1 || (knob_part < 0 && knob_pack < 0));
+    // opt-in (PSG_FORM_CURSOR): measured slower than partition + tile
+    // kernel on cfg2 (0.509 vs 0.437 ms per step)
+    cursor = index && !dense && !pack && !wide && knob_cursor == 1 && tiles > 0;
     for (size_t j = 0; cursor && j < jobs.size(); ++j) {
       const JobSpec& s = jobs[j];
       JobInfo& I = info[j];
@@ -347,8 +346,9 @@ struct JobTable {
     // at most 256 pushes whose pointers leave the top 16 bits free (the
     // kernel keeps a piece's length there) and whose tiles' elements fit one
     // pass (mean + 6 sigma <= 2,560; larger ones take more groups per tile)
-    pcursor = index && !dense && pack && knob_cursor != 0 && tiles > 0 &&
-              (knob_cursor == 1 || (knob_part < 0 && knob_pack < 0));
+    // opt-in (PSG_FORM_CURSOR): measured slower than partition + packed
+    // kernel on cfg5 (1.34 vs 0.77 ms per step)
+    pcursor = index && !dense && pack && knob_cursor == 1 && tiles > 0;
     for (size_t j = 0; pcursor && j < jobs.size(); ++j) {
       const JobSpec& s = jobs[j];
       const JobInfo& I = info[j];

@@ -279,6 +279,12 @@ class RcclExchange:
         flat = self.recv_cnt.reshape(-1)
         self.recv_off = (np.cumsum(flat) - flat).reshape(world, self.P)
 
+    def set_direct(self, on: bool = True) -> None:
+        """psg_exchange_set_direct: peer-bound pieces sent straight from the
+        push arrays (no pack copy)."""
+        from . import _lib
+        _lib.check(self._L.psg_exchange_set_direct(self._h, 1 if on else 0))
+
     def run(self, stream=None) -> None:
         from . import _lib
         _lib.check(self._L.psg_exchange_run(self._h, stream))

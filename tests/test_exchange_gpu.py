@@ -204,8 +204,9 @@ def _threads(fns):
     return res, err
 
 
-@pytest.mark.parametrize("dtype,m", [(np.float32, 1), (np.float64, 2)])
-def test_loopback_8_ranks_exchange_then_hip_merge(dtype, m):
+@pytest.mark.parametrize("dtype,m,direct", [(np.float32, 1, False), (np.float64, 2, False),
+                                            (np.float32, 1, True)])
+def test_loopback_8_ranks_exchange_then_hip_merge(dtype, m, direct):
     """The multi-rank exchange at S = 8 ranks (psg_comm_init_loopback: 8
     ranks of one process on one GPU, one host thread each), cfg5-shaped
     pushes (murmur-shuffled uniform ranks, 8 whole pushes per rank): the
@@ -215,7 +216,9 @@ def test_loopback_8_ranks_exchange_then_hip_merge(dtype, m):
     evenDivide(8) of every source's pushes, the received keys/values are
     those pieces in (source, push) order, and the HIP plan's merge of them
     equals the oracle's aggregate over the rank's key range, bit for bit.
-    Two runs land in the same buffers."""
+    Two runs land in the same buffers.  `direct`: peer-bound pieces sent
+    straight from the push arrays (psg_exchange_set_direct), one send per
+    piece and array, received in the same layout."""
     import torch
     from parameter_server_amd import shard, synth
     from parameter_server_amd._lib import PSG_F32, PSG_F64
@@ -237,6 +240,8 @@ def test_loopback_8_ranks_exchange_then_hip_merge(dtype, m):
     xs, err = _threads([lambda r=r: shard.RcclExchange(comms[r], held[r], S, vt)
                         for r in range(S)])
     assert not any(err), err
+    for x in xs:
+        x.set_direct(direct)
     streams = [torch.cuda.Stream(device=dev) for _ in range(S)]
     for _ in range(2):
         _, err = _threads([lambda r=r: xs[r].run(streams[r].cuda_stream) for r in range(S)])

@@ -955,6 +955,18 @@ def test_growing_value_array_list(torch_cuda, parallel, flush):
         assert_bitexact(out[i][1], want[0])
 
 
+def _oracle_keys(Dj, pushes):
+    """The oracle's aggregate takes Range::all() = [0, 2^64 - 1) (range.h:
+    75-78); a case whose D ends at 2^64 - 1 (the open last tile) is handed
+    to it with every key shifted down by one: same order, same matches,
+    same fold."""
+    if Dj.size and int(Dj[-1]) == (1 << 64) - 1:
+        assert int(Dj[0]) > 0
+        one = np.uint64(1)
+        return Dj - one, [(k - one, vs) for k, vs in pushes]
+    return Dj, pushes
+
+
 def _cursor_check(torch, cases, parallel, flags=0, want_form=None, reps=2):
     from parameter_server_amd._lib import PSG_KERNEL_CURSOR
     plan, keep = plan_for(torch, cases, parallel=parallel, flags=flags)
@@ -964,7 +976,8 @@ def _cursor_check(torch, cases, parallel, flags=0, want_form=None, reps=2):
         mt = plan.matched().tolist()
         want_mt = []
         for j, (Dj, pushes) in enumerate(cases):
-            rc, _, _, want, wm = O.aggregate(Dj, *ALL, pushes, parallel=parallel)
+            rc, _, _, want, wm = O.aggregate(*_oracle_keys(Dj, pushes)[:1], *ALL,
+                                             _oracle_keys(Dj, pushes)[1], parallel=parallel)
             want_mt += [int(x) for x in wm]
             assert_bitexact(keep[4 * j + 3][0].cpu().numpy()[: Dj.size], want[0])
         assert mt == want_mt
@@ -975,13 +988,14 @@ def _cursor_check(torch, cases, parallel, flags=0, want_form=None, reps=2):
 def test_plan_cursor_form(torch_cuda, parallel):
     """The cursor kernel (psg_tile_cursor.hip: no partition pass; each
     workgroup walks a chunk of tiles with one cursor per push and finds a
-    piece's end with the element loads): chosen by default for plans of
-    long pieces, bit-exact with the oracle's serialSetValue /
+    piece's end with the element loads), PSG_FORM_CURSOR on plans of long
+    pieces, bit-exact with the oracle's serialSetValue /
     parallelSetValue and matched counts, over 8, 3 and 20 pushes (groups of
     8, idle waves), 1-3 rounds per push, one- and many-tile chunks, D ending
     at 2^64 - 1 (the open last tile) and a second run."""
     torch = torch_cuda
     from parameter_server_amd import synth
+    from parameter_server_amd._lib import PSG_FORM_CURSOR
     rng = np.random.default_rng(123)
     Dh = np.unique(np.concatenate([rng.integers(1 << 63, (1 << 64) - 1, 30000, dtype=np.uint64),
                                    np.array([(1 << 64) - 1], np.uint64)]))
@@ -993,8 +1007,8 @@ def test_plan_cursor_form(torch_cuda, parallel):
     cases = [synth.overlap_pushes(31, npush=8, n=40000),            # cfg2-like: 3 rounds
              synth.overlap_pushes(33, npush=20, n=12000, overlap=0.5),  # 3 groups
              (Dh, hp),                                                 # open end, 2^64 - 1
-             synth.overlap_pushes(34, npush=6, n=2000, overlap=0.3)]    # 9 tiles
-    _cursor_check(torch, cases, parallel)
+             synth.overlap_pushes(34, npush=8, n=2000)]                 # 15 tiles
+    _cursor_check(torch, cases, parallel, flags=PSG_FORM_CURSOR)
 
 
 def test_plan_cursor_long_pieces_and_unmatched(torch_cuda):
@@ -1030,13 +1044,13 @@ def test_plan_cursor_unsorted_push_is_reported(torch_cuda):
     pushes of the same plan stay exact."""
     torch = torch_cuda
     from parameter_server_amd import synth
+    from parameter_server_amd._lib import PSG_FORM_CURSOR, PSG_KERNEL_CURSOR
     D, pushes = synth.overlap_pushes(35, npush=8, n=40000)
     for (i, j) in ((100, 101), (500, 39000)):
         bad = [(k.copy(), vs) for k, vs in pushes]
         k = bad[4][0]
         k[i], k[j] = k[j], k[i]
-        plan, keep = plan_for(torch, [(D, bad)])
-        from parameter_server_amd._lib import PSG_KERNEL_CURSOR
+        plan, keep = plan_for(torch, [(D, bad)], flags=PSG_FORM_CURSOR)
         assert plan.form == PSG_KERNEL_CURSOR
         plan.run()
         mt = plan.matched().tolist()
@@ -1044,10 +1058,11 @@ def test_plan_cursor_unsorted_push_is_reported(torch_cuda):
         plan.close()
 
 
-def _pcursor_check(torch, cases, parallel, dtype=np.float32, flags=0, reps=2):
+def _pcursor_check(torch, cases, parallel, dtype=np.float32, flags=None, reps=2):
     """Plan over `cases` in the packed cursor form: every value array and
     matched count against the oracle, `reps` runs into the same buffers."""
-    from parameter_server_amd._lib import PSG_KERNEL_PACKED_CURSOR
+    from parameter_server_amd._lib import PSG_KERNEL_PACKED_CURSOR, PSG_FORM_CURSOR
+    flags = PSG_FORM_CURSOR if flags is None else flags
     m = len(cases[0][1][0][1])
     plan, keep = plan_for(torch, cases, dtype=dtype, parallel=parallel, flags=flags)
     assert plan.form == PSG_KERNEL_PACKED_CURSOR
@@ -1056,7 +1071,8 @@ def _pcursor_check(torch, cases, parallel, dtype=np.float32, flags=0, reps=2):
         mt = plan.matched().tolist()
         want_mt = []
         for j, (Dj, pushes) in enumerate(cases):
-            _, _, _, want, wm = O.aggregate(Dj, *ALL, pushes, parallel, m, dtype)
+            Do, po = _oracle_keys(Dj, pushes)
+            _, _, _, want, wm = O.aggregate(Do, *ALL, po, parallel, m, dtype)
             want_mt += [int(x) for x in wm]
             for i in range(m):
                 assert_bitexact(keep[4 * j + 3][i].cpu().numpy()[: Dj.size], want[i])
@@ -1084,7 +1100,7 @@ def test_plan_packed_cursor_form(torch_cuda, parallel, dtype, m):
     """The packed kernel's cursor form (psg_tile_packed.hip, CUR: no
     partition pass; a workgroup walks a chunk of 2048-slot tiles and two
     lanes per push find each piece from the push's cursor), chosen by
-    default for packed plans of <= 256 pushes: bit-exact with the oracle's
+    PSG_FORM_CURSOR on packed plans of <= 256 pushes: bit-exact with the oracle's
     serialSetValue / parallelSetValue and matched counts over three jobs of
     one plan (chunk seams inside and between jobs): 256 sparse pushes with
     one dense push among them (pieces past 16 keys: the 16-key steps) and
@@ -1127,7 +1143,7 @@ def test_plan_packed_cursor_unsorted_push_is_reported(torch_cuda):
     while the other pushes of the plan stay exact."""
     torch = torch_cuda
     from parameter_server_amd import synth
-    from parameter_server_amd._lib import PSG_KERNEL_PACKED_CURSOR
+    from parameter_server_amd._lib import PSG_KERNEL_PACKED_CURSOR, PSG_FORM_CURSOR
     D, pushes = synth.cfg5_shard(1, 8)
     n = [k.size for k, _ in pushes]
     for (i, j) in ((100, 101), (50, n[9] - 50)):
@@ -1135,7 +1151,7 @@ def test_plan_packed_cursor_unsorted_push_is_reported(torch_cuda):
         k = bad[9][0].copy()
         k[i], k[j] = k[j], k[i]
         bad[9] = (k, bad[9][1])
-        plan, keep = plan_for(torch, [(D, bad)])
+        plan, keep = plan_for(torch, [(D, bad)], flags=PSG_FORM_CURSOR)
         assert plan.form == PSG_KERNEL_PACKED_CURSOR
         plan.run()
         mt = plan.matched().tolist()
