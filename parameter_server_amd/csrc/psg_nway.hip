@@ -219,6 +219,15 @@ __global__ __launch_bounds__(256) void nw_seg_kernel(NwBatch b, uint64_t nseg) {
 constexpr uint64_t kFlagAgg = 1ull << 62, kFlagPre = 2ull << 62;
 constexpr uint64_t kValMask = (1ull << 62) - 1;
 
+#ifdef PSG_NWAY_PROF
+// diagnostic build only (tools/nway_probe.py --prof): per tile (first 65,536
+// tickets), shader clocks at the phase boundaries of nw_tile_kernel
+__device__ unsigned long long g_nwprof[65536][8];
+#define NP_MARK(i) np_t[i] = clock64()
+#else
+#define NP_MARK(i) do { } while (0)
+#endif
+
 // 5. the tile merge
 template <typename V, int M>
 __global__ __launch_bounds__(kNT) void nw_tile_kernel(NwBatch bt) {
@@ -234,6 +243,9 @@ __global__ __launch_bounds__(kNT) void nw_tile_kernel(NwBatch bt) {
   __shared__ uint32_t sh_t, sh_err;
   __shared__ unsigned long long sh_base;
   const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+#ifdef PSG_NWAY_PROF
+  unsigned long long np_t[8];
+#endif
 
   // ---- ticket: tiles in dispatch order (the look-back waits only on
   // tickets taken by workgroups that are already running), then its merge
@@ -249,6 +261,7 @@ __global__ __launch_bounds__(kNT) void nw_tile_kernel(NwBatch bt) {
   const uint32_t K = a.K;
   const bool parallel = (a.flags & kFlagParallel) != 0;
 
+  NP_MARK(0);
   // ---- piece table: wave 0, one lane per push
   if (w == 0) {
     uint32_t len = 0;
@@ -283,6 +296,7 @@ __global__ __launch_bounds__(kNT) void nw_tile_kernel(NwBatch bt) {
   }
   const uint32_t E = uni(roff[K]);
 
+  NP_MARK(1);
   // ---- load the pieces: thread tid takes elements [8 tid, 8 tid + 8) of
   // the concatenated pieces (one search of the run offsets, then a walk), so
   // every load of the tile is in flight at once; then keys, source
@@ -341,14 +355,25 @@ __global__ __launch_bounds__(kNT) void nw_tile_kernel(NwBatch bt) {
     __syncthreads();
     if (e0 < E && e0 > 0 && !(qs & 1u) && !(sk[e0 - 1] < kk[0])) ++viol;
   }
+  NP_MARK(2);
   // ---- merge-path tree: round `width` merges runs [r0, r0 + width) and
   // [r0 + width, r0 + 2 width) (original run indices; the offsets of merged
   // runs are original run offsets); stable, so equal keys keep push order
   const uint32_t k0 = (uint32_t)tid * kPer;
+  // this thread's 8 outputs of the last round stay in registers (the run
+  // heads and the segmented sums read them there)
+  uint64_t rk[kPer];
+  uint16_t ri[kPer];
+  if (K <= 1) {  // one run: already in order
+#pragma unroll
+    for (int x = 0; x < kPer; ++x) {
+      rk[x] = k0 + x < E ? sk[k0 + x] : 0ull;
+      ri[x] = k0 + x < E ? si[k0 + x] : (uint16_t)0;
+    }
+  }
   for (uint32_t width = 1; width < K; width <<= 1) {
-    uint64_t rk[kPer];
-    uint16_t ri[kPer];
     uint32_t A0 = 0, B0 = 0, B1 = 0, i = 0, j = 0;  // current pair and merge position
+    uint64_t ka = 0, kb = 0;                         // sk[A0 + i], sk[B0 + j] (when in range)
 #pragma unroll
     for (int x = 0; x < kPer; ++x) {
       const uint32_t k = k0 + x;
@@ -373,14 +398,21 @@ __global__ __launch_bounds__(kNT) void nw_tile_kernel(NwBatch bt) {
           }
           i = lo;
           j = d - lo;
+          ka = i < la ? sk[A0 + i] : 0ull;
+          kb = j < lb ? sk[B0 + j] : 0ull;
         }
+        // one LDS key read per output: the side taken advances
         const uint32_t la = B0 - A0, lb = B1 - B0;
-        const bool takeA = j >= lb || (i < la && sk[A0 + i] <= sk[B0 + j]);
-        const uint32_t src = takeA ? A0 + i : B0 + j;
-        rk[x] = sk[src];
-        ri[x] = si[src];
-        i += takeA ? 1u : 0u;
-        j += takeA ? 0u : 1u;
+        const bool takeA = j >= lb || (i < la && ka <= kb);
+        rk[x] = takeA ? ka : kb;
+        ri[x] = si[takeA ? A0 + i : B0 + j];
+        if (takeA) {
+          ++i;
+          ka = i < la ? sk[A0 + i] : 0ull;
+        } else {
+          ++j;
+          kb = j < lb ? sk[B0 + j] : 0ull;
+        }
       }
     }
     __syncthreads();
@@ -393,14 +425,17 @@ __global__ __launch_bounds__(kNT) void nw_tile_kernel(NwBatch bt) {
     __syncthreads();
   }
 
+  NP_MARK(3);
   // ---- run heads (a key differing from the previous one), unique index
   uint32_t heads = 0, nh = 0;
+  {
+    const uint64_t before = k0 > 0 && k0 < E ? sk[k0 - 1] : 0ull;
 #pragma unroll
-  for (int x = 0; x < kPer; ++x) {
-    const uint32_t e = k0 + x;
-    if (e < E && (e == 0 || sk[e] != sk[e - 1])) {
-      heads |= 1u << x;
-      ++nh;
+    for (int x = 0; x < kPer; ++x) {
+      const uint32_t e = k0 + x;
+      const bool h = e < E && (e == 0 || (x == 0 ? before : rk[x - 1]) != rk[x]);
+      heads |= (uint32_t)h << x;
+      nh += h ? 1u : 0u;
     }
   }
   uint32_t incl = nh;
@@ -420,48 +455,13 @@ __global__ __launch_bounds__(kNT) void nw_tile_kernel(NwBatch bt) {
     U += wsum[v];
   }
 
-  // ---- decoupled look-back (wave 0): this tile's global offset
-  if (w == 0) {
-    unsigned long long excl = 0;
-    if (t > 0) {
-      if (lane == 0)
-        __hip_atomic_store(a.state + t, kFlagAgg | (unsigned long long)U, __ATOMIC_RELAXED,
-                           __HIP_MEMORY_SCOPE_AGENT);
-      int64_t j = (int64_t)t - 1;
-      uint32_t spins = 0;
-      for (;;) {
-        const int64_t idx = j - lane;  // lane 0: the nearest predecessor
-        const unsigned long long s =
-            idx >= 0 ? __hip_atomic_load(a.state + idx, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)
-                     : kFlagPre;  // before tile 0: an inclusive prefix of 0
-        const unsigned long long fl = s & ~kValMask;
-        const unsigned long long pm = __ballot(fl == kFlagPre);
-        const unsigned long long inv = __ballot(fl == 0);
-        const int fp = pm ? __ffsll((long long)pm) - 1 : 64;
-        const unsigned long long upto = fp >= 63 ? ~0ull : ((2ull << fp) - 1);  // lanes 0..fp
-        if (inv & upto) {  // a predecessor has not published yet
-          if (++spins > (1u << 22)) {  // never expected: report and stop waiting
-            if (lane == 0) atomicAdd(a.bad, 1ull << 40);
-            break;
-          }
-          __builtin_amdgcn_s_sleep(2);
-          continue;
-        }
-        unsigned long long v = ((upto >> lane) & 1ull) ? (s & kValMask) : 0ull;
-        for (int d = 32; d > 0; d >>= 1) v += __shfl_xor(v, d, 64);
-        excl += v;
-        if (fp < 64) break;
-        j -= 64;
-      }
-    }
-    if (lane == 0) {
-      __hip_atomic_store(a.state + t, kFlagPre | (excl + U), __ATOMIC_RELAXED,
-                         __HIP_MEMORY_SCOPE_AGENT);
-      if (t + 1 == a.T) *a.nout = excl + U;
-      sh_base = excl;
-    }
-  }
-
+  NP_MARK(4);
+  // ---- this tile's unique count for the look-back of later tiles: as
+  // early as it is known (the sums below do not need the offset, so they
+  // run while predecessors finish)
+  if (w == 0 && lane == 0 && t > 0)
+    __hip_atomic_store(a.state + t, kFlagAgg | (unsigned long long)U, __ATOMIC_RELAXED,
+                       __HIP_MEMORY_SCOPE_AGENT);
   // ---- segmented sums of this thread's runs, in push order
   uint64_t hk[kPer];
   V hs[kPer][kM];
@@ -471,19 +471,32 @@ __global__ __launch_bounds__(kNT) void nw_tile_kernel(NwBatch bt) {
 #pragma unroll
     for (int mi = 0; mi < kM; ++mi) hs[x][mi] = V(0);
     if ((heads >> x) & 1u) {
-      const uint32_t e = k0 + x;
-      const uint64_t key = sk[e];
+      const uint64_t key = rk[x];
       hk[x] = key;
       if constexpr (M > 0) {
         // the run [e, f): push 0 (run 0's sources) assigns, later pushes
         // add to the memset +0.0 or to it; serial: one trailing +0.0 when
-        // a push lacked the key (kv_vector.h:195-201)
+        // a push lacked the key (kv_vector.h:195-201).  The run's part in
+        // this thread's outputs from registers, the rest (a run crossing
+        // into the next thread's outputs) from LDS
         V acc[M];
 #pragma unroll
         for (int mi = 0; mi < M; ++mi) acc[mi] = V(0);
         const uint32_t p0 = roff[1];
-        uint32_t f = e, cnt = 0;
-        while (f < E && sk[f] == key) {
+        uint32_t cnt = 0;
+        bool open = true;
+#pragma unroll
+        for (int y = x; y < kPer; ++y) {
+          open = open && k0 + y < E && rk[y] == key;
+          if (open) {
+            const uint32_t src = ri[y];
+#pragma unroll
+            for (int mi = 0; mi < M; ++mi) acc[mi] = src < p0 ? sv[mi][src] : acc[mi] + sv[mi][src];
+            ++cnt;
+          }
+        }
+        uint32_t f = k0 + kPer;
+        while (open && f < E && sk[f] == key) {
           const uint32_t src = si[f];
 #pragma unroll
           for (int mi = 0; mi < M; ++mi) acc[mi] = src < p0 ? sv[mi][src] : acc[mi] + sv[mi][src];
@@ -496,6 +509,60 @@ __global__ __launch_bounds__(kNT) void nw_tile_kernel(NwBatch bt) {
       }
     }
   }
+  NP_MARK(5);
+  // ---- decoupled look-back (wave 0): this tile's global offset
+  if (w == 0) {
+    unsigned long long excl = 0;
+    if (t > 0) {
+      // 256 predecessors per step (4 per lane, lane l at distances 4l..4l+3,
+      // the loads independent): the nearest inclusive prefix ends the sum
+      int64_t j = (int64_t)t - 1;
+      uint32_t spins = 0;
+      for (;;) {
+        unsigned long long st4[4];
+        int dpre = 1 << 30, dinv = 1 << 30;  // nearest inclusive / unpublished
+#pragma unroll
+        for (int c = 0; c < 4; ++c) {
+          const int d = 4 * lane + c;
+          const int64_t idx = j - d;
+          st4[c] = idx >= 0 ? __hip_atomic_load(a.state + idx, __ATOMIC_RELAXED,
+                                                __HIP_MEMORY_SCOPE_AGENT)
+                            : kFlagPre;  // before tile 0: an inclusive prefix of 0
+          const unsigned long long fl = st4[c] & ~kValMask;
+          if (fl == kFlagPre && d < dpre) dpre = d;
+          if (fl == 0 && d < dinv) dinv = d;
+        }
+        for (int o = 32; o > 0; o >>= 1) {
+          const int x = __shfl_xor(dpre, o, 64), y = __shfl_xor(dinv, o, 64);
+          dpre = x < dpre ? x : dpre;
+          dinv = y < dinv ? y : dinv;
+        }
+        if (dinv < dpre && dinv < 256) {  // a predecessor has not published yet
+          if (++spins > (1u << 22)) {  // never expected: report and stop waiting
+            if (lane == 0) atomicAdd(a.bad, 1ull << 40);
+            break;
+          }
+          __builtin_amdgcn_s_sleep(2);
+          continue;
+        }
+        unsigned long long v = 0;
+#pragma unroll
+        for (int c = 0; c < 4; ++c)
+          if (4 * lane + c <= dpre) v += st4[c] & kValMask;
+        for (int d = 32; d > 0; d >>= 1) v += __shfl_xor(v, d, 64);
+        excl += v;
+        if (dpre < 256) break;
+        j -= 256;
+      }
+    }
+    if (lane == 0) {
+      __hip_atomic_store(a.state + t, kFlagPre | (excl + U), __ATOMIC_RELAXED,
+                         __HIP_MEMORY_SCOPE_AGENT);
+      if (t + 1 == a.T) *a.nout = excl + U;
+      sh_base = excl;
+    }
+  }
+
   __syncthreads();  // every read of sk / si / sv is done; sh_base is set
   // compacted: unique u of the tile at LDS position u
   {
@@ -511,12 +578,18 @@ __global__ __launch_bounds__(kNT) void nw_tile_kernel(NwBatch bt) {
     }
   }
   __syncthreads();
+  NP_MARK(6);
   const unsigned long long base = sh_base;
   for (uint32_t e = tid; e < U; e += kNT) {
     a.out_keys[base + e] = sk[e];
 #pragma unroll
     for (int mi = 0; mi < M; ++mi) ((V*)a.out_vals[mi])[base + e] = sv[mi][e];
   }
+  NP_MARK(7);
+#ifdef PSG_NWAY_PROF
+  if (tid == 0 && g < 65536u)
+    for (int i = 0; i < 8; ++i) g_nwprof[g][i] = np_t[i];
+#endif
 }
 
 template <typename V, int M>
@@ -831,6 +904,13 @@ int nway_create(int device, int dtype, int m, unsigned flags, int nmerge, const 
 }  // namespace
 
 extern "C" {
+
+#ifdef PSG_NWAY_PROF
+int psg_debug_nway_prof(unsigned long long* out, uint32_t n) {
+  if (n > 65536) n = 65536;
+  return hipMemcpyFromSymbol(out, HIP_SYMBOL(psg::g_nwprof), (size_t)n * 64) == hipSuccess ? 0 : -1;
+}
+#endif
 
 int psg_nway_max_push(void) { return psg::kMaxRuns; }
 

@@ -2,18 +2,10 @@
 set -o pipefail
 export TMPDIR=/tmp
 R=r04; O=gpurun_out/$R; mkdir -p $O
-timeout -k 10 600 python3 -u -m pytest tests -m gpu -x -q --timeout 180 --timeout-method thread > $O/gputest.log 2>&1 || { echo TESTFAIL; tail -30 $O/gputest.log; exit 1; }
-tail -1 $O/gputest.log
-timeout -k 10 300 python3 -c "import __graft_entry__ as g; g.smoke()" > $O/smoke.log 2>&1 || { echo SMOKEFAIL; tail -20 $O/smoke.log; exit 1; }
-tail -1 $O/smoke.log
-timeout -k 10 600 python3 bench.py > $O/bench.json 2> $O/bench.err || { echo "bench failed"; tail -5 $O/bench.err; exit 1; }
-python3 -c "
-import json;d=json.load(open('$O/bench.json'));r=d['roofline']
-print('cfg2 %.3e ms %.4f kern %.4f part %.4f frac %.3f step %.3f'%(d['value'],d['ms_per_step'],r['kernel_ms'],r['partition_ms'],r['frac'],r['step_frac']))
-print('f64', json.dumps(d.get('f64'))[:300])
-print('cfg5', json.dumps(d.get('cfg5'))[:600])
-print('rows', json.dumps({k:(v.get('ms'),v.get('frac')) for k,v in d.get('rows',{}).items()}))
-print('e2e', json.dumps({k:v.get('value') for k,v in d.get('end_to_end',{}).items()}))
-print('cpu', json.dumps(d.get('cpu_baseline')))
-"
+timeout -k 10 300 python3 -u -m pytest tests/test_nway_gpu.py -x -q -m gpu --timeout 120 --timeout-method thread > $O/nway_test.log 2>&1 || { echo TESTFAIL; tail -30 $O/nway_test.log; exit 1; }
+tail -1 $O/nway_test.log
+timeout -k 10 300 python3 tools/nway_probe.py > $O/nway_probe.log 2>&1 || { echo "probe failed"; tail -5 $O/nway_probe.log; exit 1; }
+tail -1 $O/nway_probe.log
+PSG_LIB_PATH=build/nwprof/libpsg.so timeout -k 10 300 python3 tools/nway_probe.py --prof --reps 3 > $O/nway_prof.log 2>&1 || { echo "probe failed"; tail -5 $O/nway_prof.log; exit 1; }
+tail -9 $O/nway_prof.log
 echo done
