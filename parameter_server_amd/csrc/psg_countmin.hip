@@ -10,6 +10,16 @@
 // query = min over probes, starting from 255; queryKeys keeps, in input
 // order, the keys whose query is > freqency.
 //
+// Insert, binned (the default when the filter's scratch holds the records):
+// the table is cut into 32 KB regions; a counting pass finds how many probes
+// land in each region, a scatter pass writes every probe as a 4-byte record
+// (offset in the region, count) into its region's list, and an apply pass
+// gives each region one workgroup that adds its records into u32 LDS
+// counters (native LDS adds: a counter's low byte is its sum mod 2^8) and
+// then adds those sums into the region's bytes -- each table byte is read
+// and written once, with no global atomics per probe (the CAS form below
+// makes one device-scope atomic per probe, the bound of its rate).
+//
 // GPU form.  The table is the reference's: n_ bytes (countmin.h:69,
 // SArray<uint8>), 64 MB for 2^26 counters, so it stays resident in the
 // 256 MB Infinity Cache while keys stream past.  There is no byte-wide
@@ -66,6 +76,136 @@ __device__ __forceinline__ uint32_t cm_query(const uint8_t* __restrict__ t, uint
 }
 
 constexpr int kProbeRegs = 8;  // probes held in registers (k <= 8: every app's k)
+
+// ---- binned insert ----
+constexpr uint32_t kRegShift = 15;                 // 32 KB of table per region
+constexpr uint32_t kRegBytes = 1u << kRegShift;
+constexpr uint32_t kMaxRegions = 4096;             // tables up to 128 MB binned
+constexpr int kBinNT = 256;
+constexpr int kBinKPT = 64;                        // keys per thread: 16 K keys per workgroup
+constexpr int kApplyNT = 1024;
+
+// probes of key i (count c != 0) -> fn(region, offset in region, c)
+template <typename F>
+__device__ __forceinline__ void probes(uint64_t key, uint32_t n, int k, F fn) {
+  uint32_t h = cm_hash(key);
+  const uint32_t delta = (h >> 17) | (h << 15);
+  for (int j = 0; j < k; ++j) {
+    const uint32_t idx = h % n;
+    fn(idx >> kRegShift, idx & (kRegBytes - 1u));
+    h += delta;
+  }
+}
+
+// pass 1: probes per region (an LDS histogram per workgroup, then one
+// global add per region)
+__global__ __launch_bounds__(kBinNT) void cm_bin_count_kernel(const uint64_t* __restrict__ keys,
+                                                              const uint32_t* __restrict__ counts,
+                                                              uint64_t nk, uint32_t n, int k,
+                                                              uint32_t nreg,
+                                                              uint32_t* __restrict__ rcount) {
+  __shared__ uint32_t hst[kMaxRegions];
+  for (uint32_t r = threadIdx.x; r < nreg; r += kBinNT) hst[r] = 0;
+  __syncthreads();
+  const uint64_t b0 = (uint64_t)blockIdx.x * kBinNT * kBinKPT + threadIdx.x;
+  for (int i = 0; i < kBinKPT; ++i) {
+    const uint64_t x = b0 + (uint64_t)i * kBinNT;
+    if (x < nk && (counts[x] & 0xffu))
+      probes(keys[x], n, k, [&](uint32_t r, uint32_t) { atomicAdd(&hst[r], 1u); });
+  }
+  __syncthreads();
+  for (uint32_t r = threadIdx.x; r < nreg; r += kBinNT)
+    if (hst[r]) atomicAdd(rcount + r, hst[r]);
+}
+
+// pass 2: exclusive scan of the region counts (one workgroup) into rbase,
+// and the reservation cursors rcur = rbase
+__global__ __launch_bounds__(kBinNT) void cm_bin_scan_kernel(const uint32_t* __restrict__ rcount,
+                                                             uint32_t nreg,
+                                                             uint32_t* __restrict__ rbase,
+                                                             uint32_t* __restrict__ rcur) {
+  __shared__ uint32_t ws[kBinNT / 64];
+  __shared__ uint32_t carry;
+  if (threadIdx.x == 0) carry = 0;
+  __syncthreads();
+  for (uint32_t b = 0; b < nreg; b += kBinNT) {
+    const uint32_t i = b + threadIdx.x;
+    const uint32_t v = i < nreg ? rcount[i] : 0u;
+    uint32_t tot;
+    const uint32_t ex = dev::block_excl_scan<kBinNT>(v, ws, &tot);
+    const uint32_t c0 = carry;
+    if (i < nreg) {
+      rbase[i] = c0 + ex;
+      rcur[i] = c0 + ex;
+    }
+    __syncthreads();
+    if (threadIdx.x == 0) carry = c0 + tot;
+    __syncthreads();
+  }
+  if (threadIdx.x == 0) rbase[nreg] = carry;
+}
+
+// pass 3: the records, region by region (a workgroup reserves its space in
+// every region with one atomic per region, then places its records with
+// LDS atomics); the keys are read again (the same workgroup's chunk)
+__global__ __launch_bounds__(kBinNT) void cm_bin_scatter_kernel(
+    const uint64_t* __restrict__ keys, const uint32_t* __restrict__ counts, uint64_t nk,
+    uint32_t n, int k, uint32_t nreg, uint32_t* __restrict__ rcur, uint32_t* __restrict__ recs) {
+  __shared__ uint32_t hst[kMaxRegions];
+  __shared__ uint32_t base[kMaxRegions];
+  for (uint32_t r = threadIdx.x; r < nreg; r += kBinNT) hst[r] = 0;
+  __syncthreads();
+  const uint64_t b0 = (uint64_t)blockIdx.x * kBinNT * kBinKPT + threadIdx.x;
+  for (int i = 0; i < kBinKPT; ++i) {
+    const uint64_t x = b0 + (uint64_t)i * kBinNT;
+    if (x < nk && (counts[x] & 0xffu))
+      probes(keys[x], n, k, [&](uint32_t r, uint32_t) { atomicAdd(&hst[r], 1u); });
+  }
+  __syncthreads();
+  for (uint32_t r = threadIdx.x; r < nreg; r += kBinNT) {
+    base[r] = hst[r] ? atomicAdd(rcur + r, hst[r]) : 0u;
+    hst[r] = 0;
+  }
+  __syncthreads();
+  for (int i = 0; i < kBinKPT; ++i) {
+    const uint64_t x = b0 + (uint64_t)i * kBinNT;
+    if (x >= nk) continue;
+    const uint32_t c = counts[x] & 0xffu;
+    if (c)
+      probes(keys[x], n, k, [&](uint32_t r, uint32_t o) {
+        recs[base[r] + atomicAdd(&hst[r], 1u)] = o | c << kRegShift;
+      });
+  }
+}
+
+// pass 4: one workgroup per region: the records into u32 LDS sums, then the
+// region's bytes += sum (mod 2^8); bytes past the table untouched
+__global__ __launch_bounds__(kApplyNT) void cm_bin_apply_kernel(
+    uint8_t* __restrict__ t, uint32_t tbytes, const uint32_t* __restrict__ rbase,
+    const uint32_t* __restrict__ recs) {
+  __shared__ uint32_t acc[kRegBytes];
+  const uint32_t r = blockIdx.x;
+  for (uint32_t i = threadIdx.x; i < kRegBytes; i += kApplyNT) acc[i] = 0;
+  __syncthreads();
+  const uint32_t a = rbase[r], b = rbase[r + 1];
+  for (uint32_t i = a + threadIdx.x; i < b; i += kApplyNT) {
+    const uint32_t v = recs[i];
+    __hip_atomic_fetch_add(&acc[v & (kRegBytes - 1u)], v >> kRegShift, __ATOMIC_RELAXED,
+                           __HIP_MEMORY_SCOPE_WORKGROUP);
+  }
+  __syncthreads();
+  // dwords of the region (the table is a whole number of dwords)
+  uint32_t* tw = (uint32_t*)(t + (size_t)r * kRegBytes);
+  const uint32_t nw = (tbytes - r * kRegBytes < kRegBytes ? tbytes - r * kRegBytes : kRegBytes) / 4u;
+  for (uint32_t i = threadIdx.x; i < nw; i += kApplyNT) {
+    const uint32_t w = tw[i];
+    uint32_t o = 0;
+#pragma unroll
+    for (int j = 0; j < 4; ++j)
+      o |= ((((w >> (8 * j)) & 0xffu) + acc[4 * i + j]) & 0xffu) << (8 * j);
+    tw[i] = o;
+  }
+}
 
 __device__ __forceinline__ uint32_t byte_add(uint32_t w, uint32_t sh, uint32_t c) {
   const uint32_t nb = ((w >> sh) + c) & 0xffu;
@@ -191,9 +331,36 @@ __global__ __launch_bounds__(kNT) void cm_scatter_kernel(const uint64_t* __restr
 
 }  // namespace
 
+size_t cm_insert_scratch_bytes(uint64_t nk, uint32_t n, int k) {
+  const uint64_t nreg = (cm_table_bytes(n) + kRegBytes - 1) / kRegBytes;
+  if (nreg > kMaxRegions || nk * (uint64_t)k >= (1ull << 32)) return 0;  // CAS form
+  return 256 + 4 * 3 * (nreg + 1) + 4 * nk * (uint64_t)k;
+}
+
 hipError_t launch_cm_insert(const uint64_t* keys, const uint32_t* counts, uint64_t nk,
-                            uint8_t* table, uint32_t n, int k, hipStream_t s) {
+                            uint8_t* table, uint32_t n, int k, void* bins, size_t bins_bytes,
+                            hipStream_t s) {
   if (nk == 0) return hipSuccess;
+  const size_t need = cm_insert_scratch_bytes(nk, n, k);
+  if (need && bins && bins_bytes >= need) {
+    const uint32_t tb = (uint32_t)cm_table_bytes(n);
+    const uint32_t nreg = (tb + kRegBytes - 1) / kRegBytes;
+    uint32_t* rcount = (uint32_t*)bins;
+    uint32_t* rbase = rcount + (nreg + 1);
+    uint32_t* rcur = rbase + (nreg + 1);
+    uint32_t* recs = (uint32_t*)((char*)bins + ((4 * 3 * (size_t)(nreg + 1) + 255) / 256) * 256);
+    const uint64_t chunks = (nk + kBinNT * kBinKPT - 1) / (kBinNT * kBinKPT);
+    hipError_t e = hipMemsetAsync(rcount, 0, 4 * (size_t)nreg, s);
+    if (e != hipSuccess) return e;
+    hipLaunchKernelGGL(cm_bin_count_kernel, dim3((uint32_t)chunks), dim3(kBinNT), 0, s, keys,
+                       counts, nk, n, k, nreg, rcount);
+    hipLaunchKernelGGL(cm_bin_scan_kernel, dim3(1), dim3(kBinNT), 0, s, rcount, nreg, rbase, rcur);
+    hipLaunchKernelGGL(cm_bin_scatter_kernel, dim3((uint32_t)chunks), dim3(kBinNT), 0, s, keys,
+                       counts, nk, n, k, nreg, rcur, recs);
+    hipLaunchKernelGGL(cm_bin_apply_kernel, dim3(nreg), dim3(kApplyNT), 0, s, table, tb, rbase,
+                       recs);
+    return hipGetLastError();
+  }
   hipLaunchKernelGGL(cm_insert_kernel, dim3((uint32_t)((nk + kNT - 1) / kNT)), dim3(kNT), 0, s,
                      keys, counts, nk, table, n, k);
   return hipGetLastError();

@@ -207,8 +207,12 @@ hipError_t launch_popcount(const uint32_t* a, uint64_t nw, unsigned long long* o
 // FreqencyFilter / CountMin<uint64, uint8> (psg_countmin.hip); the table is
 // n byte counters (allocated to a multiple of 4 bytes: dword CAS)
 inline size_t cm_table_bytes(uint32_t n) { return ((size_t)n + 3) & ~(size_t)3; }
+// binned insert scratch (0: the table is too large, the CAS form runs)
+size_t cm_insert_scratch_bytes(uint64_t nk, uint32_t n, int k);
+// bins (nullable): scratch of >= cm_insert_scratch_bytes for the binned form
 hipError_t launch_cm_insert(const uint64_t* keys, const uint32_t* counts, uint64_t nk,
-                            uint8_t* table, uint32_t n, int k, hipStream_t stream);
+                            uint8_t* table, uint32_t n, int k, void* bins, size_t bins_bytes,
+                            hipStream_t stream);
 size_t cm_query_scratch_bytes(uint64_t nk);
 hipError_t launch_cm_query(const uint64_t* keys, uint64_t nk, const uint8_t* table, uint32_t n,
                            int k, int freq, uint64_t* out, unsigned long long* nout,

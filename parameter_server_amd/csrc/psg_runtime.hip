@@ -811,6 +811,11 @@ struct Filter {
   uint8_t* d_table = nullptr;  // n byte counters (countmin.h:69)
   uint32_t n = 0;
   int k = 1;
+  // the binned insert's records (psg_countmin.hip), grown on demand; the
+  // filter's inserts are ordered on one stream (the context's, or the
+  // caller's of psg_freq_insert_dev)
+  void* d_bins = nullptr;
+  size_t bins_bytes = 0;
   // the caller's stream of the last psg_freq_*_dev call: the table is not
   // recycled (clear / resize) before the kernels enqueued there finished
   hipStream_t ext = nullptr;
@@ -1543,6 +1548,7 @@ int psg_destroy(psg_ctx* c) {
   for (auto& kv : c->ff) {
     kv.second.sync_ext();
     c->dev_put(kv.second.d_table, psg::cm_table_bytes(kv.second.n));
+    c->dev_put(kv.second.d_bins, kv.second.bins_bytes);
   }
   c->ff.clear();
   if (c->stream) (void)hipStreamSynchronize(c->stream);
@@ -2359,6 +2365,7 @@ int psg_freq_clear(psg_ctx* c, int chl) {
   if (it != c->ff.end()) {
     it->second.sync_ext();
     c->dev_put(it->second.d_table, psg::cm_table_bytes(it->second.n));
+    c->dev_put(it->second.d_bins, it->second.bins_bytes);
     c->ff.erase(it);
   }
   return PSG_OK;
@@ -2380,6 +2387,20 @@ int filter_of(psg_ctx* c, int chl, Filter** F) {
   *F = &it->second;
   return PSG_OK;
 }
+
+// the binned insert's scratch for n keys (stream s: where the insert runs);
+// a filter too large to bin gets none (the CAS form runs)
+int filter_bins(psg_ctx* c, Filter* F, size_t n, hipStream_t s) {
+  const size_t need = psg::cm_insert_scratch_bytes(n, F->n, F->k);
+  if (need == 0 || need <= F->bins_bytes) return PSG_OK;
+  F->sync_ext();
+  c->dev_put(F->d_bins, F->bins_bytes);
+  F->d_bins = nullptr;
+  F->bins_bytes = 0;
+  if (int rc = c->dev_get(need, &F->d_bins, s)) return rc;
+  F->bins_bytes = need;
+  return PSG_OK;
+}
 }  // namespace
 
 int psg_freq_insert_dev(psg_ctx* c, int chl, const uint64_t* keys, const uint32_t* counts,
@@ -2388,7 +2409,9 @@ int psg_freq_insert_dev(psg_ctx* c, int chl, const uint64_t* keys, const uint32_
   std::lock_guard<std::mutex> l(c->mu);
   Filter* F;
   if (int rc = filter_of(c, chl, &F)) return rc;
-  HIP_TRY(psg::launch_cm_insert(keys, counts, n, F->d_table, F->n, F->k, (hipStream_t)stream));
+  if (int rc = filter_bins(c, F, n, (hipStream_t)stream)) return rc;
+  HIP_TRY(psg::launch_cm_insert(keys, counts, n, F->d_table, F->n, F->k, F->d_bins,
+                                F->bins_bytes, (hipStream_t)stream));
   F->ext = (hipStream_t)stream;
   F->ext_used = true;
   return PSG_OK;
@@ -2425,9 +2448,11 @@ int psg_freq_insert(psg_ctx* c, int chl, const uint64_t* keys, const uint32_t* c
   int rc = c->h2d(blk, keys, 8 * n);
   if (rc == PSG_OK) rc = c->h2d((char*)blk + kb, counts, 4 * n);
   if (rc == PSG_OK) rc = c->join_copy();
+  if (rc == PSG_OK) rc = filter_bins(c, F, n, c->stream);
   if (rc == PSG_OK) {
     hipError_t e = psg::launch_cm_insert((const uint64_t*)blk, (const uint32_t*)((char*)blk + kb),
-                                         n, F->d_table, F->n, F->k, c->stream);
+                                         n, F->d_table, F->n, F->k, F->d_bins, F->bins_bytes,
+                                         c->stream);
     if (e != hipSuccess) rc = fail(PSG_ERR_DEVICE, "freq insert: %s", hipGetErrorString(e));
   }
   c->dev_put(blk, b);

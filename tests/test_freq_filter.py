@@ -169,3 +169,25 @@ def test_gpu_freq_filter_device_entry_points_and_k_clamp():
         got = dout[:m].cpu().numpy().view(np.uint64)
         assert np.array_equal(got, O.ff_query(t, nn, kk, keys, freq))
     v.close()
+
+
+@pytest.mark.gpu
+def test_gpu_freq_filter_large_table_cas_form():
+    """A table past the binned insert's 128 MB (2^27 + 4,096 counters): the
+    per-probe CAS form runs; bytes exact against the oracle, including
+    counters hit by many keys (repeated keys, byte wrap)."""
+    import torch
+    assert torch.cuda.is_available()
+    from parameter_server_amd import _lib
+    rng = np.random.default_rng(8)
+    v = _ctx()
+    n = (1 << 27) + 4096
+    _lib.check(v._L.psg_freq_resize(v._h, 1, n, 3))
+    t, nn, kk = O.cm_resize(n, 3)
+    keys = np.concatenate([rng.integers(0, 1 << 62, 60_000, dtype=np.uint64),
+                           np.full(700, 12345, np.uint64)])
+    counts = rng.integers(1, 300, keys.size).astype(np.uint32)
+    _lib.check(v._L.psg_freq_insert(v._h, 1, keys.ctypes.data, counts.ctypes.data, keys.size))
+    O.cm_insert(t, nn, kk, keys, counts)
+    assert np.array_equal(_table(v, 1, nn), t)
+    v.close()

@@ -1,11 +1,12 @@
 # scratch GPU command of the current step (overwritten per gpurun call)
 set -o pipefail
 export TMPDIR=/tmp
-R=r04; O=gpurun_out/$R; mkdir -p $O
-timeout -k 10 300 python3 -u -m pytest tests/test_nway_gpu.py -x -q -m gpu --timeout 120 --timeout-method thread > $O/nway_test.log 2>&1 || { echo TESTFAIL; tail -30 $O/nway_test.log; exit 1; }
-tail -1 $O/nway_test.log
-timeout -k 10 300 python3 tools/nway_probe.py > $O/nway_probe.log 2>&1 || { echo "probe failed"; tail -5 $O/nway_probe.log; exit 1; }
-tail -1 $O/nway_probe.log
-PSG_LIB_PATH=build/nwprof/libpsg.so timeout -k 10 300 python3 tools/nway_probe.py --prof --reps 3 > $O/nway_prof.log 2>&1 || { echo "probe failed"; tail -5 $O/nway_prof.log; exit 1; }
-tail -9 $O/nway_prof.log
+R=r04; OUT=gpurun_out/$R; mkdir -p $OUT
+timeout -k 10 300 python3 -u -m pytest tests/test_freq_filter.py -x -q -m gpu --timeout 200 --timeout-method thread > $OUT/freq_test.log 2>&1 || { echo TESTFAIL; tail -30 $OUT/freq_test.log; exit 1; }
+tail -1 $OUT/freq_test.log
+timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d $OUT/ktrace_rows2 -o run -- python3 tools/run_rows.py > $OUT/rows2.json 2> $OUT/rows2.err || { echo "rows failed"; tail -5 $OUT/rows2.err; exit 1; }
+python3 -c "
+import json;d=json.load(open('$OUT/rows2.json'))
+print({k:(round(v['ms'],4),round(v['frac'],3)) for k,v in d.items() if k.startswith('countmin')})"
+grep -i "cm_" $OUT/ktrace_rows2/run_kernel_stats.csv | cut -d, -f1-4
 echo done
