@@ -36,6 +36,8 @@
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
+#include <algorithm>
+
 #include "psg_device.h"
 #include "psg_internal.h"
 
@@ -145,36 +147,81 @@ __global__ __launch_bounds__(kBinNT) void cm_bin_scan_kernel(const uint32_t* __r
   if (threadIdx.x == 0) rbase[nreg] = carry;
 }
 
-// pass 3: the records, region by region (a workgroup reserves its space in
-// every region with one atomic per region, then places its records with
-// LDS atomics); the keys are read again (the same workgroup's chunk)
-__global__ __launch_bounds__(kBinNT) void cm_bin_scatter_kernel(
+// pass 3: the records, region by region.  A workgroup (1024 threads)
+// reserves its space in every region with one atomic per region, then takes
+// its keys in sub-chunks whose records fit LDS: counts them per region, lays
+// them out region-major in LDS (a scan and LDS positions), and writes each
+// region's run of records with consecutive stores of one thread, so the
+// lines of the record lists are written whole instead of 4 bytes at a time
+constexpr int kScNT = 1024;
+constexpr uint32_t kScRecs = 24576;  // staged records per sub-chunk (96 KB)
+__global__ __launch_bounds__(kScNT) void cm_bin_scatter_kernel(
     const uint64_t* __restrict__ keys, const uint32_t* __restrict__ counts, uint64_t nk,
-    uint32_t n, int k, uint32_t nreg, uint32_t* __restrict__ rcur, uint32_t* __restrict__ recs) {
-  __shared__ uint32_t hst[kMaxRegions];
+    uint32_t n, int k, uint32_t nreg, uint32_t sub, uint32_t* __restrict__ rcur,
+    uint32_t* __restrict__ recs) {
+  __shared__ uint32_t stg[kScRecs];
+  __shared__ uint32_t start[kMaxRegions + 1];
+  __shared__ uint32_t pos[kMaxRegions];
   __shared__ uint32_t base[kMaxRegions];
-  for (uint32_t r = threadIdx.x; r < nreg; r += kBinNT) hst[r] = 0;
+  __shared__ uint32_t ws[kScNT / 64];
+  const uint32_t t = threadIdx.x;
+  const uint64_t c0 = (uint64_t)blockIdx.x * kBinNT * kBinKPT;  // this workgroup's keys
+  const uint64_t c1 = c0 + kBinNT * kBinKPT < nk ? c0 + kBinNT * kBinKPT : nk;
+  // this workgroup's records per region, then its reservation in each list
+  for (uint32_t r = t; r < nreg; r += kScNT) pos[r] = 0;
   __syncthreads();
-  const uint64_t b0 = (uint64_t)blockIdx.x * kBinNT * kBinKPT + threadIdx.x;
-  for (int i = 0; i < kBinKPT; ++i) {
-    const uint64_t x = b0 + (uint64_t)i * kBinNT;
-    if (x < nk && (counts[x] & 0xffu))
-      probes(keys[x], n, k, [&](uint32_t r, uint32_t) { atomicAdd(&hst[r], 1u); });
-  }
+  for (uint64_t x = c0 + t; x < c1; x += kScNT)
+    if (counts[x] & 0xffu)
+      probes(keys[x], n, k, [&](uint32_t r, uint32_t) { atomicAdd(&pos[r], 1u); });
   __syncthreads();
-  for (uint32_t r = threadIdx.x; r < nreg; r += kBinNT) {
-    base[r] = hst[r] ? atomicAdd(rcur + r, hst[r]) : 0u;
-    hst[r] = 0;
-  }
-  __syncthreads();
-  for (int i = 0; i < kBinKPT; ++i) {
-    const uint64_t x = b0 + (uint64_t)i * kBinNT;
-    if (x >= nk) continue;
-    const uint32_t c = counts[x] & 0xffu;
-    if (c)
-      probes(keys[x], n, k, [&](uint32_t r, uint32_t o) {
-        recs[base[r] + atomicAdd(&hst[r], 1u)] = o | c << kRegShift;
-      });
+  for (uint32_t r = t; r < nreg; r += kScNT) base[r] = pos[r] ? atomicAdd(rcur + r, pos[r]) : 0u;
+  for (uint64_t s0 = c0; s0 < c1; s0 += sub) {
+    const uint64_t s1 = s0 + sub < c1 ? s0 + sub : c1;
+    __syncthreads();  // the previous sub-chunk's writes have read stg / start
+    for (uint32_t r = t; r < nreg; r += kScNT) pos[r] = 0;
+    __syncthreads();
+    for (uint64_t x = s0 + t; x < s1; x += kScNT)
+      if (counts[x] & 0xffu)
+        probes(keys[x], n, k, [&](uint32_t r, uint32_t) { atomicAdd(&pos[r], 1u); });
+    __syncthreads();
+    // exclusive scan of the counts over the regions (4 per thread)
+    {
+      uint32_t v[4], tot = 0;
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        const uint32_t r = 4 * t + j;
+        v[j] = r < nreg ? pos[r] : 0u;
+        tot += v[j];
+      }
+      uint32_t all;
+      uint32_t ex = dev::block_excl_scan<kScNT>(tot, ws, &all);
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        const uint32_t r = 4 * t + j;
+        if (r < nreg) {
+          start[r] = ex;
+          pos[r] = ex;
+        }
+        ex += v[j];
+      }
+      if (t == 0) start[nreg] = all;
+    }
+    __syncthreads();
+    for (uint64_t x = s0 + t; x < s1; x += kScNT) {
+      const uint32_t c = counts[x] & 0xffu;
+      if (c)
+        probes(keys[x], n, k, [&](uint32_t r, uint32_t o) {
+          stg[atomicAdd(&pos[r], 1u)] = o | c << kRegShift;
+        });
+    }
+    __syncthreads();
+    // each thread writes its regions' runs (consecutive stores per run)
+    for (uint32_t r = t; r < nreg; r += kScNT) {
+      const uint32_t a = start[r], e = start[r + 1];
+      uint32_t* dst = recs + base[r];
+      for (uint32_t i = a; i < e; ++i) dst[i - a] = stg[i];
+      base[r] += e - a;
+    }
   }
 }
 
@@ -355,8 +402,10 @@ hipError_t launch_cm_insert(const uint64_t* keys, const uint32_t* counts, uint64
     hipLaunchKernelGGL(cm_bin_count_kernel, dim3((uint32_t)chunks), dim3(kBinNT), 0, s, keys,
                        counts, nk, n, k, nreg, rcount);
     hipLaunchKernelGGL(cm_bin_scan_kernel, dim3(1), dim3(kBinNT), 0, s, rcount, nreg, rbase, rcur);
-    hipLaunchKernelGGL(cm_bin_scatter_kernel, dim3((uint32_t)chunks), dim3(kBinNT), 0, s, keys,
-                       counts, nk, n, k, nreg, rcur, recs);
+    // keys per staged sub-chunk: their records fit the LDS staging area
+    const uint32_t sub = std::max<uint32_t>(1, kScRecs / (uint32_t)k);
+    hipLaunchKernelGGL(cm_bin_scatter_kernel, dim3((uint32_t)chunks), dim3(kScNT), 0, s, keys,
+                       counts, nk, n, k, nreg, sub, rcur, recs);
     hipLaunchKernelGGL(cm_bin_apply_kernel, dim3(nreg), dim3(kApplyNT), 0, s, table, tb, rbase,
                        recs);
     return hipGetLastError();

@@ -2,10 +2,15 @@
 set -o pipefail
 export TMPDIR=/tmp
 R=r04; OUT=gpurun_out/$R; mkdir -p $OUT
-PASSES="1 2 3 4 5 7" ./tools/pmc2.sh $OUT/pmc_cfg5 "--workload cfg5" > $OUT/pmc_cfg5.log 2>&1 || { echo "pmc cfg5 failed"; tail -5 $OUT/pmc_cfg5.log; exit 1; }
-BPL5=$(python3 -c "import json;print(json.load(open('profiles/r04_bench.json'))['cfg5']['rank0']['bytes_per_launch'])") || exit 1
-python3 tools/pmc_traffic.py $OUT/pmc_cfg5/summary.json $BPL5 tile_packed_kernel $OUT/pmc_summary_cfg5.json cfg5 > $OUT/pmc_traffic_cfg5.json || exit 1
-echo pmc cfg5 ok
-./tools/pmc_rows.sh $OUT/pmc_rows > $OUT/pmc_rows.log 2>&1 || { echo "pmc rows failed"; tail -5 $OUT/pmc_rows.log; exit 1; }
-echo pmc rows ok
+timeout -k 10 300 python3 -u -m pytest tests/test_freq_filter.py -x -q -m gpu --timeout 200 --timeout-method thread > $OUT/freq_test.log 2>&1 || { echo TESTFAIL; tail -30 $OUT/freq_test.log; exit 1; }
+tail -1 $OUT/freq_test.log
+timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d $OUT/ktrace_rows3 -o run -- python3 tools/run_rows.py > $OUT/rows3.json 2> $OUT/rows3.err || { echo "rows failed"; tail -5 $OUT/rows3.err; exit 1; }
+python3 -c "
+import json;d=json.load(open('$OUT/rows3.json'))
+print({k:(round(v['ms'],4),round(v['frac'],3)) for k,v in d.items() if k.startswith('countmin')})"
+grep -i "cm_bin" $OUT/ktrace_rows3/run_kernel_stats.csv | cut -d, -f1-4
+PASSES="1 2" ./tools/pmc_rows.sh $OUT/pmc_rows3 > $OUT/pmc_rows3.log 2>&1 || { echo "pmc rows failed"; tail -5 $OUT/pmc_rows3.log; exit 1; }
+python3 -c "
+import json;r=json.load(open('$OUT/pmc_rows3/summary.json'))['counters']
+print({k:round(v.get('hbm_bytes_corrected',0)/1e9,3) for k,v in r.items() if k.startswith('cm_')})"
 echo done
