@@ -17,9 +17,9 @@
 //   0. candidates: every s-th key of every push, gathered into one array
 //                                                              (nw_gather)
 //   1. its rank estimate A(c) = s * sum_q (candidates of push q below c):
-//      searches of the small, cached candidate lists instead of the pushes
-//      (R(c) = sum_q lower_bound(push q, c) lies in [A, A + K(s - 1)])
-//                                                              (nw_cand)
+//      searches of the small candidate lists, staged in LDS, instead of the
+//      pushes (R(c) = sum_q lower_bound(push q, c) lies in [A, A + K(s - 1)])
+//                                                              (nw_rank)
 //   2. splitter of rank bucket b = the largest candidate with
 //      floor(A / C') == b (atomic max on the key: A is monotone in the key)
 //                                                              (nw_bucket)
@@ -92,7 +92,7 @@ struct NwArgs {
 // that are already running.
 struct NwBatch {
   const NwArgs* args;       // [nm]
-  const uint64_t* wpre;     // [nm + 1] candidate waves before merge j
+  const uint64_t* wpre;     // [nm + 1] rank-stage workgroups before merge j
   const uint64_t* cpre;     // [nm + 1] candidates before merge j
   const uint64_t* spre;     // [nm + 1] seg entries ((T + 1) K) before merge j
   const uint64_t* tpre;     // [nm + 1] tiles before merge j
@@ -120,13 +120,6 @@ __device__ __forceinline__ uint32_t owner(const NwArgs& a, uint64_t c) {
   return lo;
 }
 
-// lanes per candidate in the rank stage: K rounded up to a power of two
-__host__ __device__ __forceinline__ uint32_t cand_lanes(uint32_t K) {
-  uint32_t p = 1;
-  while (p < K) p <<= 1;
-  return p;
-}
-
 // 0. the candidates: candidate i of push q is its key (i + 1) s - 1
 __global__ __launch_bounds__(256) void nw_gather_kernel(NwBatch b, uint64_t ncand) {
   const uint64_t g = (uint64_t)blockIdx.x * 256u + threadIdx.x;
@@ -138,25 +131,62 @@ __global__ __launch_bounds__(256) void nw_gather_kernel(NwBatch b, uint64_t ncan
   a.candk[c] = a.keys[q][(c - a.cbase[q]) * a.s + a.s - 1];
 }
 
-// 1. A(c) for every candidate c: a wave holds 64 / kp candidates, lane r of
-// a candidate's kp lanes counts push r's candidates below it (interpolation
-// probes -- pushes of hashed keys are near-uniform -- then a bisection:
-// exact for any key distribution) and the kp lanes sum them: no atomics
-__global__ __launch_bounds__(256) void nw_cand_kernel(NwBatch b, uint64_t nwaves) {
-  const uint64_t wv = ((uint64_t)blockIdx.x * 256u + threadIdx.x) >> 6;
-  if (wv >= nwaves) return;
-  const uint32_t j = uni(merge_of(b.wpre, b.nm, wv));
+// 1. A(c) for every candidate c: a workgroup takes kRkChunk candidates of
+// one merge (16 per thread, in registers) and walks the merge's K candidate
+// lists: each list is staged in LDS (coalesced) and searched there, and the
+// counts are summed in registers -- no atomics, no global search chains.  A
+// list longer than the LDS stage is searched in global memory (interpolation
+// probes, then a bisection: exact for any key distribution).
+constexpr uint32_t kRkPer = 16;
+constexpr uint32_t kRkChunk = 256 * kRkPer;  // candidates per workgroup
+constexpr uint32_t kRkList = 8192;           // candidates of one list staged in LDS (64 KB)
+__global__ __launch_bounds__(256) void nw_rank_kernel(NwBatch b) {
+  __shared__ uint64_t lst[kRkList];
+  const uint32_t item = blockIdx.x;
+  const uint32_t j = uni(merge_of(b.wpre, b.nm, item));
   const NwArgs& a = b.args[j];
-  const uint32_t K = a.K, kp = cand_lanes(K), lane = threadIdx.x & 63u;
-  const uint64_t c = (wv - b.wpre[j]) * (64u / kp) + lane / kp;
-  const uint32_t r = lane % kp;
-  uint32_t l = 0;
-  if (c < a.ncand && r < K) {
-    const uint64_t c0 = a.cbase[r];
-    l = a.s * (uint32_t)dev::interp_lower_bound(a.candk + c0, a.cbase[r + 1] - c0, a.candk[c]);
+  const uint64_t c0 = (uint64_t)(item - b.wpre[j]) * kRkChunk;
+  const uint32_t t = threadIdx.x;
+  uint64_t mine[kRkPer];
+  uint32_t acc[kRkPer];
+#pragma unroll
+  for (uint32_t i = 0; i < kRkPer; ++i) {
+    const uint64_t c = c0 + t + 256u * i;
+    mine[i] = c < a.ncand ? a.candk[c] : ~0ull;
+    acc[i] = 0;
   }
-  for (uint32_t d = 1; d < kp; d <<= 1) l += (uint32_t)__shfl_xor((int)l, (int)d, 64);
-  if (c < a.ncand && r == 0) a.rank[c] = l;
+  for (uint32_t r = 0; r < a.K; ++r) {
+    const uint64_t q0 = a.cbase[r];
+    const uint32_t L = (uint32_t)(a.cbase[r + 1] - q0);
+    if (L <= kRkList) {
+      __syncthreads();  // the previous list's searches are done
+      for (uint32_t x = t; x < L; x += 256) lst[x] = a.candk[q0 + x];
+      __syncthreads();
+#pragma unroll
+      for (uint32_t i = 0; i < kRkPer; ++i) {
+        uint32_t lo = 0, n = L;  // lower_bound(lst[0, L), mine[i])
+        while (n > 0) {
+          const uint32_t h = n >> 1;
+          if (lst[lo + h] < mine[i]) {
+            lo += h + 1;
+            n -= h + 1;
+          } else {
+            n = h;
+          }
+        }
+        acc[i] += lo;
+      }
+    } else {
+#pragma unroll
+      for (uint32_t i = 0; i < kRkPer; ++i)
+        acc[i] += (uint32_t)dev::interp_lower_bound(a.candk + q0, L, mine[i]);
+    }
+  }
+#pragma unroll
+  for (uint32_t i = 0; i < kRkPer; ++i) {
+    const uint64_t c = c0 + t + 256u * i;
+    if (c < a.ncand) a.rank[c] = a.s * acc[i];
+  }
 }
 
 // 2. splitter of bucket floor(R / C') = its largest candidate key
@@ -226,6 +256,9 @@ __device__ unsigned long long g_nwprof[65536][8];
 #define NP_MARK(i) np_t[i] = clock64()
 #else
 #define NP_MARK(i) do { } while (0)
+#endif
+#ifndef PSG_NWAY_RANK
+#define PSG_NWAY_RANK 0  // A/B builds: 1 = merge by rank instead of the merge-path tree
 #endif
 
 // 5. the tile merge
@@ -305,6 +338,9 @@ __global__ __launch_bounds__(kNT) void nw_tile_kernel(NwBatch bt) {
   // the pieces concatenate to the sorted pushes (std::set_union's
   // precondition)
   uint32_t viol = 0;
+  uint64_t kk[kPer];      // this thread's elements (keys), in load order
+  uint32_t qs = 0;        // bit x: element e0 + x starts a piece
+  uint32_t qx[kPer / 4] = {};  // run of element x, 8 bits each
   {
     const uint32_t e0 = (uint32_t)tid * kPer;
     uint32_t q = 0;
@@ -315,9 +351,7 @@ __global__ __launch_bounds__(kNT) void nw_tile_kernel(NwBatch bt) {
         if (roff[mid] <= e0) q = mid; else hi = mid;
       }
     }
-    uint64_t kk[kPer];
     V vv[kPer][kM];
-    uint32_t qs = 0;  // bit x: element e0 + x starts a piece
 #pragma unroll
     for (int x = 0; x < kPer; ++x) {
       const uint32_t e = e0 + x;
@@ -328,6 +362,7 @@ __global__ __launch_bounds__(kNT) void nw_tile_kernel(NwBatch bt) {
         while (roff[q + 1] <= e) ++q;
         const uint32_t i = e - roff[q];
         qs |= (uint32_t)(i == 0u) << x;
+        qx[x / 4] |= q << (8 * (x % 4));
         kk[x] = pkey[q][i];
 #pragma unroll
         for (int mi = 0; mi < M; ++mi) vv[x][mi] = pval[q * M + mi][i];
@@ -371,6 +406,68 @@ __global__ __launch_bounds__(kNT) void nw_tile_kernel(NwBatch bt) {
       ri[x] = k0 + x < E ? si[k0 + x] : (uint16_t)0;
     }
   }
+#if PSG_NWAY_RANK
+  // ---- merge by rank (A/B build): element x of run q goes to its index in
+  // the run + the elements of runs r < q with key <= its key + those of runs
+  // r > q with key < its key (stable: equal keys keep push order).  Per run
+  // r one LDS search for the thread's first element, then a walk: its
+  // elements of one run have increasing keys
+  if (K > 1) {
+    uint32_t posv[kPer];
+#pragma unroll
+    for (int x = 0; x < kPer; ++x) {
+      const uint32_t q = (qx[x / 4] >> (8 * (x % 4))) & 0xffu;
+      posv[x] = k0 + x < E ? k0 + x - roff[q] : 0u;
+    }
+    for (uint32_t r = 0; r < K; ++r) {
+      const uint32_t rs = roff[r], re = roff[r + 1];
+      uint32_t p = rs;
+      bool on = false;  // p is valid for the previous element
+#pragma unroll
+      for (int x = 0; x < kPer; ++x) {
+        if (k0 + x >= E) break;
+        const uint32_t q = (qx[x / 4] >> (8 * (x % 4))) & 0xffu;
+        if (q == r) {
+          on = false;
+          continue;
+        }
+        const bool le = r < q;
+        const uint64_t key = kk[x];
+        if (!on || ((qs >> x) & 1u)) {  // search [rs, re)
+          uint32_t lo = rs, n = re - rs;
+          while (n > 0) {
+            const uint32_t h = n >> 1;
+            const uint64_t v = sk[lo + h];
+            if (le ? v <= key : v < key) {
+              lo += h + 1;
+              n -= h + 1;
+            } else {
+              n = h;
+            }
+          }
+          p = lo;
+          on = true;
+        } else {
+          while (p < re && (le ? sk[p] <= key : sk[p] < key)) ++p;
+        }
+        posv[x] += p - rs;
+      }
+    }
+    __syncthreads();  // every search of the runs is done
+#pragma unroll
+    for (int x = 0; x < kPer; ++x)
+      if (k0 + x < E) {
+        sk[posv[x]] = kk[x];
+        si[posv[x]] = (uint16_t)(k0 + x);
+      }
+    __syncthreads();
+#pragma unroll
+    for (int x = 0; x < kPer; ++x) {
+      rk[x] = k0 + x < E ? sk[k0 + x] : 0ull;
+      ri[x] = k0 + x < E ? si[k0 + x] : (uint16_t)0;
+    }
+  }
+#else
   for (uint32_t width = 1; width < K; width <<= 1) {
     uint32_t A0 = 0, B0 = 0, B1 = 0, i = 0, j = 0;  // current pair and merge position
     uint64_t ka = 0, kb = 0;                         // sk[A0 + i], sk[B0 + j] (when in range)
@@ -425,6 +522,7 @@ __global__ __launch_bounds__(kNT) void nw_tile_kernel(NwBatch bt) {
     __syncthreads();
   }
 
+#endif
   NP_MARK(3);
   // ---- run heads (a key differing from the previous one), unique index
   uint32_t heads = 0, nh = 0;
@@ -633,7 +731,7 @@ struct NwShape {
     T = B + 1;
     if (K == 0) B = T = 0;  // no pushes: no work, the merged count stays 0
   }
-  uint64_t waves() const { return (ncand + 64 / cand_lanes(K) - 1) / (64 / cand_lanes(K)); }
+  uint64_t waves() const { return (ncand + kRkChunk - 1) / kRkChunk; }  // rank workgroups
 };
 
 // Device scratch of a batch of nm merges: [tables: per merge key / value /
@@ -776,8 +874,7 @@ hipError_t nway_enqueue(char* b, const NwLayout& L, int dtype, hipStream_t st) {
   if (L.ncand) {
     hipLaunchKernelGGL(nw_gather_kernel, dim3((uint32_t)((L.ncand + 255) / 256)), dim3(256), 0, st,
                        B, L.ncand);
-    hipLaunchKernelGGL(nw_cand_kernel, dim3((uint32_t)((L.nwaves + 3) / 4)), dim3(256), 0, st, B,
-                       L.nwaves);
+    hipLaunchKernelGGL(nw_rank_kernel, dim3((uint32_t)L.nwaves), dim3(256), 0, st, B);
     hipLaunchKernelGGL(nw_bucket_kernel, dim3((uint32_t)((L.ncand + 255) / 256)), dim3(256), 0, st,
                        B, L.ncand);
   }

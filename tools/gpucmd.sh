@@ -1,16 +1,16 @@
 # scratch GPU command of the current step (overwritten per gpurun call)
 set -o pipefail
 export TMPDIR=/tmp
-R=r04; OUT=gpurun_out/$R; mkdir -p $OUT
-timeout -k 10 300 python3 -u -m pytest tests/test_freq_filter.py -x -q -m gpu --timeout 200 --timeout-method thread > $OUT/freq_test.log 2>&1 || { echo TESTFAIL; tail -30 $OUT/freq_test.log; exit 1; }
-tail -1 $OUT/freq_test.log
-timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d $OUT/ktrace_rows3 -o run -- python3 tools/run_rows.py > $OUT/rows3.json 2> $OUT/rows3.err || { echo "rows failed"; tail -5 $OUT/rows3.err; exit 1; }
-python3 -c "
-import json;d=json.load(open('$OUT/rows3.json'))
-print({k:(round(v['ms'],4),round(v['frac'],3)) for k,v in d.items() if k.startswith('countmin')})"
-grep -i "cm_bin" $OUT/ktrace_rows3/run_kernel_stats.csv | cut -d, -f1-4
-PASSES="1 2" ./tools/pmc_rows.sh $OUT/pmc_rows3 > $OUT/pmc_rows3.log 2>&1 || { echo "pmc rows failed"; tail -5 $OUT/pmc_rows3.log; exit 1; }
-python3 -c "
-import json;r=json.load(open('$OUT/pmc_rows3/summary.json'))['counters']
-print({k:round(v.get('hbm_bytes_corrected',0)/1e9,3) for k,v in r.items() if k.startswith('cm_')})"
+R=r04; O=gpurun_out/$R; mkdir -p $O
+timeout -k 10 300 python3 -u -m pytest tests/test_nway_gpu.py -x -q -m gpu --timeout 120 --timeout-method thread > $O/nway_test.log 2>&1 || { echo TESTFAIL; tail -30 $O/nway_test.log; exit 1; }
+tail -1 $O/nway_test.log
+PSG_LIB_PATH=build/nwrank/libpsg.so timeout -k 10 300 python3 -u -m pytest tests/test_nway_gpu.py -x -q -m gpu --timeout 120 --timeout-method thread > $O/nway_test_rank.log 2>&1 || { echo TESTFAIL rank; tail -30 $O/nway_test_rank.log; exit 1; }
+tail -1 $O/nway_test_rank.log
+for v in default rank default rank; do
+  L=""; [ $v = rank ] && L=build/nwrank/libpsg.so
+  PSG_LIB_PATH=$L timeout -k 10 300 python3 tools/nway_probe.py > $O/nway_probe.log 2>&1 || { echo "probe failed"; tail -5 $O/nway_probe.log; exit 1; }
+  echo "$v $(grep batch $O/nway_probe.log)"
+done
+PSG_LIB_PATH=build/nwrankprof/libpsg.so timeout -k 10 300 python3 tools/nway_probe.py --prof --reps 3 > $O/nway_prof_rank.log 2>&1 || { echo "prof failed"; tail -5 $O/nway_prof_rank.log; exit 1; }
+tail -9 $O/nway_prof_rank.log
 echo done

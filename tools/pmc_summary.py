@@ -17,7 +17,7 @@ def rows(pattern):
 
 def short(name):
     for k in ("cm_bin_count", "cm_bin_scan", "cm_bin_scatter", "cm_bin_apply", "nw_tile_kernel",
-              "nw_gather", "nw_bucket", "nw_split", "cursor_kernel", "tile_packed_kernel", "tile_kernel", "splitter_kernel", "partition_kernel",
+              "nw_gather", "nw_bucket", "nw_split", "nw_rank", "cursor_kernel", "tile_packed_kernel", "tile_kernel", "splitter_kernel", "partition_kernel",
               "unmatched_kernel", "gather_kernel", "union", "slice_kernel", "crc_kernel",
               "darling_kernel", "cm_insert", "cm_count", "cm_scan", "cm_scatter",
               "snappy_lit_kernel", "snappy_kernel", "nw_tile_kernel", "nw_cand", "nw_seg",
