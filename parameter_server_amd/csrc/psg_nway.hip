@@ -257,9 +257,7 @@ __device__ unsigned long long g_nwprof[65536][8];
 #else
 #define NP_MARK(i) do { } while (0)
 #endif
-#ifndef PSG_NWAY_RANK
-#define PSG_NWAY_RANK 0  // A/B builds: 1 = merge by rank instead of the merge-path tree
-#endif
+
 
 // 5. the tile merge
 template <typename V, int M>
@@ -340,7 +338,6 @@ __global__ __launch_bounds__(kNT) void nw_tile_kernel(NwBatch bt) {
   uint32_t viol = 0;
   uint64_t kk[kPer];      // this thread's elements (keys), in load order
   uint32_t qs = 0;        // bit x: element e0 + x starts a piece
-  uint32_t qx[kPer / 4] = {};  // run of element x, 8 bits each
   {
     const uint32_t e0 = (uint32_t)tid * kPer;
     uint32_t q = 0;
@@ -362,7 +359,6 @@ __global__ __launch_bounds__(kNT) void nw_tile_kernel(NwBatch bt) {
         while (roff[q + 1] <= e) ++q;
         const uint32_t i = e - roff[q];
         qs |= (uint32_t)(i == 0u) << x;
-        qx[x / 4] |= q << (8 * (x % 4));
         kk[x] = pkey[q][i];
 #pragma unroll
         for (int mi = 0; mi < M; ++mi) vv[x][mi] = pval[q * M + mi][i];
@@ -406,68 +402,6 @@ __global__ __launch_bounds__(kNT) void nw_tile_kernel(NwBatch bt) {
       ri[x] = k0 + x < E ? si[k0 + x] : (uint16_t)0;
     }
   }
-#if PSG_NWAY_RANK
-  // ---- merge by rank (A/B build): element x of run q goes to its index in
-  // the run + the elements of runs r < q with key <= its key + those of runs
-  // r > q with key < its key (stable: equal keys keep push order).  Per run
-  // r one LDS search for the thread's first element, then a walk: its
-  // elements of one run have increasing keys
-  if (K > 1) {
-    uint32_t posv[kPer];
-#pragma unroll
-    for (int x = 0; x < kPer; ++x) {
-      const uint32_t q = (qx[x / 4] >> (8 * (x % 4))) & 0xffu;
-      posv[x] = k0 + x < E ? k0 + x - roff[q] : 0u;
-    }
-    for (uint32_t r = 0; r < K; ++r) {
-      const uint32_t rs = roff[r], re = roff[r + 1];
-      uint32_t p = rs;
-      bool on = false;  // p is valid for the previous element
-#pragma unroll
-      for (int x = 0; x < kPer; ++x) {
-        if (k0 + x >= E) break;
-        const uint32_t q = (qx[x / 4] >> (8 * (x % 4))) & 0xffu;
-        if (q == r) {
-          on = false;
-          continue;
-        }
-        const bool le = r < q;
-        const uint64_t key = kk[x];
-        if (!on || ((qs >> x) & 1u)) {  // search [rs, re)
-          uint32_t lo = rs, n = re - rs;
-          while (n > 0) {
-            const uint32_t h = n >> 1;
-            const uint64_t v = sk[lo + h];
-            if (le ? v <= key : v < key) {
-              lo += h + 1;
-              n -= h + 1;
-            } else {
-              n = h;
-            }
-          }
-          p = lo;
-          on = true;
-        } else {
-          while (p < re && (le ? sk[p] <= key : sk[p] < key)) ++p;
-        }
-        posv[x] += p - rs;
-      }
-    }
-    __syncthreads();  // every search of the runs is done
-#pragma unroll
-    for (int x = 0; x < kPer; ++x)
-      if (k0 + x < E) {
-        sk[posv[x]] = kk[x];
-        si[posv[x]] = (uint16_t)(k0 + x);
-      }
-    __syncthreads();
-#pragma unroll
-    for (int x = 0; x < kPer; ++x) {
-      rk[x] = k0 + x < E ? sk[k0 + x] : 0ull;
-      ri[x] = k0 + x < E ? si[k0 + x] : (uint16_t)0;
-    }
-  }
-#else
   for (uint32_t width = 1; width < K; width <<= 1) {
     uint32_t A0 = 0, B0 = 0, B1 = 0, i = 0, j = 0;  // current pair and merge position
     uint64_t ka = 0, kb = 0;                         // sk[A0 + i], sk[B0 + j] (when in range)
@@ -522,7 +456,6 @@ __global__ __launch_bounds__(kNT) void nw_tile_kernel(NwBatch bt) {
     __syncthreads();
   }
 
-#endif
   NP_MARK(3);
   // ---- run heads (a key differing from the previous one), unique index
   uint32_t heads = 0, nh = 0;
