@@ -190,15 +190,29 @@ __global__ __launch_bounds__(256) void nw_rank_kernel(NwBatch b) {
 }
 
 // 2. splitter of bucket floor(R / C') = its largest candidate key
+// (consecutive candidates of one push have increasing keys and ranks, so
+// about C' / (K s) neighbours share a bucket: only the lane whose right
+// neighbour does not dominate it -- same merge and bucket, key not smaller
+// -- issues the atomic)
 __global__ __launch_bounds__(256) void nw_bucket_kernel(NwBatch b, uint64_t ncand) {
   const uint64_t g = (uint64_t)blockIdx.x * 256u + threadIdx.x;
-  if (g >= ncand) return;
-  const uint32_t j = merge_of(b.cpre, b.nm, g);
-  const NwArgs& a = b.args[j];
-  const uint64_t c = g - b.cpre[j];
-  const uint64_t key = a.candk[c];
-  const uint32_t bk = a.rank[c] / a.cw;
-  if (bk < a.B) atomicMax((unsigned long long*)a.split + bk, (unsigned long long)key);
+  const bool in = g < ncand;
+  uint32_t j = 0, bk = 0xffffffffu;
+  uint64_t key = 0;
+  if (in) {
+    j = merge_of(b.cpre, b.nm, g);
+    const NwArgs& a = b.args[j];
+    const uint64_t c = g - b.cpre[j];
+    key = a.candk[c];
+    bk = a.rank[c] / a.cw;
+  }
+  const uint32_t lane = threadIdx.x & 63u;
+  const uint32_t nj = (uint32_t)__shfl_down((int)j, 1, 64);
+  const uint32_t nb = (uint32_t)__shfl_down((int)bk, 1, 64);
+  const uint64_t nk = (uint64_t)__shfl_down((long long)key, 1, 64);
+  const bool dominated = lane < 63u && g + 1 < ncand && nj == j && nb == bk && nk >= key;
+  if (in && !dominated && bk < b.args[j].B)
+    atomicMax((unsigned long long*)b.args[j].split + bk, (unsigned long long)key);
 }
 
 // 3. prefix max (one workgroup per merge): splitters non-decreasing, empty
