@@ -53,9 +53,6 @@ namespace psg {
 #ifndef PSG_SKELETON
 #define PSG_SKELETON 0  // diagnostic A/B builds (profiles/r03_ab_fold.txt): 1, 2 skip phases
 #endif
-#ifndef PSG_FOLD_SPLIT
-#define PSG_FOLD_SPLIT 0  // A/B: sole-contributor slots fold without the wave order
-#endif
 #ifdef PSG_PHASES
 // diagnostic build only (tools/phases.py): shader clocks between the phase
 // marks of thread 0 of every workgroup, summed in registers and stored once
@@ -533,7 +530,7 @@ __global__ __launch_bounds__(nt_of(kGroup), (occupancy<V, M, kGroup>())) void ti
         const bool ok = ((hv & fd) >> r & 1u) && (int)pos[r] > prev;
 #endif
         okb |= (uint32_t)ok << r;
-        if ((PSG_FOLD_SPLIT || !parallel) && ok)
+        if (!parallel && ok)
           __hip_atomic_fetch_add(kCntW ? &cnt32[pos[r]] : &cnt32[pos[r] >> 1],
                                  kCntW ? 1u : 1u << (16u * (pos[r] & 1u)),
                                  __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
@@ -555,27 +552,6 @@ __global__ __launch_bounds__(nt_of(kGroup), (occupancy<V, M, kGroup>())) void ti
     // ---- fold, wave by wave (rounds are push-major)
     const uint32_t inpass = (U - done) < kNW * Rw ? U - done : kNW * Rw;
     const uint32_t wl = (inpass - 1) / Rw;  // wave holding the pass's last round
-#if PSG_FOLD_SPLIT
-    // A/B: in a tile of one pass and one push group the per-slot counts are
-    // complete after the check; a slot with one contributor needs no order,
-    // so those elements fold at once in every wave, and only slots held by
-    // several pushes go through the wave-ordered steps
-    if (kCntW && g0 == 0u && np <= (uint32_t)kGroup && done == 0u && inpass == U) {
-      __syncthreads();  // (6) every count of the pass
-#pragma unroll
-      for (int r = 0; r < kCap; ++r) {
-        if ((uint32_t)r < nrw && ((okb >> r) & 1u)) {
-          const uint32_t s = pos[r];
-          if (cnt32[s] == 1u) {
-            const bool first = (re[r] >> kCB) == 0u && !cont;
-#pragma unroll
-            for (int mi = 0; mi < M; ++mi) acc[mi][s] = first ? ev[r][mi] : acc[mi][s] + ev[r][mi];
-            okb &= ~(1u << r);
-          }
-        }
-      }
-    }
-#endif
 #if PSG_SKELETON == 3
     // diagnostic: every wave folds at once (racy: wrong sums on shared slots),
     // the cost of the wave-ordered fold's serialisation
