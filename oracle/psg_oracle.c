@@ -342,6 +342,69 @@ DEFINE_AGGREGATE(f64, double)
 DEFINE_AGGREGATE_SCATTER(f32, float)
 DEFINE_AGGREGATE_SCATTER(f64, double)
 
+/* serialSetValue (kv_vector.h:171-204) in the same O(sum n log |D|) form, for
+ * strictly increasing pushes (returns -3 on any other): oldMatch
+ * (message.h:229-267) zero-fills an aligned array and writes each matched
+ * value, the first non-empty push's array is stored (:195-196) and every
+ * later one is added element-wise (:200).  A later push lacking the key
+ * therefore adds +0.0; x + 0.0 is x except on -0.0 (-> +0.0) and a
+ * signalling NaN (quieted), and after either happened further adds keep
+ * it, so the dense fold equals the fold of the present values followed by
+ * ONE +0.0 iff some non-empty push lacked the key (a push before the first
+ * contribution leaves +0.0 + v, which that +0.0 does not change).
+ * Cross-checked against orc_aggregate (serial) in tests/test_oracle.py. */
+#define DEFINE_AGGREGATE_SCATTER_SERIAL(SUF, V)                                \
+  int orc_aggregate_scatter_serial_##SUF(                                      \
+      const uint64_t* D, size_t nD, uint64_t kb, uint64_t ke, int npush,       \
+      const uint64_t* const* keys, const size_t* n, int m, const V* const* vals,\
+      V* const* out, size_t* lo, size_t* hi, size_t* matched) {                \
+    *lo = *hi = 0;                                                             \
+    int have = 0;                                                              \
+    uint32_t nne = 0;   /* non-empty pushes */                                 \
+    uint32_t* cnt = 0;  /* pushes holding each slot */                         \
+    for (int p = 0; p < npush; ++p) {                                          \
+      matched[p] = 0;                                                          \
+      if (n[p] == 0) continue; /* kv_vector.h:177: empty push ignored */       \
+      if (nD == 0) { free(cnt); return -1; }                                   \
+      size_t plo, phi;                                                         \
+      orc_find_range_u64(D, nD, kb, ke, &plo, &phi);                           \
+      if (have && (plo != *lo || phi != *hi)) { free(cnt); return -2; }        \
+      if (!have) {                                                             \
+        for (int i = 0; i < m; ++i) memset(out[i], 0, sizeof(V) * (phi - plo));\
+        cnt = (uint32_t*)calloc(phi - plo ? phi - plo : 1, sizeof(uint32_t));  \
+      }                                                                        \
+      size_t mt = 0;                                                           \
+      for (size_t k = 0; k < n[p]; ++k) {                                      \
+        if (k > 0 && keys[p][k] <= keys[p][k - 1]) { free(cnt); return -3; }  \
+        const size_t pos = plo + lb_u64(D + plo, phi - plo, keys[p][k]);       \
+        if (pos >= phi || D[pos] != keys[p][k]) continue;                      \
+        ++mt;                                                                  \
+        ++cnt[pos - plo];                                                      \
+        for (int i = 0; i < m; ++i) {                                          \
+          V* o = out[i] + (pos - plo);                                         \
+          const V v = vals[(size_t)p * m + i][k];                              \
+          *o = have ? *o + v : v;                                              \
+        }                                                                      \
+      }                                                                        \
+      matched[p] = mt;                                                         \
+      if (!have) {                                                             \
+        *lo = plo;                                                             \
+        *hi = phi;                                                             \
+        have = 1;                                                              \
+      }                                                                        \
+      ++nne;                                                                   \
+    }                                                                          \
+    if (have)                                                                  \
+      for (size_t j = 0; j < *hi - *lo; ++j)                                   \
+        if (cnt[j] < nne)                                                      \
+          for (int i = 0; i < m; ++i) out[i][j] = out[i][j] + (V)0;            \
+    free(cnt);                                                                 \
+    return 0;                                                                  \
+  }
+
+DEFINE_AGGREGATE_SCATTER_SERIAL(f32, float)
+DEFINE_AGGREGATE_SCATTER_SERIAL(f64, double)
+
 /* kv_vector.h:215-227: oldMatch(recv_key, key_[ch], val_[ch], union range)
  * -- a gather aligned to the request keys, zero where absent. */
 #define DEFINE_GATHER(SUF, V)                                                  \

@@ -101,6 +101,15 @@ int orc_aggregate_scatter_f64(const uint64_t* D, size_t nD, uint64_t kb, uint64_
                               const uint64_t* const* keys, const size_t* n, int m,
                               const double* const* vals, double* const* out, size_t* lo,
                               size_t* hi, size_t* matched);
+/* serialSetValue in the same form, strictly increasing pushes only */
+int orc_aggregate_scatter_serial_f32(const uint64_t* D, size_t nD, uint64_t kb, uint64_t ke,
+                                     int npush, const uint64_t* const* keys, const size_t* n,
+                                     int m, const float* const* vals, float* const* out,
+                                     size_t* lo, size_t* hi, size_t* matched);
+int orc_aggregate_scatter_serial_f64(const uint64_t* D, size_t nD, uint64_t kb, uint64_t ke,
+                                     int npush, const uint64_t* const* keys, const size_t* n,
+                                     int m, const double* const* vals, double* const* out,
+                                     size_t* lo, size_t* hi, size_t* matched);
 
 /* KVVector::serialGetValue (kv_vector.h:215-227): out[i] = W[pos(req[i])]
  * or 0 when req[i] is not a server key. */

@@ -49,6 +49,12 @@ def orc() -> C.CDLL:
                                                     C.c_int, _p, _p, _psz, _psz, _p]),
             "orc_aggregate_scatter_f64": (C.c_int, [_p, _sz, _u64, _u64, C.c_int, _p, _p,
                                                     C.c_int, _p, _p, _psz, _psz, _p]),
+            "orc_aggregate_scatter_serial_f32": (C.c_int, [_p, _sz, _u64, _u64, C.c_int, _p,
+                                                           _p, C.c_int, _p, _p, _psz, _psz,
+                                                           _p]),
+            "orc_aggregate_scatter_serial_f64": (C.c_int, [_p, _sz, _u64, _u64, C.c_int, _p,
+                                                           _p, C.c_int, _p, _p, _psz, _psz,
+                                                           _p]),
             "orc_old_match_f32": (C.c_int, [_p, _sz, _p, _sz, _p, _u64, _u64, _p,
                                             _psz, _psz, _psz]),
             "orc_murmur3_x64_128": (None, [_p, C.c_int, C.c_uint32, _p]),
@@ -140,9 +146,10 @@ def aggregate(D, kb, ke, pushes, parallel=False, nthreads=1, dtype=np.float32):
     return rc, lo.value, hi.value, [o[:n] for o in outs], matched[:npush]
 
 
-def aggregate_scatter(D, kb, ke, pushes, dtype=np.float32):
-    """parallelSetValue in O(sum n log |D|) (orc_aggregate_scatter): the
-    parallel-mode result for checks too large for the merge-walk oracle."""
+def aggregate_scatter(D, kb, ke, pushes, dtype=np.float32, parallel=True):
+    """parallelSetValue (or, parallel=False, serialSetValue over strictly
+    increasing pushes) in O(sum n log |D|) (orc_aggregate_scatter[_serial]):
+    results for checks too large for the merge-walk oracle."""
     D = u64(D)
     dtype = np.dtype(dtype)
     npush = len(pushes)
@@ -157,7 +164,8 @@ def aggregate_scatter(D, kb, ke, pushes, dtype=np.float32):
     op = (C.c_void_p * m)(*[_a(o) for o in outs])
     lo, hi = C.c_size_t(), C.c_size_t()
     matched = np.zeros(max(1, npush), np.uint64)
-    f = orc().orc_aggregate_scatter_f32 if dtype == np.float32 else orc().orc_aggregate_scatter_f64
+    sfx = ("" if parallel else "_serial") + ("_f32" if dtype == np.float32 else "_f64")
+    f = getattr(orc(), "orc_aggregate_scatter" + sfx)
     rc = f(_a(D), D.size, int(kb), int(ke), npush, kp, ns, m, vp, op, C.byref(lo), C.byref(hi),
            _a(matched))
     n = hi.value - lo.value

@@ -167,6 +167,49 @@ def test_unmatched_and_duplicates_are_counted():
     assert rc == -1
 
 
+@pytest.mark.parametrize("seed", range(6))
+def test_scatter_serial_form_equals_serial_fold(seed):
+    """orc_aggregate_scatter_serial (serialSetValue with ONE trailing +0.0
+    where a non-empty push lacked the key; the whole-cfg5 serial GPU check)
+    equals the dense oldMatch fold (orc_aggregate, serial) bit for bit:
+    -0.0 and signalling / quiet NaN payloads, empty pushes (the first one
+    too), keys absent from D, sub-ranges, f32 and f64, m = 1..2."""
+    rng = np.random.default_rng(300 + seed)
+    dtype = np.float32 if seed % 2 == 0 else np.float64
+    ity = np.uint32 if dtype == np.float32 else np.uint64
+    snan = ity(0x7F800001) if dtype == np.float32 else ity(0x7FF0000000000001)
+    m = 1 + seed % 2
+    D = np.unique(rng.integers(0, 1 << 40, 2000, dtype=np.uint64))
+    pushes = []
+    for p in range(6):
+        cnt = 0 if p == (seed % 3) * 2 else int(rng.integers(1, 1500))
+        k = np.unique(np.concatenate([rng.choice(D, cnt, replace=False),
+                                      rng.integers(0, 1 << 40, 10 if cnt else 0,
+                                                   dtype=np.uint64)]))
+        vs = []
+        for _ in range(m):
+            v = rng.standard_normal(k.size).astype(dtype)
+            v[rng.random(k.size) < 0.2] = -0.0
+            bits = v.view(ity)
+            bits[rng.random(k.size) < 0.02] = snan
+            v[rng.random(k.size) < 0.02] = np.nan
+            vs.append(v)
+        pushes.append((k, vs))
+    for kb, ke in [(0, (1 << 64) - 1), (int(D[50]), int(D[1700]))]:
+        a = O.aggregate(D, kb, ke, pushes, False, 1, dtype)
+        b = O.aggregate_scatter(D, kb, ke, pushes, dtype, parallel=False)
+        assert a[0] == b[0] == 0 and a[1:3] == b[1:3]
+        assert np.array_equal(a[4], b[4])
+        for x, y in zip(a[3], b[3]):
+            assert x.tobytes() == y.tobytes()
+
+
+def test_scatter_serial_form_rejects_unsorted_push():
+    D = np.arange(10, dtype=np.uint64)
+    pushes = [(np.array([1, 3, 2], np.uint64), [np.ones(3, np.float32)])]
+    assert O.aggregate_scatter(D, 0, (1 << 64) - 1, pushes, parallel=False)[0] == -3
+
+
 def test_gather_repeated_request_reads_zero():
     out, mt = O.gather([5, 7], [1.0, 2.0], [5, 5, 7])
     assert out.tolist() == [1.0, 0.0, 2.0] and mt == 2
