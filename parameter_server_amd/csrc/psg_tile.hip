@@ -50,9 +50,6 @@
 
 namespace psg {
 
-#ifndef PSG_EARLY_D
-#define PSG_EARLY_D 0  // A/B: D's loads issued before the push tables' round trip
-#endif
 #ifndef PSG_SKELETON
 #define PSG_SKELETON 0  // diagnostic A/B builds (profiles/r03_ab_fold.txt): 1, 2 skip phases
 #endif
@@ -225,34 +222,6 @@ __global__ __launch_bounds__(nt_of(kGroup), (occupancy<V, M, kGroup>())) void ti
       if (lane == 0) rpre[0] = 0;
     }
   };
-#if PSG_EARLY_D
-  // ---- D keys, continued sums: thread t owns slots 4t..4t+3
-  const uint32_t s0 = 4u * (uint32_t)tid;
-  uint64_t d[4];
-  if (s0 + 3u < nt && ((uintptr_t)Dg & 15u) == 0u) {
-    // D is read by this tile only: nontemporal (same-box A/B: ~1-3 % faster
-    // on cfg2/cfg3 with the nontemporal sum stores; not the element loads,
-    // whose lines neighbouring tiles share)
-    const u64x2 x0 = __builtin_nontemporal_load((const AS1 u64x2*)(Dg + s0));
-    const u64x2 x1 = __builtin_nontemporal_load((const AS1 u64x2*)(Dg + s0 + 2));
-    d[0] = x0.x; d[1] = x0.y; d[2] = x1.x; d[3] = x1.y;
-  } else {
-#pragma unroll
-    for (int j = 0; j < 4; ++j) d[j] = s0 + j < nt ? G(Dg)[s0 + j] : ~0ull;
-  }
-  // the resident bucket table (plans): kBPT u16 entries per thread
-  const uint32_t* Bg = T.bt;
-  u32x2 btw = {0u, 0u};
-  if (Bg) btw = __builtin_nontemporal_load((const AS1 u32x2*)Bg + tid);
-  V a0[M][4];
-#pragma unroll
-  for (int mi = 0; mi < M; ++mi)
-#pragma unroll
-    for (int j = 0; j < 4; ++j)
-      a0[mi][j] = (cont && s0 + j < nt) ? G((const V*)T.out[mi] + T.slot0)[s0 + j] : V(0);
-
-  if (np) load_tables(0);  // wave 0's table loads wait behind D's, not before them
-#else
   if (np) load_tables(0);
 
   // ---- D keys, continued sums: thread t owns slots 4t..4t+3
@@ -280,7 +249,6 @@ __global__ __launch_bounds__(nt_of(kGroup), (occupancy<V, M, kGroup>())) void ti
     for (int j = 0; j < 4; ++j)
       a0[mi][j] = (cont && s0 + j < nt) ? G((const V*)T.out[mi] + T.slot0)[s0 + j] : V(0);
 
-#endif
   // bucket of a key: the tile's key range [klo, khi] scaled onto [0, kNB) by
   // one 32x32 high multiply; keys outside the range land in an end bucket
   // and are not found there
