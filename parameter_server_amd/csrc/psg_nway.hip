@@ -137,10 +137,14 @@ __global__ __launch_bounds__(256) void nw_gather_kernel(NwBatch b, uint64_t ncan
 // counts are summed in registers -- no atomics, no global search chains.  A
 // list longer than the LDS stage is searched in global memory (interpolation
 // probes, then a bisection: exact for any key distribution).
-constexpr uint32_t kRkPer = 16;
-constexpr uint32_t kRkChunk = 256 * kRkPer;  // candidates per workgroup
+// Candidates per thread: 16 when the batch fills the chip with workgroups of
+// 4,096 candidates; a small batch (one merge: 8 such workgroups for cfg2)
+// takes 4 or 1 per thread, so its lists are searched by more workgroups at
+// once instead of by a few long chains of LDS reads.
 constexpr uint32_t kRkList = 8192;           // candidates of one list staged in LDS (64 KB)
+template <uint32_t kRkPer>
 __global__ __launch_bounds__(256) void nw_rank_kernel(NwBatch b) {
+  constexpr uint32_t kRkChunk = 256 * kRkPer;  // candidates per workgroup
   __shared__ uint64_t lst[kRkList];
   const uint32_t item = blockIdx.x;
   const uint32_t j = uni(merge_of(b.wpre, b.nm, item));
@@ -678,7 +682,8 @@ struct NwShape {
     T = B + 1;
     if (K == 0) B = T = 0;  // no pushes: no work, the merged count stays 0
   }
-  uint64_t waves() const { return (ncand + kRkChunk - 1) / kRkChunk; }  // rank workgroups
+  // rank workgroups at `per` candidates per thread
+  uint64_t waves(uint32_t per) const { return (ncand + 256u * per - 1) / (256u * per); }
 };
 
 // Device scratch of a batch of nm merges: [tables: per merge key / value /
@@ -694,6 +699,7 @@ struct NwLayout {
   std::vector<Off> off;
   size_t o_args = 0, o_pre = 0, o_zero = 0, o_ticket = 0, o_misc = 0, zero_len = 0, bytes = 0;
   uint64_t nwaves = 0, ncand = 0, nseg = 0, ntiles = 0;
+  uint32_t rk_per = 16;  // rank-stage candidates per thread (16, 4 or 1)
 
   // pn: the merges' push lengths back to back, npush[j] per merge
   void plan(uint32_t nmerge, const uint32_t* npush, const uint64_t* pn, int mm) {
@@ -733,8 +739,15 @@ struct NwLayout {
     }
     bytes = o;
     nwaves = ncand = nseg = ntiles = 0;
+    // the fewest candidates per thread that still gives >= 512 rank workgroups
+    uint64_t w16 = 0, w4 = 0;
     for (const NwShape& x : sh) {
-      nwaves += x.waves();
+      w16 += x.waves(16);
+      w4 += x.waves(4);
+    }
+    rk_per = w16 >= 512 ? 16u : (w4 >= 512 ? 4u : 1u);
+    for (const NwShape& x : sh) {
+      nwaves += x.waves(rk_per);
       ncand += x.ncand;
       nseg += (uint64_t)(x.T + 1) * x.K;
       ntiles += x.T;
@@ -799,7 +812,7 @@ struct NwLayout {
       A.s = x.s;
       A.cw = x.cw;
       A.flags = flags;
-      pre[j + 1] = pre[j] + x.waves();
+      pre[j + 1] = pre[j] + x.waves(rk_per);
       pre[(nm + 1) + j + 1] = pre[(nm + 1) + j] + x.ncand;
       pre[2 * (nm + 1) + j + 1] = pre[2 * (nm + 1) + j] + (uint64_t)(x.T + 1) * K;
       pre[3 * (nm + 1) + j + 1] = pre[3 * (nm + 1) + j] + x.T;
@@ -821,7 +834,12 @@ hipError_t nway_enqueue(char* b, const NwLayout& L, int dtype, hipStream_t st) {
   if (L.ncand) {
     hipLaunchKernelGGL(nw_gather_kernel, dim3((uint32_t)((L.ncand + 255) / 256)), dim3(256), 0, st,
                        B, L.ncand);
-    hipLaunchKernelGGL(nw_rank_kernel, dim3((uint32_t)L.nwaves), dim3(256), 0, st, B);
+    if (L.rk_per == 16)
+      hipLaunchKernelGGL(nw_rank_kernel<16>, dim3((uint32_t)L.nwaves), dim3(256), 0, st, B);
+    else if (L.rk_per == 4)
+      hipLaunchKernelGGL(nw_rank_kernel<4>, dim3((uint32_t)L.nwaves), dim3(256), 0, st, B);
+    else
+      hipLaunchKernelGGL(nw_rank_kernel<1>, dim3((uint32_t)L.nwaves), dim3(256), 0, st, B);
     hipLaunchKernelGGL(nw_bucket_kernel, dim3((uint32_t)((L.ncand + 255) / 256)), dim3(256), 0, st,
                        B, L.ncand);
   }

@@ -35,6 +35,10 @@
 #include "../../include/psg.h"
 #include "psg_internal.h"
 
+#ifndef PSG_SNAPPY_PREFETCH
+#define PSG_SNAPPY_PREFETCH 1  // A/B: 0 = no L2 prefetch of the parts
+#endif
+
 namespace psg {
 
 namespace {
@@ -58,6 +62,8 @@ constexpr uint32_t kWin = 4096;
 constexpr uint32_t kBigLit = 2048;   // literals deferred to the copy kernel
 constexpr uint32_t kMaxDef = 768;    // deferred pieces per part (LDS list)
 constexpr uint32_t kLitUnits = 256;  // 16-B units per copy-kernel chunk (4 KB)
+constexpr uint64_t kPrefetchParts = 64;         // parts per launch that are prefetched into L2
+constexpr uint64_t kPrefetchMax = 2ull << 20;   // largest part prefetched
 
 __global__ __launch_bounds__(64) void snappy_kernel(const uint8_t* __restrict__ src,
                                                     const uint64_t* __restrict__ soff,
@@ -69,7 +75,7 @@ __global__ __launch_bounds__(64) void snappy_kernel(const uint8_t* __restrict__ 
                                                     uint32_t* __restrict__ nlits,
                                                     uint32_t lit_cap,
                                                     unsigned long long* __restrict__ nbad,
-                                                    int pairs) {
+                                                    int pairs, int prefetch) {
   __shared__ uint8_t ring[kRing];
   __shared__ __attribute__((aligned(4))) uint8_t win[kWin];
   // deferred pieces of the current part, in output order: output start,
@@ -96,6 +102,14 @@ __global__ __launch_bounds__(64) void snappy_kernel(const uint8_t* __restrict__ 
     // doubled it)
     const uint32_t e = (uint32_t)slen;
     int32_t st = 0;
+    // A launch of few parts (a message's: the compressed-push path) pulls
+    // each part into its XCD's L2 first -- one byte load per 128-B line, all
+    // in flight at once -- so the walk's window refills, one after each
+    // skipped literal and each a dependent round trip, hit L2 instead of
+    // HBM.  Many parts at once would evict each other: no prefetch there.
+    uint32_t pfx = 0;
+    if (prefetch && slen <= kPrefetchMax)
+      for (uint32_t x = lane * 128u; x < e; x += 64u * 128u) pfx ^= s0[x];
     // the element stream is read from an LDS window (4 KB, refilled with
     // coalesced 4-byte loads), and from it into a 64-byte register
     // lookahead (lane j holds byte lp + j) whose bytes the parse takes with
@@ -332,6 +346,7 @@ __global__ __launch_bounds__(64) void snappy_kernel(const uint8_t* __restrict__ 
       status[msg] = st;
       if (st && nbad) atomicAdd(nbad, 1ull);
     }
+    asm volatile("" ::"v"(pfx));  // the prefetch loads are kept
 #ifdef PSG_SNAPPY_PROF
     sp[2] = clock64() - sp_part;
     if (lane == 0 && msg < 4096)
@@ -455,7 +470,7 @@ hipError_t launch_snappy(const uint8_t* src, const uint64_t* soff, uint64_t nmsg
   const uint64_t blocks = nmsg < 512 ? nmsg : 512;
   hipLaunchKernelGGL(snappy_kernel, dim3((uint32_t)blocks), dim3(64), 0, stream, src, soff, dst,
                      doff, dcap, nmsg, status, nlits ? lits : nullptr, nlits, cap, nbad,
-                     pairs ? 1 : 0);
+                     pairs ? 1 : 0, nmsg <= kPrefetchParts ? PSG_SNAPPY_PREFETCH : 0);
   if (!nlits) return hipGetLastError();
   hipLaunchKernelGGL(snappy_lit_kernel, dim3(1024), dim3(256), 0, stream, lits, nlits, cap);
   return hipGetLastError();
