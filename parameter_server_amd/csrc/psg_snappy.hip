@@ -35,6 +35,7 @@
 #include "../../include/psg.h"
 #include "psg_internal.h"
 
+#define AS1 __attribute__((address_space(1)))
 #ifndef PSG_SNAPPY_PREFETCH
 #define PSG_SNAPPY_PREFETCH 1  // A/B: 0 = no L2 prefetch of the parts
 #endif
@@ -45,9 +46,9 @@ namespace {
 
 #ifdef PSG_SNAPPY_PROF
 // diagnostic build only (tools/snappy_prof.py): per part, shader clocks in
-// [0] window refills, [1] copies' piece lookups, [2] the whole part, and
-// counts [3] refills, [4] deferred pieces, [5] copies resolved per lane,
-// [6] elements
+// [0] window refills, [1] copies' piece lookups, [2] the whole part,
+// [5] literals moved in the parse, [7] the part's end (flush, hand-off), and
+// counts [3] refills, [4] deferred pieces, [6] elements
 __device__ unsigned long long g_sprof[4096][8];
 #define SP_T0() const unsigned long long _sp0 = clock64()
 #define SP_ADD(i) (sp[i] += clock64() - _sp0)
@@ -76,7 +77,7 @@ __global__ __launch_bounds__(64) void snappy_kernel(const uint8_t* __restrict__ 
                                                     uint32_t lit_cap,
                                                     unsigned long long* __restrict__ nbad,
                                                     int pairs, int prefetch) {
-  __shared__ uint8_t ring[kRing];
+  __shared__ __attribute__((aligned(16))) uint8_t ring[kRing];
   __shared__ __attribute__((aligned(4))) uint8_t win[kWin];
   // deferred pieces of the current part, in output order: output start,
   // input start, length
@@ -84,9 +85,12 @@ __global__ __launch_bounds__(64) void snappy_kernel(const uint8_t* __restrict__ 
   const uint32_t lane = threadIdx.x;
   for (uint64_t msg = blockIdx.x; msg < nmsg; msg += gridDim.x) {
     // pairs: soff holds (begin, end) device addresses per part
-    const uint8_t* const s0 = pairs ? (const uint8_t*)soff[2 * msg] : src + soff[msg];
+    // global (not flat) pointers: a flat load also counts on lgkmcnt, so every
+    // LDS wait of the parse would wait for the loads in flight as well
+    const AS1 uint8_t* const s0 =
+        (const AS1 uint8_t*)(pairs ? (const uint8_t*)soff[2 * msg] : src + soff[msg]);
     const uint64_t slen = pairs ? soff[2 * msg + 1] - soff[2 * msg] : soff[msg + 1] - soff[msg];
-    uint8_t* const out = dst + doff[msg];
+    AS1 uint8_t* const out = (AS1 uint8_t*)(dst + doff[msg]);
     const uint64_t cap = dcap ? dcap[msg] : doff[msg + 1] - doff[msg];
     // an empty part is an empty array (uncompressFrom of 0 bytes clears, :233)
     if (slen == 0) {
@@ -116,6 +120,10 @@ __global__ __launch_bounds__(64) void snappy_kernel(const uint8_t* __restrict__ 
     // a scalar readlane: one LDS read serves several tags
     const uintptr_t mis = (uintptr_t)s0 & 3u;
     int32_t wb = -(int32_t)kWin - 64;  // part offset of win[0]; nothing loaded
+    // an aligned in-range word for the refill's out-of-range lanes (a part
+    // of fewer than 8 bytes may have none: every word is then an edge word
+    // and the address is never used for data; 0 keeps it inside the part)
+    const int64_t gs = e >= 8u ? (int64_t)((4u - (uint32_t)mis) & 3u) : 0;
 #ifdef PSG_SNAPPY_PROF
     unsigned long long sp[8] = {0, 0, 0, 0, 0, 0, 0, 0};
     const unsigned long long sp_part = clock64();
@@ -129,16 +137,30 @@ __global__ __launch_bounds__(64) void snappy_kernel(const uint8_t* __restrict__ 
       // all 16 loads in flight before the first LDS store (one HBM round
       // trip per refill, not 16: a refill follows every skipped literal)
       constexpr int kR = (int)(kWin / 256u);
+      // The in-range words load from their address and the others from the
+      // window's first in-range word (gs, the result dropped): no branch
+      // around the loads, so all 16 issue back to back (a per-word branch
+      // made the compiler wait after each, 16 round trips per refill).
+      // Words that straddle the part's ends (at most two per refill) are
+      // assembled byte by byte afterwards.
       uint32_t v[kR];
+      bool edge = false;
 #pragma unroll
       for (int r = 0; r < kR; ++r) {
         const int64_t g = (int64_t)wb + lane * 4u + 256u * r;
-        v[r] = 0;
-        if (g >= 0 && g + 4 <= (int64_t)e) {
-          v[r] = *(const uint32_t*)(s0 + g);
-        } else {
-          for (uint32_t b = 0; b < 4; ++b)
-            if (g + b >= 0 && g + b < (int64_t)e) v[r] |= (uint32_t)s0[g + b] << (8 * b);
+        const bool inb = g >= 0 && g + 4 <= (int64_t)e;
+        edge |= !inb;
+        v[r] = *(const AS1 uint32_t*)(s0 + (inb ? g : gs));  // no select on the result
+      }
+      if (__ballot(edge)) {
+#pragma unroll
+        for (int r = 0; r < kR; ++r) {
+          const int64_t g = (int64_t)wb + lane * 4u + 256u * r;
+          if (!(g >= 0 && g + 4 <= (int64_t)e)) {
+            v[r] = 0;
+            for (uint32_t b = 0; b < 4; ++b)
+              if (g + b >= 0 && g + b < (int64_t)e) v[r] |= (uint32_t)s0[g + b] << (8 * b);
+          }
         }
       }
 #pragma unroll
@@ -182,6 +204,33 @@ __global__ __launch_bounds__(64) void snappy_kernel(const uint8_t* __restrict__ 
     // store holds vmcnt, which the next window refill would wait for).
     // A flush skips the deferred pieces (the copy kernel writes them).
     uint32_t fl = 0, ofs = 0xffffffffu, fk = 0;
+    // ring bytes [a, b) to the output: 16 B per lane where the output is
+    // 16-B aligned (ring and output agree mod 16 then), four 1-KB steps in
+    // flight at once; bytes at the ends one per lane
+    const bool out16 = ((uintptr_t)out & 15u) == 0u;
+    auto flush_range = [&](uint32_t a, uint32_t b) {
+      typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
+      uint32_t a16 = a, b16 = a;
+      if (out16 && b - a >= 256u) {
+        a16 = (a + 15u) & ~15u;
+        b16 = b & ~15u;
+      }
+      for (uint32_t y = a + lane; y < a16; y += 64) out[y] = ring[y & (kRing - 1)];
+      for (uint32_t y0 = a16; y0 < b16; y0 += 4096u) {
+        u32x4 v[4];
+#pragma unroll
+        for (int k = 0; k < 4; ++k) {
+          const uint32_t y = y0 + 16u * (64u * k + lane);
+          if (y < b16) v[k] = *(const u32x4*)&ring[y & (kRing - 1)];
+        }
+#pragma unroll
+        for (int k = 0; k < 4; ++k) {
+          const uint32_t y = y0 + 16u * (64u * k + lane);
+          if (y < b16) *(AS1 u32x4*)(out + y) = v[k];
+        }
+      }
+      for (uint32_t y = b16 + lane; y < b; y += 64) out[y] = ring[y & (kRing - 1)];
+    };
     auto flush = [&](uint32_t to) {
       __builtin_amdgcn_wave_barrier();
       uint32_t x = fl;
@@ -193,7 +242,7 @@ __global__ __launch_bounds__(64) void snappy_kernel(const uint8_t* __restrict__ 
           continue;
         }
         const uint32_t end = fk < nd && tdst[fk] < to ? tdst[fk] : to;
-        for (uint32_t y = x + lane; y < end; y += 64) out[y] = ring[y & (kRing - 1)];
+        flush_range(x, end);
         x = end;
       }
       fl = to;
@@ -254,6 +303,7 @@ __global__ __launch_bounds__(64) void snappy_kernel(const uint8_t* __restrict__ 
           p += len;
           continue;
         }
+        SP_T0();
         if ((int32_t)p >= wb && (int64_t)p + len <= (int64_t)wb + kWin) {
           room(len);  // len <= kWin < kRing
           const uint32_t w0 = (uint32_t)((int32_t)p - wb);
@@ -266,6 +316,7 @@ __global__ __launch_bounds__(64) void snappy_kernel(const uint8_t* __restrict__ 
             o += len - c < 64u ? len - c : 64u;
           }
         }
+        SP_ADD(5);
         p += len;
         continue;
       }
@@ -301,9 +352,6 @@ __global__ __launch_bounds__(64) void snappy_kernel(const uint8_t* __restrict__ 
         }
         // else: bytes in deferred pieces come from the compressed input,
         // the rest from the ring (or, past it, memory)
-#ifdef PSG_SNAPPY_PROF
-        sp[5] += 1;
-#endif
         const uint32_t pos = slo + li;
         uint32_t from = 0xffffffffu;
         const int jj = find(pos);
@@ -329,6 +377,9 @@ __global__ __launch_bounds__(64) void snappy_kernel(const uint8_t* __restrict__ 
       }
       o += len;
     }
+#ifdef PSG_SNAPPY_PROF
+    const unsigned long long sp_end = clock64();
+#endif
     if (!st && o != ucap) st = PSG_ERR_ARG;
     if (!st) flush(o);
     if (!st && nd) {
@@ -338,7 +389,7 @@ __global__ __launch_bounds__(64) void snappy_kernel(const uint8_t* __restrict__ 
       if (lane == 0) base = atomicAdd(nlits, nd);
       base = (uint32_t)__builtin_amdgcn_readfirstlane((int)base);
       for (uint32_t i = lane; i < nd; i += 64)
-        if (base + i < lit_cap) lits[base + i] = SnappyLit{s0 + tsrc[i], out + tdst[i], tlen[i]};
+        if (base + i < lit_cap) lits[base + i] = SnappyLit{(const uint8_t*)(s0 + tsrc[i]), (uint8_t*)(out + tdst[i]), tlen[i]};
       for (uint32_t i = (base < lit_cap ? lit_cap - base : 0u); i < nd; ++i)
         for (uint32_t b = lane; b < tlen[i]; b += 64) out[tdst[i] + b] = s0[tsrc[i] + b];
     }
@@ -349,6 +400,7 @@ __global__ __launch_bounds__(64) void snappy_kernel(const uint8_t* __restrict__ 
     asm volatile("" ::"v"(pfx));  // the prefetch loads are kept
 #ifdef PSG_SNAPPY_PROF
     sp[2] = clock64() - sp_part;
+    sp[7] = clock64() - sp_end;
     if (lane == 0 && msg < 4096)
       for (int i = 0; i < 8; ++i) g_sprof[msg][i] = sp[i];
 #endif

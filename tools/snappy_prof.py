@@ -55,7 +55,8 @@ def main():
         out[name] = {"ms": e0.elapsed_time(e1),
                      "per_part": [{"refill_clk": int(r[0]), "lookup_clk": int(r[1]),
                                    "total_clk": int(r[2]), "refills": int(r[3]),
-                                   "deferred": int(r[4]), "lane_resolved": int(r[5]),
+                                   "deferred": int(r[4]), "literal_clk": int(r[5]),
+                                   "end_clk": int(r[7]),
                                    "elements": int(r[6]), "bytes_in": int(comps[base + i].size)}
                                   for i, r in enumerate(prof)]}
     got = dd.cpu().numpy()
