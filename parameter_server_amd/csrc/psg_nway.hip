@@ -65,6 +65,18 @@ constexpr int kMaxRuns = 64;        // pushes per merge (runs per tile)
 
 __device__ __forceinline__ uint32_t uni(uint32_t v) { return __builtin_amdgcn_readfirstlane(v); }
 
+// global (not flat) accesses: a flat access also counts on lgkmcnt, so the
+// LDS waits of the rank and tile stages would wait for loads in flight too
+#define AS1 __attribute__((address_space(1)))
+template <typename T>
+__device__ __forceinline__ const AS1 T* G(const T* p) {
+  return (const AS1 T*)p;
+}
+template <typename T>
+__device__ __forceinline__ AS1 T* GW(T* p) {
+  return (AS1 T*)p;
+}
+
 struct NwArgs {
   const uint64_t* const* keys;  // [K] push keys
   const void* const* vals;      // [K * M] push values (M > 0)
@@ -156,7 +168,7 @@ __global__ __launch_bounds__(256) void nw_rank_kernel(NwBatch b) {
 #pragma unroll
   for (uint32_t i = 0; i < kRkPer; ++i) {
     const uint64_t c = c0 + t + 256u * i;
-    mine[i] = c < a.ncand ? a.candk[c] : ~0ull;
+    mine[i] = c < a.ncand ? G(a.candk)[c] : ~0ull;
     acc[i] = 0;
   }
   for (uint32_t r = 0; r < a.K; ++r) {
@@ -164,7 +176,7 @@ __global__ __launch_bounds__(256) void nw_rank_kernel(NwBatch b) {
     const uint32_t L = (uint32_t)(a.cbase[r + 1] - q0);
     if (L <= kRkList) {
       __syncthreads();  // the previous list's searches are done
-      for (uint32_t x = t; x < L; x += 256) lst[x] = a.candk[q0 + x];
+      for (uint32_t x = t; x < L; x += 256) lst[x] = G(a.candk)[q0 + x];
       __syncthreads();
 #pragma unroll
       for (uint32_t i = 0; i < kRkPer; ++i) {
@@ -189,7 +201,7 @@ __global__ __launch_bounds__(256) void nw_rank_kernel(NwBatch b) {
 #pragma unroll
   for (uint32_t i = 0; i < kRkPer; ++i) {
     const uint64_t c = c0 + t + 256u * i;
-    if (c < a.ncand) a.rank[c] = a.s * acc[i];
+    if (c < a.ncand) GW(a.rank)[c] = a.s * acc[i];
   }
 }
 
@@ -315,7 +327,7 @@ __global__ __launch_bounds__(kNT) void nw_tile_kernel(NwBatch bt) {
   if (w == 0) {
     uint32_t len = 0;
     if ((uint32_t)lane < K) {
-      const uint32_t s0 = a.seg[(size_t)t * K + lane], s1 = a.seg[(size_t)(t + 1) * K + lane];
+      const uint32_t s0 = G(a.seg)[(size_t)t * K + lane], s1 = G(a.seg)[(size_t)(t + 1) * K + lane];
       len = s1 > s0 ? s1 - s0 : 0u;
       pkey[lane] = a.keys[lane] + s0;
 #pragma unroll
@@ -377,9 +389,9 @@ __global__ __launch_bounds__(kNT) void nw_tile_kernel(NwBatch bt) {
         while (roff[q + 1] <= e) ++q;
         const uint32_t i = e - roff[q];
         qs |= (uint32_t)(i == 0u) << x;
-        kk[x] = pkey[q][i];
+        kk[x] = G(pkey[q])[i];
 #pragma unroll
-        for (int mi = 0; mi < M; ++mi) vv[x][mi] = pval[q * M + mi][i];
+        for (int mi = 0; mi < M; ++mi) vv[x][mi] = G(pval[q * M + mi])[i];
       }
     }
     const uint64_t klo = t > 0 ? a.split[t - 1] : 0ull;
@@ -630,9 +642,9 @@ __global__ __launch_bounds__(kNT) void nw_tile_kernel(NwBatch bt) {
   NP_MARK(6);
   const unsigned long long base = sh_base;
   for (uint32_t e = tid; e < U; e += kNT) {
-    a.out_keys[base + e] = sk[e];
+    GW(a.out_keys)[base + e] = sk[e];
 #pragma unroll
-    for (int mi = 0; mi < M; ++mi) ((V*)a.out_vals[mi])[base + e] = sv[mi][e];
+    for (int mi = 0; mi < M; ++mi) GW((V*)a.out_vals[mi])[base + e] = sv[mi][e];
   }
   NP_MARK(7);
 #ifdef PSG_NWAY_PROF

@@ -121,8 +121,12 @@ __device__ __forceinline__ void stream_item(const JobDev& J, uint32_t p, uint32_
   const uint64_t* S = J.pkeys[p];
   const uint64_t n = J.pn[p];
   const uint32_t nt = J.ntiles;
-  const uint64_t* sp = J.split;
-  uint32_t* seg = J.seg + (size_t)p * J.segq;  // kStream: push-major, segb = 1
+  // global (not flat) accesses: a flat load also counts on lgkmcnt, so the
+  // LDS searches would wait for the splitter and key loads in flight too
+  const __attribute__((address_space(1))) uint64_t* sp =
+      (const __attribute__((address_space(1))) uint64_t*)J.split;
+  __attribute__((address_space(1))) uint32_t* seg =
+      (__attribute__((address_space(1))) uint32_t*)(J.seg + (size_t)p * J.segq);  // push-major, segb = 1
   const uint64_t i0 = (uint64_t)c * kStreamChunk;
   const uint32_t cl = (uint32_t)(n - i0 < kStreamChunk ? n - i0 : kStreamChunk);
   const bool last = i0 + cl == n;
@@ -159,7 +163,7 @@ __device__ __forceinline__ void stream_item(const JobDev& J, uint32_t p, uint32_
     const int64_t tq = gq + lane;
     const uint64_t q0 = tq <= (int64_t)nt ? sp[tq] : ~0ull;
     const uint64_t q1 = tq + 64 <= (int64_t)nt ? sp[tq + 64] : ~0ull;
-    const uint64_t kp = uni64(S[i0 - 1]);
+    const uint64_t kp = uni64(((const __attribute__((address_space(1))) uint64_t*)S)[i0 - 1]);
     const uint64_t s0 = uni64(sp[0]), sn = uni64(sp[nt]);
     uint32_t qc = 64;  // splitters <= kp in the guessed window (64+: not usable)
     if (kp >= s0 && kp < sn) {
@@ -191,7 +195,7 @@ __device__ __forceinline__ void stream_item(const JobDev& J, uint32_t p, uint32_
         T0 = g + (int64_t)cnt - 1;
         win = (int32_t)cnt;
       } else {
-        T0 = (int64_t)dev::wave_search(sp, (uint64_t)nt + 1u, kp, true, lane) - 1;
+        T0 = (int64_t)dev::wave_search(J.split, (uint64_t)nt + 1u, kp, true, lane) - 1;
       }
     }
   }
@@ -231,7 +235,8 @@ __device__ __forceinline__ void stream_item(const JobDev& J, uint32_t p, uint32_
   // element j - 1, or the previous chunk's last key)
   uint32_t bad = 0;
   {
-    const uint64_t before = i0 > 0 ? uni64(S[i0 - 1]) : 0ull;
+    const uint64_t before =
+        i0 > 0 ? uni64(((const __attribute__((address_space(1))) uint64_t*)S)[i0 - 1]) : 0ull;
 #pragma unroll
     for (int j = 0; j < kKPL; ++j) {
       const uint64_t up = (uint64_t)__shfl_up((long long)k[j], 1, 64);
