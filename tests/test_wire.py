@@ -513,6 +513,14 @@ def test_gpu_snappy_batched_parts_vs_oracle():
     assert st == [0] * len(parts)
     for g, d in zip(got, datas):
         assert g == d
+    # the same parts six times over: a launch of more than 64 parts skips the
+    # L2 prefetch of each part (psg_snappy.hip kPrefetchParts)
+    many = parts * 6
+    assert len(many) > 64
+    got, st = _gpu_snappy(many, [len(d) for d in datas] * 6)
+    assert st == [0] * len(many)
+    for g, d in zip(got, datas * 6):
+        assert g == d
     # corrupt parts among good ones
     bad = [bytes([0x04, 0x01, 0x05]), parts[1], bytes([0x06, 0x04]) + b"ab", parts[0]]
     got, st = _gpu_snappy(bad, [4, 12, 6, 11])
