@@ -120,10 +120,9 @@ __global__ __launch_bounds__(64) void snappy_kernel(const uint8_t* __restrict__ 
     // a scalar readlane: one LDS read serves several tags
     const uintptr_t mis = (uintptr_t)s0 & 3u;
     int32_t wb = -(int32_t)kWin - 64;  // part offset of win[0]; nothing loaded
-    // an aligned in-range word for the refill's out-of-range lanes (a part
-    // of fewer than 8 bytes may have none: every word is then an edge word
-    // and the address is never used for data; 0 keeps it inside the part)
-    const int64_t gs = e >= 8u ? (int64_t)((4u - (uint32_t)mis) & 3u) : 0;
+    // an aligned in-range word for the refill's out-of-range lanes (parts
+    // of at least 8 bytes; shorter ones are read byte by byte)
+    const int64_t gs = (int64_t)((4u - (uint32_t)mis) & 3u);
 #ifdef PSG_SNAPPY_PROF
     unsigned long long sp[8] = {0, 0, 0, 0, 0, 0, 0, 0};
     const unsigned long long sp_part = clock64();
@@ -145,18 +144,24 @@ __global__ __launch_bounds__(64) void snappy_kernel(const uint8_t* __restrict__ 
       // assembled byte by byte afterwards.
       uint32_t v[kR];
       bool edge = false;
+      if (e >= 8u) {  // a part of fewer than 8 bytes may hold no aligned word: bytes only
 #pragma unroll
-      for (int r = 0; r < kR; ++r) {
-        const int64_t g = (int64_t)wb + lane * 4u + 256u * r;
-        const bool inb = g >= 0 && g + 4 <= (int64_t)e;
-        edge |= !inb;
-        v[r] = *(const AS1 uint32_t*)(s0 + (inb ? g : gs));  // no select on the result
+        for (int r = 0; r < kR; ++r) {
+          const int64_t g = (int64_t)wb + lane * 4u + 256u * r;
+          const bool inb = g >= 0 && g + 4 <= (int64_t)e;
+          edge |= !inb;
+          v[r] = *(const AS1 uint32_t*)(s0 + (inb ? g : gs));  // no select on the result
+        }
+      } else {
+        edge = true;
+#pragma unroll
+        for (int r = 0; r < kR; ++r) v[r] = 0;
       }
       if (__ballot(edge)) {
 #pragma unroll
         for (int r = 0; r < kR; ++r) {
           const int64_t g = (int64_t)wb + lane * 4u + 256u * r;
-          if (!(g >= 0 && g + 4 <= (int64_t)e)) {
+          if (e < 8u || !(g >= 0 && g + 4 <= (int64_t)e)) {
             v[r] = 0;
             for (uint32_t b = 0; b < 4; ++b)
               if (g + b >= 0 && g + b < (int64_t)e) v[r] |= (uint32_t)s0[g + b] << (8 * b);
