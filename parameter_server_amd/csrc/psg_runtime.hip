@@ -1084,6 +1084,9 @@ struct psg_ctx {
   // held pushes' pinned buffers (PSG_HOLD_BUFFERS: valid until received):
   // copied by one zero-copy launch when the merge needs them (join_copy)
   psg::HostCopyBatch zc;
+  // a group of copies the caller flushes as one zero-copy launch (a
+  // compressed push's parts), held buffers or not
+  bool zc_group = false;
   int zc_flush() {
     if (zc.n == 0) return PSG_OK;
     const hipError_t e = psg::launch_host_copy_batch(zc, copy);
@@ -1099,10 +1102,11 @@ struct psg_ctx {
       // the GPU reads the caller's pinned buffer itself when both ends are
       // 16-B aligned (a DMA copy's fixed cost dominates at push sizes)
       const bool zok = zero_copy && sdev && (((uintptr_t)sdev | (uintptr_t)dst) & 15u) == 0;
-      if (zok && defer && (flags & PSG_HOLD_BUFFERS)) {
+      if (zok && ((defer && (flags & PSG_HOLD_BUFFERS)) || zc_group)) {
         if (zc.n == (uint32_t)psg::kHostCopyBatch)
           if (int rc = zc_flush()) return rc;
         zc.d[zc.n++] = psg::HostCopyDesc{sdev, dst, (uint64_t)len};
+        if (!(flags & PSG_HOLD_BUFFERS)) pinned_wait = true;
         return PSG_OK;
       }
       if (zok)
@@ -2032,9 +2036,12 @@ int psg_push_compressed(psg_ctx* c, int chl, int time, uint64_t kb, uint64_t ke,
   // decoded right before the merge that needs them (psg_ctx::flush), with
   // every other compressed push pending then, in one launch
   const int np = m + 1;
-  std::vector<uint64_t> soff(np + 1, 0);
-  soff[1] = ckeys_bytes;
-  for (int i = 0; i < m; ++i) soff[i + 2] = soff[i + 1] + cvals_bytes[i];
+  // part i at soff[i], 16-B aligned (the zero-copy read needs both ends
+  // aligned), plen[i] bytes
+  std::vector<uint64_t> soff(np + 1, 0), plen(np, 0);
+  plen[0] = ckeys_bytes;
+  for (int i = 0; i < m; ++i) plen[i + 1] = cvals_bytes[i];
+  for (int i = 0; i < np; ++i) soff[i + 1] = align_up(soff[i] + plen[i], 16);
   const size_t tb = align_up(soff[np], 256);
   void* blk = nullptr;
   if (int rc = c->dev_get(tb, &blk, c->copy)) return rc;
@@ -2044,11 +2051,16 @@ int psg_push_compressed(psg_ctx* c, int chl, int time, uint64_t kb, uint64_t ke,
   int rc = c->new_keys(n, &k);
   if (rc == PSG_OK) rc = c->dev_get(m * vb, &vblock, c->copy);
   char* b = (char*)blk;
+  // the parts in one zero-copy launch when the caller's buffers are pinned
+  c->zc_group = true;
   if (rc == PSG_OK) rc = c->h2d(b, ckeys, ckeys_bytes, true);
   for (int i = 0; rc == PSG_OK && i < m; ++i) rc = c->h2d(b + soff[i + 1], cvals[i], cvals_bytes[i], true);
+  c->zc_group = false;
+  if (rc == PSG_OK && !(c->flags & PSG_HOLD_BUFFERS)) rc = c->zc_flush();
   // the caller's buffers are free once their copies land (unless held)
   if (rc == PSG_OK) rc = c->h2d_finish();
   if (rc != PSG_OK) {
+    if (!(c->flags & PSG_HOLD_BUFFERS)) c->zc.n = 0;  // this push's queued copies only
     (void)hipStreamSynchronize(c->copy);
     c->dev_put(blk, tb);
     c->dev_put(vblock, m * vb);
@@ -2058,7 +2070,7 @@ int psg_push_compressed(psg_ctx* c, int chl, int time, uint64_t kb, uint64_t ke,
   cp.cparts = np;
   for (int i = 0; i < np; ++i) {
     cp.cbeg[i] = (uint64_t)(b + soff[i]);
-    cp.cend[i] = (uint64_t)(b + soff[i + 1]);
+    cp.cend[i] = (uint64_t)(b + soff[i] + plen[i]);
     cp.cdst[i] = i == 0 ? (uint64_t)k->d : (uint64_t)((char*)vblock + (i - 1) * vb);
     cp.ccap[i] = i == 0 ? (uint64_t)klen : (uint64_t)(n * sv);
   }
