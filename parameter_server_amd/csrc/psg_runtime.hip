@@ -1993,10 +1993,17 @@ int psg_push(psg_ctx* c, int chl, int time, uint64_t kb, uint64_t ke,
     k->host = (const uint64_t*)kdev;
   } else {
     rc = c->new_keys(n, &k);
-    // a dense push's keys are read by its check right away: not deferred
+    // the keys and values of a pinned push in one zero-copy launch (a dense
+    // push's keys are read by its check right away: not deferred)
+    c->zc_group = !dense;
     if (rc == PSG_OK) rc = c->h2d(k->d, keys, 8 * n, !dense);
   }
   if (rc == PSG_OK) rc = c->push_values(chl, time, kb, ke, k, m, vals, nullptr, dense ? &a : nullptr);
+  c->zc_group = false;
+  if (!(c->flags & PSG_HOLD_BUFFERS)) {
+    if (rc == PSG_OK) rc = c->zc_flush();
+    else c->zc.n = 0;  // this push's queued copies only (its blocks went back)
+  }
   const int rf = c->h2d_finish();
   return rc ? rc : rf;
 }
