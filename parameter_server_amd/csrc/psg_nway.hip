@@ -174,7 +174,9 @@ __global__ __launch_bounds__(256) void nw_rank_kernel(NwBatch b) {
   for (uint32_t r = 0; r < a.K; ++r) {
     const uint64_t q0 = a.cbase[r];
     const uint32_t L = (uint32_t)(a.cbase[r + 1] - q0);
-    if (L <= kRkList) {
+    // one candidate per thread (a small batch): each search straight in the
+    // list in global memory (L2-resident), no staging round per list
+    if (kRkPer > 1 && L <= kRkList) {
       __syncthreads();  // the previous list's searches are done
       for (uint32_t x = t; x < L; x += 256) lst[x] = G(a.candk)[q0 + x];
       __syncthreads();
