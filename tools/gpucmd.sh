@@ -1,11 +1,9 @@
 # scratch GPU command of the current step (overwritten per gpurun call)
 set -o pipefail
 export TMPDIR=/tmp
-O=gpurun_out/final; mkdir -p $O
-timeout -k 10 600 python3 -u -m pytest tests -m gpu -x -q --timeout 400 --timeout-method thread > $O/gputest.log 2>&1 || { echo TESTFAIL; tail -30 $O/gputest.log; exit 1; }
-tail -1 $O/gputest.log
-timeout -k 10 300 python3 -c "import __graft_entry__ as g; g.smoke()" > $O/smoke.log 2>&1 || { echo SMOKEFAIL; tail -20 $O/smoke.log; exit 1; }
-tail -1 $O/smoke.log
-timeout -k 10 600 python3 bench.py > $O/bench.json 2> $O/bench.err || { echo BENCHFAIL; tail -5 $O/bench.err; exit 1; }
-python3 -c "import json;d=json.load(open('$O/bench.json'));r=d['roofline'];print('value %.4e kern %.4f part %.4f frac %.3f step %.3f'%(d['value'],r['kernel_ms'],r['partition_ms'],r['frac'],r['step_frac']));print(' '.join('%s %.4f'%(k,v['ms']) for k,v in d['rows'].items()))"
+O=gpurun_out/ab; mkdir -p $O
+for rep in 1 2; do for v in r16 r4 r1; do
+  PSG_LIB_PATH=$PWD/build/$v/libpsg.so timeout -k 10 300 python3 tools/nway_probe.py > $O/nw_$v.txt 2>&1 || { echo FAIL $v; tail -5 $O/nw_$v.txt; exit 1; }
+  echo "$rep $v $(grep batch $O/nw_$v.txt | tail -1)"
+done; done
 echo done
