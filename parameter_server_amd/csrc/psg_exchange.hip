@@ -180,6 +180,9 @@ struct LoopPair {
   hipStream_t rstream = nullptr;
   // result
   bool have_send = false, have_recv = false, done = false;
+  // one side gave up waiting (timeout): the other side completes the pair
+  // with an error and no copy (the buffers of the side that left may be gone)
+  bool cancelled = false;
   int status = PSG_OK;
   hipEvent_t copied = nullptr;
   int users = 2;  // sender + receiver; the last one to leave frees the events
@@ -195,6 +198,10 @@ struct LoopHub {
 
   void complete(LoopPair& P) {  // with mu held; both sides present
     P.done = true;
+    if (P.cancelled) {
+      P.status = PSG_ERR_DEVICE;
+      return;
+    }
     if (P.sbytes != P.rbytes) {
       P.status = PSG_ERR_SIZE;
       return;
@@ -288,14 +295,19 @@ int loop_group(psg_comm* c, hipStream_t st, const std::vector<XOp>& ops) {
     }
     if (P->status != PSG_OK && rc == PSG_OK)
       rc = fail(P->status, "loopback rank %d: %s", me,
-                P->status == PSG_ERR_SIZE ? "send and receive sizes differ" : "device copy failed");
+                P->status == PSG_ERR_SIZE ? "send and receive sizes differ"
+                : P->cancelled            ? "the peer left the group (timeout)"
+                                          : "device copy failed");
   }
+  // pairs still missing their peer: cancelled, so a peer that joins later
+  // fails them instead of copying from or into this rank's buffers
+  for (auto& P : mine)
+    if (!P->done) P->cancelled = true;
   // a send buffer is reusable once its copy ran: later work on `st` waits
   for (size_t i = 0; rc == PSG_OK && i < ops.size(); ++i)
     if (ops[i].send && mine[i]->copied && hipStreamWaitEvent(st, mine[i]->copied, 0) != hipSuccess)
       rc = fail(PSG_ERR_DEVICE, "loopback: stream wait");
-  for (auto& P : mine)
-    if (P->done) LoopHub::leave(*P);
+  for (auto& P : mine) LoopHub::leave(*P);
   return rc;
 }
 

@@ -318,10 +318,11 @@ struct JobTable {
       if (j >= (1ull << 27)) return fail(PSG_ERR_ARG, "too many jobs");
     }
     // the cursor form: plans (resident index) of search-mode jobs of at most
-    // kCursorPushes pushes whose pieces fit kr <= 3 rounds (mean + 4 sigma
-    // keys per push per tile <= 192; longer ones would finish round by round)
-    // opt-in (PSG_FORM_CURSOR): measured slower than partition + tile
-    // kernel on cfg2 (0.509 vs 0.437 ms per step)
+    // kCursorPushes pushes; kr = the rounds of 64 keys loaded per push per
+    // tile (mean + 4 sigma keys, at most 3: longer pieces finish round by
+    // round in the fold step).  Opt-in only (PSG_FORM_CURSOR), with no size
+    // gate: measured slower than partition + tile kernel on cfg2 (0.509 vs
+    // 0.437 ms per step)
     cursor = index && !dense && !pack && !wide && knob_cursor == 1 && tiles > 0;
     for (size_t j = 0; cursor && j < jobs.size(); ++j) {
       const JobSpec& s = jobs[j];
@@ -334,7 +335,6 @@ struct JobTable {
       for (uint64_t n : I.pn) kv += (double)n;
       const double piece = I.np && I.ntiles ? kv / ((double)I.np * I.ntiles) : 0.0;
       const double need = piece + 4.0 * std::sqrt(piece) + 1.0;
-      if (need > 192.0 && knob_cursor != 1) cursor = false;
       I.kr = (uint32_t)std::min(3.0, std::max(1.0, std::ceil(need / 64.0)));
     }
     if (cursor) {  // one kernel instance: the jobs' largest round count
@@ -344,10 +344,10 @@ struct JobTable {
     }
     // the packed cursor form: plans (resident index) of packed-round jobs of
     // at most 256 pushes whose pointers leave the top 16 bits free (the
-    // kernel keeps a piece's length there) and whose tiles' elements fit one
-    // pass (mean + 6 sigma <= 2,560; larger ones take more groups per tile)
-    // opt-in (PSG_FORM_CURSOR): measured slower than partition + packed
-    // kernel on cfg5 (1.34 vs 0.77 ms per step)
+    // kernel keeps a piece's length there); tiles whose elements overflow one
+    // pass take more groups.  Opt-in only (PSG_FORM_CURSOR), with no size
+    // gate: measured slower than partition + packed kernel on cfg5 (1.34 vs
+    // 0.77 ms per step)
     pcursor = index && !dense && pack && knob_cursor == 1 && tiles > 0;
     for (size_t j = 0; pcursor && j < jobs.size(); ++j) {
       const JobSpec& s = jobs[j];
@@ -361,10 +361,6 @@ struct JobTable {
         for (int i = 0; i < m; ++i) hi |= ((uint64_t)s.pvals[p * m + i] >> 48) != 0;
         if (hi) pcursor = false;
       }
-      double kv = 0;
-      for (uint64_t n : I.pn) kv += (double)n;
-      const double per_tile = I.ntiles ? kv / I.ntiles : 0.0;
-      if (per_tile + 6.0 * std::sqrt(per_tile) > 2560.0 && knob_cursor != 1) pcursor = false;
     }
     bxs = pcursor ? (uint32_t)psg::kPackCursorPushes : 32u;
     if (cursor || pcursor) {
@@ -783,9 +779,19 @@ struct CacheKey {
     return chl != o.chl ? chl < o.chl : kb != o.kb ? kb < o.kb : ke < o.ke;
   }
 };
+// The device check of a carried signature (keys + values message): its
+// counter and the event after it on `copy`.  The entry that stored those
+// keys is restorable only once the check passed; the reference checks before
+// it stores (remote_node.cc:161-165).
+struct SigCheck {
+  unsigned long long* d = nullptr;
+  hipEvent_t ev = nullptr;
+};
+using SigCheckRef = std::shared_ptr<SigCheck>;
 struct CacheEntry {
   uint32_t sig = 0;
   KeyRef keys;
+  SigCheckRef chk;  // null: checked (or stored by a key-only message, checked at once)
 };
 
 // pinned host memory, and the address the device reads it at
@@ -824,6 +830,13 @@ struct Filter {
     if (ext_used) (void)hipStreamSynchronize(ext);
     ext_used = false;
   }
+  // the filter's operations run in call order whatever streams they are
+  // enqueued on (the reference's calls are sequential): each one waits for
+  // the event recorded after the previous one when their streams differ.
+  // The binned insert reuses d_bins and writes table dwords with plain
+  // read-modify-write stores, so two inserts must never overlap.
+  hipEvent_t last = nullptr;
+  hipStream_t last_s = nullptr;
 };
 
 }  // namespace
@@ -859,6 +872,14 @@ struct psg_ctx {
   };
   std::multimap<size_t, Pooled> pool;
   size_t pool_bytes = 0;
+  // the real size of every block this pool made (carved or allocated): a
+  // reused block may be up to twice the size asked for, and the counts of
+  // the pool and the slabs add and subtract that same size
+  std::unordered_map<const void*, size_t> bsize;
+  size_t real_size(const void* p, size_t b) const {
+    auto it = bsize.find(p);
+    return it == bsize.end() ? b : it->second;
+  }
   std::vector<hipEvent_t> free_ev;
   static constexpr size_t kPoolCap = size_t(8) << 30;
   // ---- slabs: blocks up to kSlabBlock bytes (staged pushes, cached keys,
@@ -916,6 +937,10 @@ struct psg_ctx {
         } else {
           ++it;
         }
+      }
+      for (auto it = bsize.begin(); it != bsize.end();) {
+        const char* q = (const char*)it->first;
+        it = (q >= s.p && q < s.p + s.size) ? bsize.erase(it) : std::next(it);
       }
       if (slab_cur >= s.p && slab_cur <= s.p + s.size) {
         slab_cur = nullptr;
@@ -977,6 +1002,7 @@ struct psg_ctx {
         slab_cur += b;
         slab_left -= b;
         slabs[(size_t)slab_of(*p)].carved += b;
+        bsize[*p] = b;
         return PSG_OK;
       }
     }
@@ -986,6 +1012,7 @@ struct psg_ctx {
       if (!reclaim_slabs()) return fail(PSG_ERR_OOM, "device allocation of %zu bytes", b);
       HIP_TRY(hipMalloc(p, b));
     }
+    bsize[*p] = b;
     return PSG_OK;
   }
   void dev_put(void* p, size_t b) {
@@ -993,7 +1020,7 @@ struct psg_ctx {
     // a deferred copy may target the block: issue it and order it before
     // the block's release event on `stream`
     if (zc.n) (void)join_copy();
-    b = align_up(b ? b : 1, 4096);
+    b = real_size(p, align_up(b ? b : 1, 4096));
     const int si = slab_of(p);  // a carved block is pooled (or counted back) always
     const bool carved = si >= 0;
     if (carved) {
@@ -1005,7 +1032,10 @@ struct psg_ctx {
         hipEventRecord(e, stream) != hipSuccess) {
       if (e) free_ev.push_back(e);
       (void)hipStreamSynchronize(stream);
-      if (!carved) (void)hipFree(p);  // a carved block goes with its slab
+      if (!carved) {  // a carved block goes with its slab
+        (void)hipFree(p);
+        bsize.erase(p);
+      }
       return;
     }
     pool.emplace(b, Pooled{p, e});
@@ -1020,6 +1050,7 @@ struct psg_ctx {
     }
     pool.clear();
     pool_bytes = 0;
+    bsize.clear();
     for (auto& sl : slabs) (void)hipFree(sl.p);
     slabs.clear();
     slab_cur = nullptr;
@@ -1027,6 +1058,43 @@ struct psg_ctx {
     slab_idle = 0;
     for (hipEvent_t e : free_ev) (void)hipEventDestroy(e);
     free_ev.clear();
+  }
+
+  // the carried signature of resident keys checked on `copy` into a counter
+  // of its own (the entry's), after the key copy
+  int sig_check_pending(const KeyRef& k, uint32_t sig, SigCheckRef* out) {
+    SigCheck* s = new SigCheck();
+    if (int rc = dev_get(8, (void**)&s->d, copy)) {
+      delete s;
+      return rc;
+    }
+    int rc = event(&s->ev);
+    if (rc == PSG_OK && (hipMemsetAsync(s->d, 0, 8, copy) != hipSuccess ||
+                         psg::launch_sig_check((const uint8_t*)k->d, 8 * k->n, PSG_MAX_SIG_LEN,
+                                               sig, s->d, copy) != hipSuccess ||
+                         hipEventRecord(s->ev, copy) != hipSuccess))
+      rc = fail(PSG_ERR_DEVICE, "signature check launch");
+    if (rc != PSG_OK) {
+      (void)hipStreamSynchronize(copy);
+      if (s->ev) free_ev.push_back(s->ev);
+      dev_put(s->d, 8);
+      delete s;
+      return rc;
+    }
+    *out = SigCheckRef(s, [this](SigCheck* q) {
+      (void)hipEventSynchronize(q->ev);  // the counter block is not reused under the check
+      free_ev.push_back(q->ev);
+      dev_put(q->d, 8);
+      delete q;
+    });
+    return PSG_OK;
+  }
+  // the result of a pending check (host wait, once per stored entry)
+  int sig_check_result(const SigCheckRef& s, bool* ok) {
+    HIP_TRY(hipEventSynchronize(s->ev));
+    HIP_TRY(hipMemcpy(h_small + 11, s->d, 8, hipMemcpyDeviceToHost));
+    *ok = h_small[11] == 0;
+    return PSG_OK;
   }
 
   int new_keys(size_t n, KeyRef* out) {
@@ -1530,6 +1598,10 @@ int psg_create(int device, int dtype, unsigned flags, psg_ctx** out) {
   return PSG_OK;
 }
 
+namespace {
+void filter_release(psg_ctx* c, Filter& F);
+}  // namespace
+
 int psg_destroy(psg_ctx* c) {
   if (!c) return PSG_OK;
   (void)hipSetDevice(c->device);
@@ -1549,11 +1621,7 @@ int psg_destroy(psg_ctx* c) {
     if (kv.second.hev) (void)hipEventDestroy(kv.second.hev);
   }
   c->ch.clear();
-  for (auto& kv : c->ff) {
-    kv.second.sync_ext();
-    c->dev_put(kv.second.d_table, psg::cm_table_bytes(kv.second.n));
-    c->dev_put(kv.second.d_bins, kv.second.bins_bytes);
-  }
+  for (auto& kv : c->ff) filter_release(c, kv.second);
   c->ff.clear();
   if (c->stream) (void)hipStreamSynchronize(c->stream);
   for (auto& f : c->fly) c->free_ev.push_back(f.ev);
@@ -2123,9 +2191,13 @@ int push_cached_impl(psg_ctx* c, int sender, int chl, int time, uint64_t kb, uin
     }
     uint32_t got = 0;  // crc32c::Value of no bytes
     // with values (m > 0) the check runs on the device and a mismatch is
-    // reported by psg_received (no host wait); a key-only message merges
-    // into the channel's keys at once, so it is checked before that
+    // reported by psg_received (no host wait); the entry stores the keys as
+    // pending on that check: a restore waits for its result and fails (and
+    // drops the entry) if it failed.  A key-only message merges into the
+    // channel's keys at once, so it is checked before that
+    SigCheckRef pend;
     if (nkeys && m > 0) {
+      if (int rc = c->sig_check_pending(k, sig, &pend)) return rc;
       sigcheck = true;
       got = sig;
     } else if (nkeys) {
@@ -2143,9 +2215,24 @@ int push_cached_impl(psg_ctx* c, int sender, int chl, int time, uint64_t kb, uin
     CacheEntry& e = c->kcache[ck];
     e.sig = sig;
     e.keys = k;
+    e.chk = pend;
   } else {
     // keys restored from the cache (remote_node.cc:172-176)
     auto it = c->kcache.find(ck);
+    if (it != c->kcache.end() && it->second.chk) {
+      // stored by a keyed message whose device check has not been read yet
+      bool ok = false;
+      if (int rc = c->sig_check_result(it->second.chk, &ok)) return rc;
+      if (!ok) {
+        const uint32_t bad = it->second.sig;
+        c->kcache.erase(it);
+        return fail(PSG_ERR_SIGNATURE,
+                    "key cache of channel %d [%llu,%llu): the stored keys did not match their "
+                    "signature %08x",
+                    chl, (unsigned long long)kb, (unsigned long long)ke, bad);
+      }
+      it->second.chk.reset();
+    }
     const uint32_t have = it == c->kcache.end() ? 0u : it->second.sig;
     if (sig != have)  // CHECK_EQ(sig, cache.first)
       return fail(PSG_ERR_SIGNATURE, "key cache of channel %d [%llu,%llu): signature %08x != %08x",
@@ -2382,9 +2469,7 @@ int psg_freq_clear(psg_ctx* c, int chl) {
   std::lock_guard<std::mutex> l(c->mu);
   auto it = c->ff.find(chl);
   if (it != c->ff.end()) {
-    it->second.sync_ext();
-    c->dev_put(it->second.d_table, psg::cm_table_bytes(it->second.n));
-    c->dev_put(it->second.d_bins, it->second.bins_bytes);
+    filter_release(c, it->second);
     c->ff.erase(it);
   }
   return PSG_OK;
@@ -2420,6 +2505,32 @@ int filter_bins(psg_ctx* c, Filter* F, size_t n, hipStream_t s) {
   F->bins_bytes = need;
   return PSG_OK;
 }
+
+// order an operation on stream s after the filter's previous one
+int filter_order(Filter* F, hipStream_t s) {
+  if (F->last && F->last_s != s) HIP_TRY(hipStreamWaitEvent(s, F->last, 0));
+  return PSG_OK;
+}
+// ... and mark it as the filter's last
+int filter_mark(psg_ctx* c, Filter* F, hipStream_t s) {
+  if (!F->last)
+    if (int rc = c->event(&F->last)) return rc;
+  HIP_TRY(hipEventRecord(F->last, s));
+  F->last_s = s;
+  return PSG_OK;
+}
+void filter_release(psg_ctx* c, Filter& F) {
+  F.sync_ext();
+  if (F.last) {
+    (void)hipEventSynchronize(F.last);
+    c->free_ev.push_back(F.last);
+    F.last = nullptr;
+  }
+  c->dev_put(F.d_table, psg::cm_table_bytes(F.n));
+  c->dev_put(F.d_bins, F.bins_bytes);
+  F.d_table = nullptr;
+  F.d_bins = nullptr;
+}
 }  // namespace
 
 int psg_freq_insert_dev(psg_ctx* c, int chl, const uint64_t* keys, const uint32_t* counts,
@@ -2428,12 +2539,13 @@ int psg_freq_insert_dev(psg_ctx* c, int chl, const uint64_t* keys, const uint32_
   std::lock_guard<std::mutex> l(c->mu);
   Filter* F;
   if (int rc = filter_of(c, chl, &F)) return rc;
+  if (int rc = filter_order(F, (hipStream_t)stream)) return rc;
   if (int rc = filter_bins(c, F, n, (hipStream_t)stream)) return rc;
   HIP_TRY(psg::launch_cm_insert(keys, counts, n, F->d_table, F->n, F->k, F->d_bins,
                                 F->bins_bytes, (hipStream_t)stream));
   F->ext = (hipStream_t)stream;
   F->ext_used = true;
-  return PSG_OK;
+  return filter_mark(c, F, (hipStream_t)stream);
 }
 
 size_t psg_freq_query_scratch_bytes(size_t n) { return psg::cm_query_scratch_bytes(n); }
@@ -2445,11 +2557,12 @@ int psg_freq_query_dev(psg_ctx* c, int chl, const uint64_t* keys, size_t n, int 
   std::lock_guard<std::mutex> l(c->mu);
   Filter* F;
   if (int rc = filter_of(c, chl, &F)) return rc;
+  if (int rc = filter_order(F, (hipStream_t)stream)) return rc;
   HIP_TRY(psg::launch_cm_query(keys, n, F->d_table, F->n, F->k, freq, out, nout, scratch,
                                (hipStream_t)stream));
   F->ext = (hipStream_t)stream;
   F->ext_used = true;
-  return PSG_OK;
+  return filter_mark(c, F, (hipStream_t)stream);
 }
 
 int psg_freq_insert(psg_ctx* c, int chl, const uint64_t* keys, const uint32_t* counts,
@@ -2467,6 +2580,7 @@ int psg_freq_insert(psg_ctx* c, int chl, const uint64_t* keys, const uint32_t* c
   int rc = c->h2d(blk, keys, 8 * n);
   if (rc == PSG_OK) rc = c->h2d((char*)blk + kb, counts, 4 * n);
   if (rc == PSG_OK) rc = c->join_copy();
+  if (rc == PSG_OK) rc = filter_order(F, c->stream);
   if (rc == PSG_OK) rc = filter_bins(c, F, n, c->stream);
   if (rc == PSG_OK) {
     hipError_t e = psg::launch_cm_insert((const uint64_t*)blk, (const uint32_t*)((char*)blk + kb),
@@ -2474,6 +2588,7 @@ int psg_freq_insert(psg_ctx* c, int chl, const uint64_t* keys, const uint32_t* c
                                          c->stream);
     if (e != hipSuccess) rc = fail(PSG_ERR_DEVICE, "freq insert: %s", hipGetErrorString(e));
   }
+  if (rc == PSG_OK) rc = filter_mark(c, F, c->stream);
   c->dev_put(blk, b);
   const int rf = c->h2d_finish();
   return rc ? rc : rf;
@@ -2496,8 +2611,10 @@ int psg_freq_query(psg_ctx* c, int chl, const uint64_t* keys, size_t n, int freq
   void* d_s = (char*)c->scratch + 2 * kb;
   if (int rc = c->h2d(d_keys, keys, 8 * n)) return rc;
   if (int rc = c->join_copy()) return rc;
+  if (int rc = filter_order(F, c->stream)) return rc;
   HIP_TRY(psg::launch_cm_query(d_keys, n, F->d_table, F->n, F->k, freq, d_out, c->d_small + 7,
                                d_s, c->stream));
+  if (int rc = filter_mark(c, F, c->stream)) return rc;
   HIP_TRY(hipMemcpyAsync(c->h_small + 7, c->d_small + 7, 8, hipMemcpyDeviceToHost, c->stream));
   HIP_TRY(hipStreamSynchronize(c->stream));
   const size_t m = (size_t)c->h_small[7];
@@ -2513,6 +2630,7 @@ int psg_freq_table(psg_ctx* c, int chl, uint8_t* out, size_t n) {
   if (int rc = filter_of(c, chl, &F)) return rc;
   if (n > F->n) return fail(PSG_ERR_ARG, "table copy of %zu > %u counters", n, F->n);
   if (int rc = set_dev(c->device)) return rc;
+  if (int rc = filter_order(F, c->stream)) return rc;
   if (n) HIP_TRY(hipMemcpyAsync(out, F->d_table, n, hipMemcpyDeviceToHost, c->stream));
   HIP_TRY(hipStreamSynchronize(c->stream));
   return PSG_OK;

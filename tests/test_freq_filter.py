@@ -9,6 +9,8 @@ countmin.h cannot be compiled here (glog through shared_array_inl.h); it is
 checked against an independent pure-Python restatement.  The GPU table is
 compared byte for byte and the filtered keys in order.
 """
+import ctypes as C
+
 import numpy as np
 import pytest
 
@@ -190,4 +192,42 @@ def test_gpu_freq_filter_large_table_cas_form():
     _lib.check(v._L.psg_freq_insert(v._h, 1, keys.ctypes.data, counts.ctypes.data, keys.size))
     O.cm_insert(t, nn, kk, keys, counts)
     assert np.array_equal(_table(v, 1, nn), t)
+    v.close()
+
+
+@pytest.mark.gpu
+def test_gpu_freq_filter_inserts_on_two_streams_in_call_order():
+    """Binned inserts share the filter's record scratch and write table dwords
+    with plain stores: an insert on a caller stream, then inserts on the
+    context stream and on a second caller stream, issued back to back with no
+    host wait, must land exactly as sequential calls (the reference's
+    insertKeys calls are sequential, frequency_filter.h:37-43)."""
+    import torch
+    assert torch.cuda.is_available()
+    from parameter_server_amd import _lib
+    rng = np.random.default_rng(9)
+    v = _ctx()
+    n = 1 << 22
+    _lib.check(v._L.psg_freq_resize(v._h, 4, n, 4))
+    t, nn, kk = O.cm_resize(n, 4)
+    s1, s2 = torch.cuda.Stream(), torch.cuda.Stream()
+    batches = []
+    for b in range(3):
+        keys = np.unique(zipf_keys(rng, 300_000))
+        counts = rng.integers(1, 400, keys.size).astype(np.uint32)
+        batches.append((keys, counts))
+    dev = [(torch.from_numpy(k.view(np.int64)).cuda(), torch.from_numpy(c.view(np.int32)).cuda())
+           for k, c in batches]
+    torch.cuda.synchronize()
+    k0, c0 = dev[0]
+    _lib.check(v._L.psg_freq_insert_dev(v._h, 4, k0.data_ptr(), c0.data_ptr(), batches[0][0].size,
+                                        C.c_void_p(s1.cuda_stream)))
+    _lib.check(v._L.psg_freq_insert(v._h, 4, batches[1][0].ctypes.data, batches[1][1].ctypes.data,
+                                    batches[1][0].size))
+    k2, c2 = dev[2]
+    _lib.check(v._L.psg_freq_insert_dev(v._h, 4, k2.data_ptr(), c2.data_ptr(), batches[2][0].size,
+                                        C.c_void_p(s2.cuda_stream)))
+    for keys, counts in batches:
+        O.cm_insert(t, nn, kk, keys, counts)
+    assert np.array_equal(_table(v, 4, nn), t)
     v.close()

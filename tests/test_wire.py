@@ -263,6 +263,50 @@ def test_key_cache_signature_errors_and_erase():
 
 
 @pytest.mark.gpu
+def test_key_cache_bad_signature_is_never_restored():
+    """The reference checks a carried signature before it stores the keys
+    (remote_node.cc:161-165).  Here a keys + values message is checked on the
+    device after return; the entry it stored is pending on that check, so a
+    later signature-only message with the same signature must fail (and the
+    entry is dropped) instead of restoring keys that never matched.  The same
+    holds when the keyed message itself failed a later host check (values
+    size), and a good entry restores after its check passed."""
+    import torch
+    assert torch.cuda.is_available()
+    from parameter_server_amd._lib import PSGError, PSG_ERR_SIGNATURE, PSG_ERR_SIZE
+    rng = np.random.default_rng(14)
+    D = np.unique(rng.integers(0, 1 << 40, 6000, dtype=np.uint64))
+    k = np.sort(rng.choice(D, 800, replace=False))
+    x = rng.standard_normal(k.size).astype(np.float32)
+    v = _kvv()
+    v.setValue(_msg(D))
+    bad = O.key_signature(k) ^ 0x5A5A
+    v.setValue(_msg(k, [x], t=1, sig=bad, sender=3))  # stored pending, check fails on the device
+    with pytest.raises(PSGError) as e:
+        v.setValue(_msg(None, [x], t=2, sig=bad, has_key=False, sender=3))
+    assert e.value.status == PSG_ERR_SIGNATURE
+    assert v.key_cache_bytes(3) == 0  # the entry was dropped
+    with pytest.raises(PSGError) as e:
+        v.received(1)
+    assert e.value.status == PSG_ERR_SIGNATURE
+    # a keyed message that fails its values-size check after storing
+    with pytest.raises(PSGError) as e:
+        v.setValue(_msg(k, [x[:-1]], t=3, sig=bad, sender=4))
+    assert e.value.status == PSG_ERR_SIZE
+    with pytest.raises(PSGError) as e:
+        v.setValue(_msg(None, [x], t=3, sig=bad, has_key=False, sender=4))
+    assert e.value.status == PSG_ERR_SIGNATURE
+    # a good signature: stored pending, restored once its check passed
+    good = O.key_signature(k)
+    v.setValue(_msg(k, [x], t=5, sig=good, sender=5))
+    v.setValue(_msg(None, [x], t=5, sig=good, has_key=False, sender=5))
+    (_, got), = v.received(5)
+    want = O.aggregate(D, 0, (1 << 64) - 1, [(k, [x])] * 2)[3][0]
+    assert np.array_equal(_bits(got), _bits(want))
+    v.close()
+
+
+@pytest.mark.gpu
 def test_key_cache_replaced_while_pushes_pending_and_key_only():
     """An entry replaced (new keys, same channel/range) while pushes restored
     from the old one are still pending: those pushes keep the old resident

@@ -1,9 +1,9 @@
 # scratch GPU command of the current step (overwritten per gpurun call)
 set -o pipefail
 export TMPDIR=/tmp
-O=gpurun_out/ab; mkdir -p $O
-for rep in 1 2; do for v in r16 r4 r1; do
-  PSG_LIB_PATH=$PWD/build/$v/libpsg.so timeout -k 10 300 python3 tools/nway_probe.py > $O/nw_$v.txt 2>&1 || { echo FAIL $v; tail -5 $O/nw_$v.txt; exit 1; }
-  echo "$rep $v $(grep batch $O/nw_$v.txt | tail -1)"
-done; done
+O=gpurun_out/r05a; mkdir -p $O
+timeout -k 10 400 python3 -u -m pytest tests -m gpu -x -q --timeout 120 --timeout-method thread > $O/tests.log 2>&1 || { echo TESTS FAILED; tail -30 $O/tests.log; exit 1; }
+tail -2 $O/tests.log
+timeout -k 10 300 python3 bench.py --no-cpu-baseline > $O/bench.json 2> $O/bench.err || { echo bench failed; tail -5 $O/bench.err; exit 1; }
+python3 -c "import json;d=json.load(open('$O/bench.json'));print(d['value'],d['ms_per_step'],d['roofline']['frac'],d['roofline'].get('kernel_ms'))"
 echo done
