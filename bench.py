@@ -93,6 +93,8 @@ def parse():
     ap.add_argument("--no-f64", action="store_true",
                     help="skip the f64 (the reference apps' double) cfg2 block of the default line")
     ap.add_argument("--cfg5-steps", type=int, default=10)
+    ap.add_argument("--no-shard8", action="store_true",
+                    help="skip the cfg5 block's one-GPU per-shard leg (shard_of_8)")
     ap.add_argument("--cfg5-unsliced-child", action="store_true",
                     help=argparse.SUPPRESS)  # internal: the unsliced leg in its own process
     ap.add_argument("--cpu-seconds", type=float, default=10.0)
@@ -512,7 +514,68 @@ def cfg5_block(args, rank, world, bounds, dist, dev, local, stream):
     else:
         out["one_gpu_ms_per_step"] = out["ms_per_step"]
         out["speedup_vs_1gpu"] = 1.0
+        if not args.no_shard8:
+            out["shard_of_8"] = cfg5_shard_of_8(args, pushes, dev, local, stream,
+                                                out["ms_per_step"])
     return out
+
+
+def cfg5_shard_of_8(args, pushes, dev, local, stream, whole_ms):
+    """One-GPU per-rank measurement (NOT a scaling result): each of the 8
+    evenDivide(8) shards of the cfg5 workload (range.h:85-98,
+    linear_method.cc:137-145) merged exactly as rank r of an 8-GPU job runs
+    it in the sliced mode -- its pieces of all 256 pushes
+    (sliceKeyOrderedMsg, message.h:89-123), partition + aggregate, K steps
+    -- one shard after the other on this GPU.  The max per-shard step bounds
+    what 8 GPUs can reach on this path: whole-workload step / max shard step
+    is the speedup ceiling before any transport cost.  `launch_floor_ms` is
+    the same two-launch step on a one-tile plan: the fixed cost per step
+    that does not shrink with the shard."""
+    from parameter_server_amd import synth
+    from parameter_server_amd.kv_vector import shard_bounds
+    sh = stream.cuda_stream
+    K = args.cfg5_steps
+    b8 = shard_bounds(8)
+    shards = []
+    for r in range(8):
+        pieces = synth.shard_pieces(pushes, b8, r)
+        D = np.unique(np.concatenate([k for k, _ in pieces]))
+        plan, keep, _ = make_plan([(D, pieces)], dev, local)
+        plan.run(sh)
+        assert args.no_check or np.array_equal(
+            plan.matched(), np.array([k.size for k, _ in pieces], np.uint64))
+        wall, (part_ms, agg_ms) = timed_stages([lambda: plan.run_stage(0, sh),
+                                                lambda: plan.run_stage(1, sh)], K, 2, stream, None)
+        nbytes = int(plan.bytes)
+        shards.append({"shard": r, "slots": int(D.size), "kv": int(plan.kv_pairs),
+                       "ms_per_step": wall / K * 1e3, "partition_ms": part_ms,
+                       "kernel_ms": agg_ms, "bytes_per_launch": nbytes,
+                       "frac": nbytes / (agg_ms * 1e-3) / 1e9 / HBM_PEAK_GBPS,
+                       "step_frac": nbytes / (wall / K) / 1e9 / HBM_PEAK_GBPS,
+                       "form": kernel_name(plan)})
+        del plan, keep
+    # the fixed per-step cost: the same two launches on a one-tile plan
+    rng = np.random.default_rng(0)
+    Dt = np.unique(rng.integers(0, 1 << 40, 2048, dtype=np.uint64))[:1024]
+    tiny = [(np.sort(rng.choice(Dt, 64, replace=False)), [np.ones(64, np.float32)])
+            for _ in range(8)]
+    plan, keep, _ = make_plan([(Dt, tiny)], dev, local)
+    wall, (tp, ta) = timed_stages([lambda: plan.run_stage(0, sh),
+                                   lambda: plan.run_stage(1, sh)], K, 2, stream, None)
+    floor = {"ms_per_step": wall / K * 1e3, "partition_ms": tp, "kernel_ms": ta}
+    del plan, keep
+    steps = [x["ms_per_step"] for x in shards]
+    return {
+        "what": "one-GPU per-rank measurement, not a scaling result: each evenDivide(8) shard "
+                "of the cfg5 workload merged (sliced ingress) on this GPU as its rank would",
+        "max_ms_per_step": max(steps), "min_ms_per_step": min(steps),
+        "max_kernel_ms": max(x["kernel_ms"] for x in shards),
+        "max_partition_ms": max(x["partition_ms"] for x in shards),
+        "whole_ms_per_step": whole_ms,
+        "speedup_ceiling_8": whole_ms / max(steps),
+        "launch_floor": floor,
+        "shards": shards,
+    }
 
 
 def cfg5_unsliced_child(args, rank, world, dist):

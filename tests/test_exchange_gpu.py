@@ -328,3 +328,99 @@ def test_loopback_bad_rank_fails_everywhere_without_hang():
         x.close()
     for c in comms:
         shard.destroy_comm(c)
+
+
+@pytest.mark.timeout(900)
+@pytest.mark.parametrize("direct", [False, True])
+def test_loopback_8_ranks_full_cfg5(direct):
+    """BASELINE.json configs[4] at its real size through the 8-rank exchange:
+    256 pushes x 262,144 murmur-shuffled uniform keys (1e9-rank space, f32),
+    32 whole pushes held per rank (the bench's unsliced leg at N = 8; ranks
+    are loopback ranks of one process on one GPU, psg_comm_init_loopback).
+    Per rank: the received counts equal the oracle's sliceKeyOrderedMsg cut
+    (message.h:89-123) at evenDivide(8) (range.h:85-98) of every source's
+    pushes; the received keys and values are those pieces in (source, push)
+    order, byte for byte; the HIP merge of the received buffers equals the
+    HIP merge of the same pieces staged separately (the sliced leg) and the
+    oracle's serialSetValue over the rank's range (orc_aggregate_scatter_serial),
+    bit for bit.  Pack mode and direct mode."""
+    import torch
+    from parameter_server_amd import shard, synth
+    from parameter_server_amd._lib import PSG_F32
+    from parameter_server_amd.kv_vector import MergePlan, shard_bounds
+    S = 8
+    _, pushes = synth.uniform_pushes(seed=5, union=False)
+    P = len(pushes)
+    assert P == 256 and all(k.size == 262144 for k, _ in pushes)
+    PR = P // S
+    b = shard_bounds(S)
+    dev = torch.device("cuda", 0)
+    comms = shard.loopback_comms(0, S)
+    held = [_dev_pushes(pushes[r * PR:(r + 1) * PR], dev) for r in range(S)]
+    xs, err = _threads([lambda r=r: shard.RcclExchange(comms[r], held[r], S, PSG_F32)
+                        for r in range(S)])
+    assert not any(err), err
+    try:
+        for x in xs:
+            x.set_direct(direct)
+        streams = [torch.cuda.Stream(device=dev) for _ in range(S)]
+        for _ in range(2):
+            _, err = _threads([lambda r=r: xs[r].run(streams[r].cuda_stream) for r in range(S)])
+            assert not any(err), err
+        torch.cuda.synchronize()
+        ALL = (0, (1 << 64) - 1)
+        cut = [O.slice_key_ordered(k, *ALL, b)[0].astype(np.int64) for k, _ in pushes]
+        assert sum(x.nrecv for x in xs) == P * 262144
+        for r in range(S):
+            x = xs[r]
+            assert x.status() == 0
+            want_cnt = np.array([[cut[s * PR + p][r + 1] - cut[s * PR + p][r] for p in range(PR)]
+                                 for s in range(S)], np.int64)
+            assert np.array_equal(x.recv_cnt, want_cnt), f"rank {r} recv counts"
+            pieces = []
+            for s in range(S):
+                for p in range(PR):
+                    k, vs = pushes[s * PR + p]
+                    a, e = int(cut[s * PR + p][r]), int(cut[s * PR + p][r + 1])
+                    assert int(x.recv_off[s, p]) == sum(pc[0].size for pc in pieces)
+                    pieces.append((k[a:e], [vs[0][a:e]]))
+            rk = d2h(x.recv_keys_ptr, 8 * x.nrecv).view(np.uint64)
+            rv = d2h(x.recv_vals_ptr[0], 4 * x.nrecv)
+            assert np.array_equal(rk, np.concatenate([k for k, _ in pieces])), f"rank {r} keys"
+            assert rv.tobytes() == np.concatenate([v[0] for _, v in pieces]).tobytes()
+            del rk, rv
+            # the rank's merge of the received buffers vs the same pieces staged apart
+            Dr = np.unique(np.concatenate([k for k, _ in pieces]))
+            dD = torch.from_numpy(Dr.view(np.int64)).to(dev)
+            pcs = x.pieces()
+            o_x = torch.empty(Dr.size, dtype=torch.float32, device=dev)
+            plan_x = MergePlan(0, PSG_F32, 1, [{
+                "keys": dD.data_ptr(), "nslots": int(Dr.size),
+                "push_keys": [x.recv_keys_ptr + 8 * a for a, _ in pcs],
+                "push_vals": [[x.recv_vals_ptr[0] + 4 * a] for a, _ in pcs],
+                "push_n": [c for _, c in pcs], "out": [o_x.data_ptr()]}])
+            sp = _dev_pushes(pieces, dev)
+            o_s = torch.empty(Dr.size, dtype=torch.float32, device=dev)
+            plan_s = MergePlan(0, PSG_F32, 1, [{
+                "keys": dD.data_ptr(), "nslots": int(Dr.size),
+                "push_keys": [k.data_ptr() for k, _ in sp],
+                "push_vals": [[v[0].data_ptr()] for _, v in sp],
+                "push_n": [int(k.size) for k, _ in pieces], "out": [o_s.data_ptr()]}])
+            plan_x.run()
+            plan_s.run()
+            torch.cuda.synchronize()
+            assert list(plan_x.matched()) == [c for _, c in pcs]
+            assert torch.equal(o_x.view(torch.int32), o_s.view(torch.int32)), f"rank {r} merge"
+            if r in (0, 5):  # the oracle on two ranks (one at each end of the key space)
+                rc, lo, hi, want, _ = O.aggregate_scatter(Dr, int(b[r]), int(b[r + 1]), pieces,
+                                                          parallel=False)
+                assert rc == 0 and (lo, hi) == (0, Dr.size)
+                assert o_x.cpu().numpy().tobytes() == np.asarray(want[0], np.float32).tobytes()
+            plan_x.close()
+            plan_s.close()
+            del sp, dD, o_x, o_s
+    finally:
+        for x in xs:
+            x.close()
+        for c in comms:
+            shard.destroy_comm(c)
