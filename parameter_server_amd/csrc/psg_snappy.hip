@@ -57,11 +57,18 @@ __device__ unsigned long long g_sprof[4096][8];
 #define SP_ADD(i) do { } while (0)
 #endif
 
-constexpr uint32_t kRing = 65536;
+#ifndef PSG_SNAPPY_RING
+#define PSG_SNAPPY_RING 65536  // A/B builds: a smaller ring, more waves per CU
+#endif
+#ifndef PSG_SNAPPY_MAXDEF
+#define PSG_SNAPPY_MAXDEF 768
+#endif
+constexpr uint32_t kRing = PSG_SNAPPY_RING;
+static_assert((kRing & (kRing - 1)) == 0 && kRing >= 4096, "ring: a power of two >= the window");
 constexpr uint32_t kWin = 4096;
 
 constexpr uint32_t kBigLit = 2048;   // literals deferred to the copy kernel
-constexpr uint32_t kMaxDef = 768;    // deferred pieces per part (LDS list)
+constexpr uint32_t kMaxDef = PSG_SNAPPY_MAXDEF;  // deferred pieces per part (LDS list)
 constexpr uint32_t kLitUnits = 256;  // 16-B units per copy-kernel chunk (4 KB)
 constexpr uint64_t kPrefetchParts = 64;         // parts per launch that are prefetched into L2
 constexpr uint64_t kPrefetchMax = 2ull << 20;   // largest part prefetched

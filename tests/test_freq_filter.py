@@ -231,3 +231,45 @@ def test_gpu_freq_filter_inserts_on_two_streams_in_call_order():
         O.cm_insert(t, nn, kk, keys, counts)
     assert np.array_equal(_table(v, 4, nn), t)
     v.close()
+
+
+@pytest.mark.gpu
+@pytest.mark.timeout(600)
+@pytest.mark.parametrize("k,nq", [(1, 400_000), (3, 1_000_003), (4, 2_000_000), (5, 700_001),
+                                  (8, 9_000_000)])
+def test_gpu_freq_query_binned_vs_oracle(k, nq):
+    """queryKeys (frequency_filter.h:27-34, countmin.h:42-51) through the
+    binned query (probes moved to 128 KB table regions, the region read once
+    into LDS, results binned back per key block): kept keys, in input order,
+    exact against the oracle for k = 1..8, table sizes with a partial last
+    region, thresholds around the table's counts, repeated and unsorted
+    query keys, and at k = 8 / 9 M keys two chunks of the key stream (the
+    scratch holds 8 M keys' records at k = 8).  The device entry point runs
+    the same form with caller scratch."""
+    import torch
+    assert torch.cuda.is_available()
+    from parameter_server_amd import _lib
+    rng = np.random.default_rng(100 + k)
+    v = _ctx()
+    n = 3_000_017 if k != 8 else (1 << 24) + 12
+    _lib.check(v._L.psg_freq_resize(v._h, 5, n, k))
+    t, nn, kk = O.cm_resize(n, k)
+    keys = np.unique(zipf_keys(rng, 600_000))
+    counts = rng.integers(1, 40, keys.size).astype(np.uint32)
+    _lib.check(v._L.psg_freq_insert(v._h, 5, keys.ctypes.data, counts.ctypes.data, keys.size))
+    O.cm_insert(t, nn, kk, keys, counts)
+    q = np.concatenate([zipf_keys(rng, nq - 1000), keys[:1000]])
+    for freq in (0, 3, 20):
+        assert np.array_equal(_query(v, 5, q, freq), O.ff_query(t, nn, kk, q, freq)), freq
+    if k == 4:
+        m = 500_000
+        dq = torch.from_numpy(q[:m].view(np.int64)).cuda()
+        sb = v._L.psg_freq_query_scratch_bytes(m)
+        scratch = torch.empty(sb, dtype=torch.uint8, device="cuda")
+        dout = torch.empty(m, dtype=torch.int64, device="cuda")
+        dn = torch.zeros(1, dtype=torch.int64, device="cuda")
+        _lib.check(v._L.psg_freq_query_dev(v._h, 5, dq.data_ptr(), m, 3, dout.data_ptr(),
+                                           dn.data_ptr(), scratch.data_ptr(), None))
+        got = dout[:int(dn.item())].cpu().numpy().view(np.uint64)
+        assert np.array_equal(got, O.ff_query(t, nn, kk, q[:m], 3))
+    v.close()
