@@ -970,7 +970,7 @@ def load_traffic(bytes_per_launch, workload):
             "source": d.get("source")}
 
 
-def bench_rows(device, reps=5, insts=None):
+def bench_rows(device, reps=5, insts=None, only=None):
     """The SURVEY 8(f) rows beside the merge, each on device-resident input
     with its own HBM roofline: algorithmic bytes / mean kernel time (HIP
     events on the stream the kernel runs on).  Shapes: the N-way merge of
@@ -1006,191 +1006,199 @@ def bench_rows(device, reps=5, insts=None):
 
     rng = np.random.default_rng(3)
     D, pushes = synth.overlap_pushes(1)
-    # N-way merge (psg_nway): cfg2's 8 key-only pushes ->
-    # the merged key set (BatchSolver's key pushes, setUnion push after
-    # push), and the same pushes with their f32 values -> union + sums
-    from parameter_server_amd.kv_vector import NWayMerge
-    dk = [torch.from_numpy(k.view(np.int64)).to(dev) for k, _ in pushes]
-    dv = [torch.from_numpy(vs[0]).to(dev) for _, vs in pushes]
-    tot = sum(k.size for k, _ in pushes)
-    ok = torch.empty(tot, dtype=torch.int64, device=dev)
-    ov = torch.empty(tot, dtype=torch.float32, device=dev)
-    for name, m in (("key_union", 0), ("nway_merge_1agg", 1)):
-        u = NWayMerge(device, _lib.PSG_F32, [t.data_ptr() for t in dk], [k.size for k, _ in pushes],
-                      [[t.data_ptr()] for t in dv] if m else [[] for _ in dk], ok.data_ptr(),
-                      [ov.data_ptr()] if m else [])
-        u.run()
-        nu = u.result()
-        assert nu == D.size, "N-way union size"
-        ms = timed(lambda: u.run(st.cuda_stream))
-        assert u.result() == D.size
-        u.close()
-        row(name, ms, tot * (8 + 4 * m) + D.size * (8 + 4 * m), tot, "keys/s")
-        out[name]["shape"] = ("8 pushes x 131,072 sorted keys (cfg2) -> U = 956,827 merged keys" +
-                              (" + f32 sums" if m else ""))
-    assert np.array_equal(ok[:D.size].cpu().numpy().view(np.uint64), D)
-    del dk, dv, ok, ov
-    if insts:
-        # the N-way merge at the headline's scale: its --batch cfg2
-        # aggregates (keys + f32 values) as one pipeline (psg_nway_create_batch:
-        # one launch per stage over every aggregate)
-        from parameter_server_amd.kv_vector import NWayMergeBatch
-        keepb, merges, nb, kvb = [], [], 0, 0
-        for Dj, ps in insts:
-            dkb = [torch.from_numpy(k.view(np.int64)).to(dev) for k, _ in ps]
-            dvb = [torch.from_numpy(vs[0]).to(dev) for _, vs in ps]
-            totb = sum(k.size for k, _ in ps)
-            okb = torch.empty(totb, dtype=torch.int64, device=dev)
-            ovb = torch.empty(totb, dtype=torch.float32, device=dev)
-            keepb.append((dkb, dvb, okb, ovb))
-            merges.append(dict(push_keys=[t.data_ptr() for t in dkb],
-                               push_n=[k.size for k, _ in ps],
-                               push_vals=[[t.data_ptr()] for t in dvb],
-                               out_keys=okb.data_ptr(), out_vals=[ovb.data_ptr()]))
-            nb += totb * 12 + Dj.size * 12
-            kvb += totb
-        u = NWayMergeBatch(device, _lib.PSG_F32, merges)
-        u.run()
-        assert u.result() == [Dj.size for Dj, _ in insts], "batched N-way union sizes"
-        ms = timed(lambda: u.run(st.cuda_stream))
-        u.result()
-        u.close()
-        row("nway_merge", ms, nb, kvb, "keys/s")
-        out["nway_merge"]["shape"] = (f"{len(insts)} cfg2 aggregates (8 pushes x 131,072 keys + "
-                                      "f32 values each -> U = 956,827 keys + sums), one pipeline")
-        del keepb, merges
-    # pull gather (getValue) of 1 M sorted request keys from a cfg2 shard
-    req = np.sort(np.concatenate([k for k, _ in pushes[:8]]))[::1]
-    dD = torch.from_numpy(D.view(np.int64)).to(dev)
-    dW = torch.from_numpy(rng.standard_normal(D.size).astype(np.float32)).to(dev)
-    dR = torch.from_numpy(req.view(np.int64)).to(dev)
-    dO = torch.empty(req.size, dtype=torch.float32, device=dev)
-    dM = torch.zeros(1, dtype=torch.int64, device=dev)
-    ms = timed(lambda: _lib.check(L.psg_gather_dev(_lib.PSG_F32, dD.data_ptr(), D.size,
-                                                   dW.data_ptr(), dR.data_ptr(), req.size,
-                                                   dO.data_ptr(), dM.data_ptr(), None)))
-    row("gather", ms, req.size * (8 + 4 + 4), req.size, "keys/s")
-    del dD, dW, dR, dO
-    # crc32c: key signatures (2048 B of each of 65,536 pushes) and one 1 GiB stream
-    nsig = 65536
-    blob = torch.randint(0, 255, (nsig * 4096,), dtype=torch.uint8, device=dev)
-    off = torch.arange(0, nsig + 1, dtype=torch.int64, device=dev) * 4096
-    sig = torch.empty(nsig, dtype=torch.int32, device=dev)
-    ms = timed(lambda: _lib.check(L.psg_crc32c_dev(blob.data_ptr(), off.data_ptr(), nsig,
-                                                   _lib.PSG_MAX_SIG_LEN, None, sig.data_ptr(),
-                                                   None)))
-    row("crc32c_signatures", ms, nsig * 2048, nsig, "signatures/s")
-    big = torch.randint(0, 255, (1 << 30,), dtype=torch.uint8, device=dev)
-    off1 = torch.tensor([0, 1 << 30], dtype=torch.int64, device=dev)
-    ms = timed(lambda: _lib.check(L.psg_crc32c_dev(big.data_ptr(), off1.data_ptr(), 1, 1 << 30,
-                                                   None, sig.data_ptr(), None)))
-    row("crc32c_stream", ms, 1 << 30, 1 << 30, "bytes/s")
-    del blob, big
-    # snappy: 2048 parts of 64 KB, each a synthetic raw stream of alternating
-    # 16-byte literals and 16-byte copies (2-byte offsets): 4096 elements per
-    # part, the element density of typical snappy output
-    nparts, plen = 2048, 65536
+    if only is None or 'nway' in only:
+        # N-way merge (psg_nway): cfg2's 8 key-only pushes ->
+        # the merged key set (BatchSolver's key pushes, setUnion push after
+        # push), and the same pushes with their f32 values -> union + sums
+        from parameter_server_amd.kv_vector import NWayMerge
+        dk = [torch.from_numpy(k.view(np.int64)).to(dev) for k, _ in pushes]
+        dv = [torch.from_numpy(vs[0]).to(dev) for _, vs in pushes]
+        tot = sum(k.size for k, _ in pushes)
+        ok = torch.empty(tot, dtype=torch.int64, device=dev)
+        ov = torch.empty(tot, dtype=torch.float32, device=dev)
+        for name, m in (("key_union", 0), ("nway_merge_1agg", 1)):
+            u = NWayMerge(device, _lib.PSG_F32, [t.data_ptr() for t in dk], [k.size for k, _ in pushes],
+                          [[t.data_ptr()] for t in dv] if m else [[] for _ in dk], ok.data_ptr(),
+                          [ov.data_ptr()] if m else [])
+            u.run()
+            nu = u.result()
+            assert nu == D.size, "N-way union size"
+            ms = timed(lambda: u.run(st.cuda_stream))
+            assert u.result() == D.size
+            u.close()
+            row(name, ms, tot * (8 + 4 * m) + D.size * (8 + 4 * m), tot, "keys/s")
+            out[name]["shape"] = ("8 pushes x 131,072 sorted keys (cfg2) -> U = 956,827 merged keys" +
+                                  (" + f32 sums" if m else ""))
+        assert np.array_equal(ok[:D.size].cpu().numpy().view(np.uint64), D)
+        del dk, dv, ok, ov
+        if insts:
+            # the N-way merge at the headline's scale: its --batch cfg2
+            # aggregates (keys + f32 values) as one pipeline (psg_nway_create_batch:
+            # one launch per stage over every aggregate)
+            from parameter_server_amd.kv_vector import NWayMergeBatch
+            keepb, merges, nb, kvb = [], [], 0, 0
+            for Dj, ps in insts:
+                dkb = [torch.from_numpy(k.view(np.int64)).to(dev) for k, _ in ps]
+                dvb = [torch.from_numpy(vs[0]).to(dev) for _, vs in ps]
+                totb = sum(k.size for k, _ in ps)
+                okb = torch.empty(totb, dtype=torch.int64, device=dev)
+                ovb = torch.empty(totb, dtype=torch.float32, device=dev)
+                keepb.append((dkb, dvb, okb, ovb))
+                merges.append(dict(push_keys=[t.data_ptr() for t in dkb],
+                                   push_n=[k.size for k, _ in ps],
+                                   push_vals=[[t.data_ptr()] for t in dvb],
+                                   out_keys=okb.data_ptr(), out_vals=[ovb.data_ptr()]))
+                nb += totb * 12 + Dj.size * 12
+                kvb += totb
+            u = NWayMergeBatch(device, _lib.PSG_F32, merges)
+            u.run()
+            assert u.result() == [Dj.size for Dj, _ in insts], "batched N-way union sizes"
+            ms = timed(lambda: u.run(st.cuda_stream))
+            u.result()
+            u.close()
+            row("nway_merge", ms, nb, kvb, "keys/s")
+            out["nway_merge"]["shape"] = (f"{len(insts)} cfg2 aggregates (8 pushes x 131,072 keys + "
+                                          "f32 values each -> U = 956,827 keys + sums), one pipeline")
+            del keepb, merges
+    if only is None or 'gather' in only:
+        # pull gather (getValue) of 1 M sorted request keys from a cfg2 shard
+        req = np.sort(np.concatenate([k for k, _ in pushes[:8]]))[::1]
+        dD = torch.from_numpy(D.view(np.int64)).to(dev)
+        dW = torch.from_numpy(rng.standard_normal(D.size).astype(np.float32)).to(dev)
+        dR = torch.from_numpy(req.view(np.int64)).to(dev)
+        dO = torch.empty(req.size, dtype=torch.float32, device=dev)
+        dM = torch.zeros(1, dtype=torch.int64, device=dev)
+        ms = timed(lambda: _lib.check(L.psg_gather_dev(_lib.PSG_F32, dD.data_ptr(), D.size,
+                                                       dW.data_ptr(), dR.data_ptr(), req.size,
+                                                       dO.data_ptr(), dM.data_ptr(), None)))
+        row("gather", ms, req.size * (8 + 4 + 4), req.size, "keys/s")
+        del dD, dW, dR, dO
+    if only is None or 'crc' in only:
+        # crc32c: key signatures (2048 B of each of 65,536 pushes) and one 1 GiB stream
+        nsig = 65536
+        blob = torch.randint(0, 255, (nsig * 4096,), dtype=torch.uint8, device=dev)
+        off = torch.arange(0, nsig + 1, dtype=torch.int64, device=dev) * 4096
+        sig = torch.empty(nsig, dtype=torch.int32, device=dev)
+        ms = timed(lambda: _lib.check(L.psg_crc32c_dev(blob.data_ptr(), off.data_ptr(), nsig,
+                                                       _lib.PSG_MAX_SIG_LEN, None, sig.data_ptr(),
+                                                       None)))
+        row("crc32c_signatures", ms, nsig * 2048, nsig, "signatures/s")
+        big = torch.randint(0, 255, (1 << 30,), dtype=torch.uint8, device=dev)
+        off1 = torch.tensor([0, 1 << 30], dtype=torch.int64, device=dev)
+        ms = timed(lambda: _lib.check(L.psg_crc32c_dev(big.data_ptr(), off1.data_ptr(), 1, 1 << 30,
+                                                       None, sig.data_ptr(), None)))
+        row("crc32c_stream", ms, 1 << 30, 1 << 30, "bytes/s")
+        del blob, big
+    if only is None or 'snappy' in only:
+        # snappy: 2048 parts of 64 KB, each a synthetic raw stream of alternating
+        # 16-byte literals and 16-byte copies (2-byte offsets): 4096 elements per
+        # part, the element density of typical snappy output
+        nparts, plen = 2048, 65536
 
-    def part(seed):
-        r = np.random.default_rng(seed)
-        b = bytearray([0x80, 0x80, 0x04])  # varint 65536
-        o = 0
-        while o < plen:
-            b.append(15 << 2)  # literal of 16
-            b += r.integers(0, 256, 16, dtype=np.uint8).tobytes()
-            o += 16
-            off = int(r.integers(1, min(o, 4096) + 1))
-            b += bytes([2 | (15 << 2), off & 0xff, off >> 8])  # copy of 16
-            o += 16
-        return bytes(b)
+        def part(seed):
+            # per 32 output bytes: a literal of 16 (tag 15 << 2, 16 bytes),
+            # then a copy of 16 (tag 2 | 15 << 2, 2-byte offset in [1, min(o, 4096)])
+            r = np.random.default_rng(seed)
+            npair = plen // 32
+            o = 32 * np.arange(npair, dtype=np.int64) + 16
+            off = r.integers(1, np.minimum(o, 4096) + 1)
+            rec = np.empty((npair, 20), np.uint8)
+            rec[:, 0] = 15 << 2
+            rec[:, 1:17] = r.integers(0, 256, (npair, 16), dtype=np.uint8)
+            rec[:, 17] = 2 | (15 << 2)
+            rec[:, 18] = off & 0xff
+            rec[:, 19] = off >> 8
+            return bytes([0x80, 0x80, 0x04]) + rec.tobytes()  # varint 65536
 
-    parts = [part(i % 16) for i in range(nparts)]
-    soff = np.concatenate([[0], np.cumsum([len(x) for x in parts])]).astype(np.uint64)
-    dsrc = torch.from_numpy(np.frombuffer(b"".join(parts), np.uint8).copy()).to(dev)
-    dso = torch.from_numpy(soff.view(np.int64)).to(dev)
-    ddo = torch.arange(0, nparts + 1, dtype=torch.int64, device=dev) * plen
-    ddst = torch.empty(nparts * plen, dtype=torch.uint8, device=dev)
-    dst_ = torch.empty(nparts, dtype=torch.int32, device=dev)
-    ms = timed(lambda: _lib.check(L.psg_snappy_uncompress_dev(
-        dsrc.data_ptr(), dso.data_ptr(), nparts, ddst.data_ptr(), ddo.data_ptr(),
-        dst_.data_ptr(), None)))
-    assert int(dst_.abs().sum().item()) == 0, "snappy row: a part failed to decode"
-    row("snappy_uncompress", ms, int(soff[-1]) + nparts * plen, nparts * plen,
-        "uncompressed bytes/s")
-    del dsrc, ddst
-    # snappy, incompressible 1 MB parts (a cfg2 push's key part: what snappy
-    # emits for random data is one 65,536-byte literal per block), 16 parts:
-    # the parse defers the literals, the copy kernel moves them chip-wide
-    nbig, blen = 16, 1 << 20
+        parts = [part(i % 16) for i in range(nparts)]
+        soff = np.concatenate([[0], np.cumsum([len(x) for x in parts])]).astype(np.uint64)
+        dsrc = torch.from_numpy(np.frombuffer(b"".join(parts), np.uint8).copy()).to(dev)
+        dso = torch.from_numpy(soff.view(np.int64)).to(dev)
+        ddo = torch.arange(0, nparts + 1, dtype=torch.int64, device=dev) * plen
+        ddst = torch.empty(nparts * plen, dtype=torch.uint8, device=dev)
+        dst_ = torch.empty(nparts, dtype=torch.int32, device=dev)
+        ms = timed(lambda: _lib.check(L.psg_snappy_uncompress_dev(
+            dsrc.data_ptr(), dso.data_ptr(), nparts, ddst.data_ptr(), ddo.data_ptr(),
+            dst_.data_ptr(), None)))
+        assert int(dst_.abs().sum().item()) == 0, "snappy row: a part failed to decode"
+        row("snappy_uncompress", ms, int(soff[-1]) + nparts * plen, nparts * plen,
+            "uncompressed bytes/s")
+        del dsrc, ddst
+        # snappy, incompressible 1 MB parts (a cfg2 push's key part: what snappy
+        # emits for random data is one 65,536-byte literal per block), 16 parts:
+        # the parse defers the literals, the copy kernel moves them chip-wide
+        nbig, blen = 16, 1 << 20
 
-    def lit_part(seed):
-        r = np.random.default_rng(seed)
-        b = bytearray([0x80, 0x80, 0x40])  # varint 1 MiB
-        for _ in range(blen // 65536):
-            b += bytes([61 << 2, 0xff, 0xff]) + r.integers(0, 256, 65536, dtype=np.uint8).tobytes()
-        return bytes(b)
+        def lit_part(seed):
+            r = np.random.default_rng(seed)
+            b = bytearray([0x80, 0x80, 0x40])  # varint 1 MiB
+            for _ in range(blen // 65536):
+                b += bytes([61 << 2, 0xff, 0xff]) + r.integers(0, 256, 65536, dtype=np.uint8).tobytes()
+            return bytes(b)
 
-    parts = [lit_part(i) for i in range(nbig)]
-    soff = np.concatenate([[0], np.cumsum([len(x) for x in parts])]).astype(np.uint64)
-    dsrc = torch.from_numpy(np.frombuffer(b"".join(parts), np.uint8).copy()).to(dev)
-    dso = torch.from_numpy(soff.view(np.int64)).to(dev)
-    ddo = torch.arange(0, nbig + 1, dtype=torch.int64, device=dev) * blen
-    ddst = torch.empty(nbig * blen, dtype=torch.uint8, device=dev)
-    dst_ = torch.empty(nbig, dtype=torch.int32, device=dev)
-    ms = timed(lambda: _lib.check(L.psg_snappy_uncompress_dev(
-        dsrc.data_ptr(), dso.data_ptr(), nbig, ddst.data_ptr(), ddo.data_ptr(),
-        dst_.data_ptr(), None)))
-    assert int(dst_.abs().sum().item()) == 0, "snappy row: a large part failed to decode"
-    row("snappy_uncompress_1MB_parts", ms, int(soff[-1]) + nbig * blen, nbig * blen,
-        "uncompressed bytes/s")
-    del dsrc, ddst
-    # CountMin: insertKeys / queryKeys of 16.8 M keys, 2^26 counters, k = 4
-    from parameter_server_amd.kv_vector import KVVector, Message
-    v = KVVector(device)
-    nk = 1 << 24
-    keys = torch.randint(0, 1 << 62, (nk,), dtype=torch.int64, device=dev)
-    cnt = torch.randint(1, 100, (nk,), dtype=torch.int32, device=dev)
-    _lib.check(L.psg_freq_resize(v._h, 0, 1 << 26, 4))
-    ms = timed(lambda: _lib.check(L.psg_freq_insert_dev(v._h, 0, keys.data_ptr(),
-                                                        cnt.data_ptr(), nk, None)))
-    # keys + counts read; per probe one counter byte read and written
-    # (countmin.h:69: uint8 counters, the table 64 MB)
-    row("countmin_insert", ms, nk * (8 + 4) + nk * 4 * 2, nk, "keys/s")
-    scratch = torch.empty(L.psg_freq_query_scratch_bytes(nk), dtype=torch.uint8, device=dev)
-    qo = torch.empty(nk, dtype=torch.int64, device=dev)
-    qn = torch.zeros(1, dtype=torch.int64, device=dev)
-    ms = timed(lambda: _lib.check(L.psg_freq_query_dev(v._h, 0, keys.data_ptr(), nk, 200,
-                                                       qo.data_ptr(), qn.data_ptr(),
-                                                       scratch.data_ptr(), None)))
-    kept = int(qn.item())
-    # keys read by the count and the scatter pass, one byte per probe, kept keys written
-    row("countmin_query", ms, nk * 8 * 2 + nk * 4 + kept * 8, nk, "keys/s")
-    v.close()
-    del keys, cnt, qo, scratch
-    # Darling's server step over 16.8 M f64 positions: the (G, U) aggregate of
-    # one resident push plus the fused updateWeight (nothing crosses PCIe)
-    n = 1 << 24
-    Dk = np.arange(n, dtype=np.uint64) * np.uint64(3)
-    v = KVVector(device, _lib.PSG_F64)
-    v.setValue(Message(key=Dk))
-    v.set_value_array(0, np.zeros(n))
-    _lib.check(L.psg_darling_init(v._h, 0, 1.0))
-    G = rng.standard_normal(n)
-    U = rng.random(n)
-    P = (C.c_double * 4)(1.0, 0.1, 1e20, 5.0)
-    vio = C.c_double()
-    times = []
-    for r in range(reps + 1):
-        v.setValue(Message(time=r, key=Dk, value=[G, U]))  # H2D here, untimed
-        torch.cuda.synchronize()
-        t0 = time.perf_counter()
-        _lib.check(L.psg_darling_update(v._h, 0, r, C.cast(P, C.c_void_p), C.byref(vio)))
-        if r:
-            times.append(time.perf_counter() - t0)
-    v.close()
-    ms = float(np.median(times)) * 1e3
-    # aggregate (dense: values in, sums out) + update (G, U, w, delta r/w)
-    row("darling_server_step", ms, n * 16 + n * 16 + n * (16 + 16 + 16), n, "positions/s")
+        parts = [lit_part(i) for i in range(nbig)]
+        soff = np.concatenate([[0], np.cumsum([len(x) for x in parts])]).astype(np.uint64)
+        dsrc = torch.from_numpy(np.frombuffer(b"".join(parts), np.uint8).copy()).to(dev)
+        dso = torch.from_numpy(soff.view(np.int64)).to(dev)
+        ddo = torch.arange(0, nbig + 1, dtype=torch.int64, device=dev) * blen
+        ddst = torch.empty(nbig * blen, dtype=torch.uint8, device=dev)
+        dst_ = torch.empty(nbig, dtype=torch.int32, device=dev)
+        ms = timed(lambda: _lib.check(L.psg_snappy_uncompress_dev(
+            dsrc.data_ptr(), dso.data_ptr(), nbig, ddst.data_ptr(), ddo.data_ptr(),
+            dst_.data_ptr(), None)))
+        assert int(dst_.abs().sum().item()) == 0, "snappy row: a large part failed to decode"
+        row("snappy_uncompress_1MB_parts", ms, int(soff[-1]) + nbig * blen, nbig * blen,
+            "uncompressed bytes/s")
+        del dsrc, ddst
+    if only is None or 'countmin' in only:
+        # CountMin: insertKeys / queryKeys of 16.8 M keys, 2^26 counters, k = 4
+        from parameter_server_amd.kv_vector import KVVector, Message
+        v = KVVector(device)
+        nk = 1 << 24
+        keys = torch.randint(0, 1 << 62, (nk,), dtype=torch.int64, device=dev)
+        cnt = torch.randint(1, 100, (nk,), dtype=torch.int32, device=dev)
+        _lib.check(L.psg_freq_resize(v._h, 0, 1 << 26, 4))
+        ms = timed(lambda: _lib.check(L.psg_freq_insert_dev(v._h, 0, keys.data_ptr(),
+                                                            cnt.data_ptr(), nk, None)))
+        # keys + counts read; per probe one counter byte read and written
+        # (countmin.h:69: uint8 counters, the table 64 MB)
+        row("countmin_insert", ms, nk * (8 + 4) + nk * 4 * 2, nk, "keys/s")
+        scratch = torch.empty(L.psg_freq_query_scratch_bytes(nk), dtype=torch.uint8, device=dev)
+        qo = torch.empty(nk, dtype=torch.int64, device=dev)
+        qn = torch.zeros(1, dtype=torch.int64, device=dev)
+        ms = timed(lambda: _lib.check(L.psg_freq_query_dev(v._h, 0, keys.data_ptr(), nk, 200,
+                                                           qo.data_ptr(), qn.data_ptr(),
+                                                           scratch.data_ptr(), None)))
+        kept = int(qn.item())
+        # keys read by the count and the scatter pass, one byte per probe, kept keys written
+        row("countmin_query", ms, nk * 8 * 2 + nk * 4 + kept * 8, nk, "keys/s")
+        v.close()
+        del keys, cnt, qo, scratch
+    if only is None or 'darling' in only:
+        # Darling's server step over 16.8 M f64 positions: the (G, U) aggregate of
+        # one resident push plus the fused updateWeight (nothing crosses PCIe)
+        n = 1 << 24
+        Dk = np.arange(n, dtype=np.uint64) * np.uint64(3)
+        v = KVVector(device, _lib.PSG_F64)
+        v.setValue(Message(key=Dk))
+        v.set_value_array(0, np.zeros(n))
+        _lib.check(L.psg_darling_init(v._h, 0, 1.0))
+        G = rng.standard_normal(n)
+        U = rng.random(n)
+        P = (C.c_double * 4)(1.0, 0.1, 1e20, 5.0)
+        vio = C.c_double()
+        times = []
+        for r in range(reps + 1):
+            v.setValue(Message(time=r, key=Dk, value=[G, U]))  # H2D here, untimed
+            torch.cuda.synchronize()
+            t0 = time.perf_counter()
+            _lib.check(L.psg_darling_update(v._h, 0, r, C.cast(P, C.c_void_p), C.byref(vio)))
+            if r:
+                times.append(time.perf_counter() - t0)
+        v.close()
+        ms = float(np.median(times)) * 1e3
+        # aggregate (dense: values in, sums out) + update (G, U, w, delta r/w)
+        row("darling_server_step", ms, n * 16 + n * 16 + n * (16 + 16 + 16), n, "positions/s")
     return out
 
 

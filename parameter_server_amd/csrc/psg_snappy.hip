@@ -13,13 +13,19 @@
 // compressed stream, itself refilled with coalesced loads) and takes tag and
 // offset bytes from it with readlane; the bytes of an element are moved by
 // all 64 lanes.  The
-// last 64 KB of output live in an LDS ring: a copy reads its source bytes
+// last 8 KB of output live in an LDS ring: a copy reads its source bytes
 // there.  A copy's source is output[o - off + (l mod off)] for byte l, which
 // lies before o for every l, so even overlapping (run-length) copies move in
 // one step; copies are <= 64 bytes, so the step's reads precede its writes.
-// Offsets beyond the ring (possible only for 4-byte-offset copies, which
-// snappy's own compressor never emits across its 64 KB blocks) read the
-// output in global memory after a fence.
+// Offsets beyond the ring read the output in global memory after a flush
+// and a fence (slower per element, rare in the payloads here: sorted keys
+// and float values match their recent neighbours).
+//
+// The parse is latency-bound per element, so the throughput is the number
+// of parts in flight: the ring is 8 KB (r04: 64 KB, two parts per CU) and a
+// part keeps up to 256 deferred pieces, ~15 KB of LDS per wave, ten parts
+// per CU -- 2048 element-dense 64 KB parts decode 3.3x faster (28.5 ->
+// 93 GB/s, profiles/r05_ab_snappy_ring.txt).
 //
 // Long literals (>= kBigLit bytes: what incompressible data becomes -- the
 // cfg2 key and value parts are one 64 KB literal per snappy block) are not
@@ -58,10 +64,10 @@ __device__ unsigned long long g_sprof[4096][8];
 #endif
 
 #ifndef PSG_SNAPPY_RING
-#define PSG_SNAPPY_RING 65536  // A/B builds: a smaller ring, more waves per CU
+#define PSG_SNAPPY_RING 8192  // A/B builds: 16384, 65536 (r04's)
 #endif
 #ifndef PSG_SNAPPY_MAXDEF
-#define PSG_SNAPPY_MAXDEF 768
+#define PSG_SNAPPY_MAXDEF 256  // r04: 768
 #endif
 constexpr uint32_t kRing = PSG_SNAPPY_RING;
 static_assert((kRing & (kRing - 1)) == 0 && kRing >= 4096, "ring: a power of two >= the window");
@@ -530,8 +536,13 @@ hipError_t launch_snappy(const uint8_t* src, const uint64_t* soff, uint64_t nmsg
     const hipError_t e = hipMemsetAsync(nlits, 0, 4, stream);
     if (e != hipSuccess) return e;
   }
-  // 64 KB of LDS per workgroup: two resident per CU
-  const uint64_t blocks = nmsg < 512 ? nmsg : 512;
+  // one wave per part, as many resident per CU as the LDS allows (the ring,
+  // the window and the piece list): the parse is latency-bound per part, so
+  // resident parts are the throughput
+  constexpr uint64_t kLdsPerPart = kRing + kWin + 12ull * kMaxDef + 64;
+  constexpr uint64_t kPerCU = 163840ull / kLdsPerPart > 0 ? 163840ull / kLdsPerPart : 1;
+  const uint64_t grid_cap = 256ull * kPerCU;
+  const uint64_t blocks = nmsg < grid_cap ? nmsg : grid_cap;
   hipLaunchKernelGGL(snappy_kernel, dim3((uint32_t)blocks), dim3(64), 0, stream, src, soff, dst,
                      doff, dcap, nmsg, status, nlits ? lits : nullptr, nlits, cap, nbad,
                      pairs ? 1 : 0, nmsg <= kPrefetchParts ? PSG_SNAPPY_PREFETCH : 0);

@@ -94,6 +94,44 @@ typedef unsigned long long u64x2 __attribute__((ext_vector_type(2)));
 typedef uint32_t u32x2 __attribute__((ext_vector_type(2)));
 
 __device__ __forceinline__ uint32_t uni(uint32_t v) { return __builtin_amdgcn_readfirstlane(v); }
+__device__ __forceinline__ uint64_t uni64(uint64_t v) {
+  return ((uint64_t)uni((uint32_t)(v >> 32)) << 32) | uni((uint32_t)v);
+}
+
+#ifndef PSG_DDMA
+#define PSG_DDMA 1  // A/B builds: 0 = D and the resident bucket table through registers
+#endif
+// 16 B per lane from global memory straight into LDS (gfx950 LDS-DMA): lane l
+// writes lds + 16 l; nontemporal (D and the bucket table are read by one tile)
+// Issued by inline asm (M0 saved and restored, as the compiler reserves it):
+// the builtin form made the compiler's wait-count pass wait for the DMA at
+// the next reuse of its address registers, i.e. right after issuing it.  The
+// compiler does not see these loads, so readers of the LDS they fill wait
+// for them explicitly (dma_wait); its own vmcnt waits stay correct, only
+// more conservative (the DMAs are older than its loads).
+typedef __attribute__((address_space(3))) void* LdsPtr;
+__device__ __forceinline__ void dma16(const void* g, void* lds) {
+  const uint32_t la = (uint32_t)(uintptr_t)(LdsPtr)lds;
+  uint32_t keep;
+  asm volatile(
+      "s_mov_b32 %0, m0\n\ts_mov_b32 m0, %2\n\ts_nop 0\n\t"
+      "global_load_lds_dwordx4 %1, off nt\n\ts_mov_b32 m0, %0"
+      : "=&s"(keep)
+      : "v"(g), "s"(la)
+      : "memory");
+}
+__device__ __forceinline__ void dma_wait() {
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+}
+// a workgroup barrier that makes LDS writes visible but leaves vector-memory
+// operations (LDS-DMA, loads) in flight: __syncthreads() would wait for them
+// (its release fence waits vmcnt(0) while an LDS-DMA is pending)
+__device__ __forceinline__ void lds_barrier() {
+  asm volatile("" ::: "memory");
+  __builtin_amdgcn_s_waitcnt(0xc07f);  // lgkmcnt(0); vmcnt and expcnt not waited for
+  __builtin_amdgcn_s_barrier();
+  asm volatile("" ::: "memory");
+}
 
 // blocks b and b+8 share an XCD (observed dispatch, speed only): give each
 // XCD a contiguous run of tiles
@@ -222,58 +260,78 @@ __global__ __launch_bounds__(nt_of(kGroup), (occupancy<V, M, kGroup>())) void ti
       if (lane == 0) rpre[0] = 0;
     }
   };
-  if (np) load_tables(0);
-
   // ---- D keys, continued sums: thread t owns slots 4t..4t+3
   const uint32_t s0 = 4u * (uint32_t)tid;
-  uint64_t d[4];
-  if (s0 + 3u < nt && ((uintptr_t)Dg & 15u) == 0u) {
-    // D is read by this tile only: nontemporal (same-box A/B: ~1-3 % faster
-    // on cfg2/cfg3 with the nontemporal sum stores; not the element loads,
-    // whose lines neighbouring tiles share)
-    const u64x2 x0 = __builtin_nontemporal_load((const AS1 u64x2*)(Dg + s0));
-    const u64x2 x1 = __builtin_nontemporal_load((const AS1 u64x2*)(Dg + s0 + 2));
-    d[0] = x0.x; d[1] = x0.y; d[2] = x1.x; d[3] = x1.y;
+  const uint32_t* Bg = T.bt;
+  // full tiles: D (and a plan's resident bucket table) by LDS-DMA, issued
+  // before the push tables are waited for and left in flight across barrier
+  // (1) and the element loads, so D's HBM trip overlaps theirs (through
+  // registers, D had to land before barrier (1), and the element loads went
+  // out only after it: r05 phase clocks, profiles/r05_phases_cfg2.txt)
+  const bool dma = PSG_DDMA && nt == (uint32_t)kTS && ((uintptr_t)Dg & 15u) == 0u &&
+                   ((uintptr_t)Bg & 15u) == 0u;
+  auto issue_dma = [&]() {
+#pragma unroll
+    for (int j = 0; j < 2; ++j) {  // kTS / 2 16-B units: 2 wave instructions per wave
+      const uint32_t c = 2u * w + (uint32_t)j;
+      dma16(Dg + 128u * c + 2u * (uint32_t)lane, (char*)dk + 1024u * c);
+    }
+    static_assert(kNB / 512 <= kNW, "one 1-KB unit of the bucket table per wave at most");
+    if (Bg && w < (uint32_t)kNB / 512u)
+      dma16((const char*)Bg + 1024u * w + 16u * (uint32_t)lane, (char*)bt32 + 1024u * w);
+  };
+  if (dma && w != 0) issue_dma();
+  if (np) load_tables(0);
+  if (dma && w == 0) issue_dma();  // after wave 0's table loads: its wait for them does not wait for D
+  // through registers (partial or unaligned tiles): loaded and installed
+  // on this branch only, so no load of it is pending where the LDS-DMA
+  // path rejoins (a pending one would make the compiler wait for all, D's
+  // LDS-DMA included, at the next reuse of its registers)
+  if (!dma) {
+    uint64_t d[4];
+    if (s0 + 3u < nt && ((uintptr_t)Dg & 15u) == 0u) {
+      // D is read by this tile only: nontemporal (same-box A/B: ~1-3 % faster
+      // on cfg2/cfg3 with the nontemporal sum stores; not the element loads,
+      // whose lines neighbouring tiles share)
+      const u64x2 x0 = __builtin_nontemporal_load((const AS1 u64x2*)(Dg + s0));
+      const u64x2 x1 = __builtin_nontemporal_load((const AS1 u64x2*)(Dg + s0 + 2));
+      d[0] = x0.x; d[1] = x0.y; d[2] = x1.x; d[3] = x1.y;
+    } else {
+#pragma unroll
+      for (int j = 0; j < 4; ++j) d[j] = s0 + j < nt ? G(Dg)[s0 + j] : ~0ull;
+    }
+    // the resident bucket table (plans): kBPT u16 entries per thread
+    u32x2 btw = {0u, 0u};
+    if (Bg) btw = __builtin_nontemporal_load((const AS1 u32x2*)Bg + tid);
+#pragma unroll
+    for (int j = 0; j < 4; ++j) dk[s0 + j] = d[j];
+    if (Bg) {
+      bt32[tid * (kBPT / 2)] = btw.x;
+      bt32[tid * (kBPT / 2) + 1] = btw.y;
+    }
+    // drained here, explicitly: the compiler's merge of this branch's wait
+    // state into the LDS-DMA path otherwise left a vmcnt(0) on that path
+    __builtin_amdgcn_s_waitcnt(0x0f70);  // vmcnt(0)
+  }
+  // ---- sums, counts; clear the histogram.  The continued sums only on
+  // their own (uniform) branch, for the same reason
+  if (cont) {
+    V a0[M][4];
+#pragma unroll
+    for (int mi = 0; mi < M; ++mi)
+#pragma unroll
+      for (int j = 0; j < 4; ++j)
+        a0[mi][j] = s0 + j < nt ? G((const V*)T.out[mi] + T.slot0)[s0 + j] : V(0);
+    __builtin_amdgcn_s_waitcnt(0x0f70);  // vmcnt(0), on this branch only (see above)
+#pragma unroll
+    for (int mi = 0; mi < M; ++mi)
+#pragma unroll
+      for (int j = 0; j < 4; ++j) acc[mi][s0 + j] = a0[mi][j];
   } else {
 #pragma unroll
-    for (int j = 0; j < 4; ++j) d[j] = s0 + j < nt ? G(Dg)[s0 + j] : ~0ull;
-  }
-  // the resident bucket table (plans): kBPT u16 entries per thread
-  const uint32_t* Bg = T.bt;
-  u32x2 btw = {0u, 0u};
-  if (Bg) btw = __builtin_nontemporal_load((const AS1 u32x2*)Bg + tid);
-  V a0[M][4];
+    for (int mi = 0; mi < M; ++mi)
 #pragma unroll
-  for (int mi = 0; mi < M; ++mi)
-#pragma unroll
-    for (int j = 0; j < 4; ++j)
-      a0[mi][j] = (cont && s0 + j < nt) ? G((const V*)T.out[mi] + T.slot0)[s0 + j] : V(0);
-
-  // bucket of a key: the tile's key range [klo, khi] scaled onto [0, kNB) by
-  // one 32x32 high multiply; keys outside the range land in an end bucket
-  // and are not found there
-  const uint64_t klo = G(Dg)[0];
-  const uint64_t khi = G(Dg)[nt - 1];
-  const uint64_t range = khi - klo;
-  const int bits = range ? 64 - __builtin_clzll(range) : 0;
-  const int s2 = bits > 32 ? bits - 32 : 0;
-  const uint64_t r32 = range >> s2;  // < 2^32
-  const uint32_t mul = dev::bucket_scale(r32, kNB);
-  auto bucket = [&](uint64_t k) -> uint32_t {
-    const uint64_t x = (k - klo) >> s2;
-    // no branch: an out-of-range x saturates, and the clamp puts it in the
-    // end bucket (umulhi(r32, mul) < kNB for every in-range x)
-    const uint32_t xs = x > r32 ? 0xffffffffu : (uint32_t)x;
-    const uint32_t b = __umulhi(xs, mul);
-    return b < (uint32_t)(kNB - 1) ? b : (uint32_t)(kNB - 1);
-  };
-
-  // ---- install D, sums, counts; clear the histogram
-#pragma unroll
-  for (int j = 0; j < 4; ++j) {
-    dk[s0 + j] = d[j];
-#pragma unroll
-    for (int mi = 0; mi < M; ++mi) acc[mi][s0 + j] = a0[mi][j];
+      for (int j = 0; j < 4; ++j) acc[mi][s0 + j] = V(0);
   }
   if constexpr (kCntW) {
     typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
@@ -283,17 +341,18 @@ __global__ __launch_bounds__(nt_of(kGroup), (occupancy<V, M, kGroup>())) void ti
     cnt32[2 * tid + 1] = 0u;
   }
   if (tid < 4) dk[kTS + tid] = ~0ull;
-  if (Bg) {  // resident table: installed as loaded
-    bt32[tid * (kBPT / 2)] = btw.x;
-    bt32[tid * (kBPT / 2) + 1] = btw.y;
-    if (tid == 0) bt[kNB] = (uint16_t)nt;
+  if (Bg) {  // resident table: installed above or by the LDS-DMA
+    if (tid == 0) bt[kNB] = (uint16_t)nt;  // past its kNB entries
   } else {
     uint32_t z = 0;  // zero
 #pragma unroll
     for (int i = 0; i < kBPT / 2; ++i) bt32[tid * (kBPT / 2) + i] = z;
   }
   if (tid == 0) pcarry = -1;
-  __syncthreads();  // (1) tables, D, cleared histogram (or the resident bucket table)
+  if (dma)
+    lds_barrier();  // (1) tables, sums, counts (D and the bucket table still in flight)
+  else
+    __syncthreads();  // (1) tables, D, cleared histogram (or the resident bucket table)
   PH(0);
 
   // ---- a pass: this wave's run of rounds, loaded into registers
@@ -357,7 +416,33 @@ __global__ __launch_bounds__(nt_of(kGroup), (occupancy<V, M, kGroup>())) void ti
     }
   };
   if (U) load_pass();
+  if (dma) {  // (1b) D and the bucket table landed (with the element loads)
+    dma_wait();
+    __syncthreads();
+  }
   PH(1);
+
+  // bucket of a key: the tile's key range [klo, khi] scaled onto [0, kNB) by
+  // one 32x32 high multiply; keys outside the range land in an end bucket
+  // and are not found there
+  // (from LDS: D is installed; a global read here would wait for every
+  // load in flight, the LDS-DMA of D included)
+  const uint64_t klo = uni64(dk[0]);
+  const uint64_t khi = uni64(dk[nt - 1]);
+  const uint64_t range = khi - klo;
+  const int bits = range ? 64 - __builtin_clzll(range) : 0;
+  const int s2 = bits > 32 ? bits - 32 : 0;
+  const uint64_t r32 = range >> s2;  // < 2^32
+  const uint32_t mul = dev::bucket_scale(r32, kNB);
+  auto bucket = [&](uint64_t k) -> uint32_t {
+    const uint64_t x = (k - klo) >> s2;
+    // no branch: an out-of-range x saturates, and the clamp puts it in the
+    // end bucket (umulhi(r32, mul) < kNB for every in-range x)
+    const uint32_t xs = x > r32 ? 0xffffffffu : (uint32_t)x;
+    const uint32_t b = __umulhi(xs, mul);
+    return b < (uint32_t)(kNB - 1) ? b : (uint32_t)(kNB - 1);
+  };
+
 
   // ---- bucket table: histogram, exclusive scan -> bt[b] = first slot of bucket b
   // (skipped when the plan's resident index supplied it).  D keys back from

@@ -106,6 +106,35 @@ typedef unsigned long long u64x2 __attribute__((ext_vector_type(2)));
 typedef uint32_t u32x2 __attribute__((ext_vector_type(2)));
 
 __device__ __forceinline__ uint32_t uni(uint32_t v) { return __builtin_amdgcn_readfirstlane(v); }
+__device__ __forceinline__ uint64_t uni64(uint64_t v) {
+  return ((uint64_t)uni((uint32_t)(v >> 32)) << 32) | uni((uint32_t)v);
+}
+
+#ifndef PSG_DDMA
+#define PSG_DDMA 1  // A/B builds: 0 = D and the resident bucket table through registers
+#endif
+// 16 B per lane from global memory straight into LDS (gfx950 LDS-DMA), as
+// in psg_tile.hip: inline asm (the builtin made the compiler wait for it at
+// the next reuse of its address registers); readers wait with dma_wait()
+typedef __attribute__((address_space(3))) void* LdsPtr;
+__device__ __forceinline__ void dma16(const void* g, void* lds) {
+  const uint32_t la = (uint32_t)(uintptr_t)(LdsPtr)lds;
+  uint32_t keep;
+  asm volatile(
+      "s_mov_b32 %0, m0\n\ts_mov_b32 m0, %2\n\ts_nop 0\n\t"
+      "global_load_lds_dwordx4 %1, off nt\n\ts_mov_b32 m0, %0"
+      : "=&s"(keep)
+      : "v"(g), "s"(la)
+      : "memory");
+}
+__device__ __forceinline__ void dma_wait() { asm volatile("s_waitcnt vmcnt(0)" ::: "memory"); }
+// a barrier for LDS writes that leaves vector-memory operations in flight
+__device__ __forceinline__ void lds_barrier() {
+  asm volatile("" ::: "memory");
+  __builtin_amdgcn_s_waitcnt(0xc07f);  // lgkmcnt(0)
+  __builtin_amdgcn_s_barrier();
+  asm volatile("" ::: "memory");
+}
 // the lane index recomputed from nothing (mbcnt over a full mask), so a value
 // needed late in the kernel does not keep the thread-id register live (at 64
 // VGPRs it is the value that would be spilled to scratch: HBM writes)
@@ -465,80 +494,104 @@ __global__ __launch_bounds__(kNT, (occupancy<V, M>())) void tile_packed_kernel(
     }
     if (t == 0u) pre[0] = 0;
   };
+  // ---- D keys, continued sums: thread t owns slots 4t..4t+3
+  const uint32_t s0i = 4u * (uint32_t)tid;
+  // the plan's resident bucket table (psg_tile.hip bucket_index_kernel<64>:
+  // the same 2048 buckets over the same tile)
+  const uint32_t* Bg = T.bt;
+  // full tiles of the partition form: D and the resident bucket table by
+  // LDS-DMA, left in flight across barriers (1) and (1b) and the element
+  // loads (through registers, D had to land before (1) and the element
+  // loads went out after it; psg_tile.hip, profiles/r05_phases_cfg2.txt)
+  const bool dma = !CUR && PSG_DDMA && nt == (uint32_t)kTS && ((uintptr_t)Dg & 15u) == 0u &&
+                   ((uintptr_t)Bg & 15u) == 0u;
+  auto issue_dma = [&]() {
+#pragma unroll
+    for (int j = 0; j < 2; ++j) {  // kTS / 2 16-B units: 2 wave instructions per wave
+      const uint32_t c = 2u * w + (uint32_t)j;
+      dma16(Dg + 128u * c + 2u * (uint32_t)lane, (char*)dk + 1024u * c);
+    }
+    static_assert(kNB / 512 <= kNW, "one 1-KB unit of the bucket table per wave at most");
+    if (Bg && w < (uint32_t)kNB / 512u)
+      dma16((const char*)Bg + 1024u * w + 16u * (uint32_t)lane, (char*)bt32 + 1024u * w);
+  };
+  if (dma && w >= 2) issue_dma();
   if (np) {
     if constexpr (!CUR) tables_a(0);
   }
-
-
-  // ---- D keys, continued sums: thread t owns slots 4t..4t+3
-  const uint32_t s0i = 4u * (uint32_t)tid;
-  uint64_t d[4];
-  if (s0i + 3u < nt && ((uintptr_t)Dg & 15u) == 0u) {
-    const u64x2 x0 = *(const AS1 u64x2*)(Dg + s0i);
-    const u64x2 x1 = *(const AS1 u64x2*)(Dg + s0i + 2);
-    d[0] = x0.x; d[1] = x0.y; d[2] = x1.x; d[3] = x1.y;
-  } else {
+  if (dma && w < 2) issue_dma();  // after waves 0-1's table loads: their waits do not wait for D
+  if (!dma) {
+    // through registers, loaded and installed on this branch only, drained
+    // at its end (the compiler's merged wait state otherwise put a vmcnt(0)
+    // on the LDS-DMA path)
+    uint64_t d[4];
+    if (s0i + 3u < nt && ((uintptr_t)Dg & 15u) == 0u) {
+      const u64x2 x0 = *(const AS1 u64x2*)(Dg + s0i);
+      const u64x2 x1 = *(const AS1 u64x2*)(Dg + s0i + 2);
+      d[0] = x0.x; d[1] = x0.y; d[2] = x1.x; d[3] = x1.y;
+    } else {
 #pragma unroll
-    for (int j = 0; j < 4; ++j) d[j] = s0i + j < nt ? G(Dg)[s0i + j] : ~0ull;
+      for (int j = 0; j < 4; ++j) d[j] = s0i + j < nt ? G(Dg)[s0i + j] : ~0ull;
+    }
+    u32x2 btw = {0u, 0u};
+    if (Bg) btw = __builtin_nontemporal_load((const AS1 u32x2*)Bg + tid);
+#pragma unroll
+    for (int j = 0; j < 4; ++j) dk[s0i + j] = d[j];
+    if (Bg) *(u32x2*)&bt[tid * kBPT] = btw;
+    __builtin_amdgcn_s_waitcnt(0x0f70);  // vmcnt(0)
   }
-  // the plan's resident bucket table (psg_tile.hip bucket_index_kernel<64>:
-  // the same 2048 buckets over the same tile), kBPT u16 entries per thread
-  const uint32_t* Bg = T.bt;
-  u32x2 btw = {0u, 0u};
-  if (Bg) btw = __builtin_nontemporal_load((const AS1 u32x2*)Bg + tid);
-  V a0[M][4];
-#pragma unroll
-  for (int mi = 0; mi < M; ++mi)
-#pragma unroll
-    for (int j = 0; j < 4; ++j)
-      a0[mi][j] = (cont && s0i + j < nt) ? G((const V*)T.out[mi] + T.slot0)[s0i + j] : V(0);
   // cursor form: the pieces, while D and the index are in flight
   uint32_t cx = 0, clv = 0;
   if constexpr (CUR) {
     if (np) clv = cur_a(0, true, &cx);
   }
 
-  // bucket of a key: the tile's key range [klo, khi] scaled onto [0, kNB) by
-  // one 32x32 high multiply; keys outside the range land in an end bucket
-  // and are not found there
-  const uint64_t klo = G(Dg)[0];
-  const uint64_t khi = G(Dg)[nt - 1];
-  const uint64_t range = khi - klo;
-  const int bits = range ? 64 - __builtin_clzll(range) : 0;
-  const int s2 = bits > 32 ? bits - 32 : 0;
-  const uint64_t r32 = range >> s2;  // < 2^32
-  const uint32_t mul = dev::bucket_scale(r32, kNB);
-  auto bucket = [&](uint64_t k) -> uint32_t {
-    const uint64_t x = (k - klo) >> s2;
-    return x > r32 ? (uint32_t)(kNB - 1) : __umulhi((uint32_t)x, mul);
-  };
-
-  // ---- install D, sums, lastl; clear the histogram and the bitmaps
-  // (constants as opaque values: hoisted out of the cursor form's tile loop
-  // they would hold VGPRs across it, and spill)
+  // ---- sums, lastl; clear the histogram and the bitmaps (constants as
+  // opaque values: hoisted out of the cursor form's tile loop they would
+  // hold VGPRs across it, and spill).  The continued sums on their own
+  // branch, drained there (as above)
   uint32_t ones = ~0u, one = 1u;
   if constexpr (CUR) asm volatile("" : "+v"(ones), "+v"(one));
+  if (cont) {
+    V a0[M][4];
 #pragma unroll
-  for (int j = 0; j < 4; ++j) {
-    dk[s0i + j] = d[j];
+    for (int mi = 0; mi < M; ++mi)
 #pragma unroll
-    for (int mi = 0; mi < M; ++mi) acc[mi][s0i + j] = a0[mi][j];
-    lastl[s0i + j] = (uint16_t)one;  // last = -1 = g0 - 1
+      for (int j = 0; j < 4; ++j)
+        a0[mi][j] = s0i + j < nt ? G((const V*)T.out[mi] + T.slot0)[s0i + j] : V(0);
+    __builtin_amdgcn_s_waitcnt(0x0f70);  // vmcnt(0)
+#pragma unroll
+    for (int mi = 0; mi < M; ++mi)
+#pragma unroll
+      for (int j = 0; j < 4; ++j) acc[mi][s0i + j] = a0[mi][j];
+  } else {
+#pragma unroll
+    for (int mi = 0; mi < M; ++mi)
+#pragma unroll
+      for (int j = 0; j < 4; ++j) acc[mi][s0i + j] = V(0);
   }
+#pragma unroll
+  for (int j = 0; j < 4; ++j) lastl[s0i + j] = (uint16_t)one;  // last = -1 = g0 - 1
   if (tid < 8) dk[kTS + tid] = (uint64_t)ones << 32 | ones;
   {
     uint32_t z = 0;  // opaque zero: not a hoisted (and spilled) constant vector
     asm volatile("" : "+v"(z));
-    *(u32x2*)&bt[tid * kBPT] = Bg ? btw : u32x2{z, z};  // resident table, or a cleared histogram
-    if (Bg && tid == 0) bt[kNB] = (uint16_t)nt;
+    if (!Bg) *(u32x2*)&bt[tid * kBPT] = u32x2{z, z};  // a cleared histogram
+    if (Bg && tid == 0) bt[kNB] = (uint16_t)nt;  // past the table's kNB entries
   }
   if (tid == 0) pcarry = (int)ones;
-  __syncthreads();  // (1) pieces scanned, D, cleared histogram (or the resident bucket table)
+  if (dma)
+    lds_barrier();  // (1) pieces scanned, sums (D and the bucket table in flight)
+  else
+    __syncthreads();  // (1) pieces scanned, D, cleared histogram (or the resident bucket table)
   if (np) {
     if constexpr (CUR) cur_b(0, clv, cx);
     else tables_b(0);
   }
-  __syncthreads();  // (1b) the group's tables
+  if (dma)
+    lds_barrier();  // (1b) the group's tables
+  else
+    __syncthreads();  // (1b) the group's tables
 
   // ---- a pass: this wave's run of rounds, loaded into registers
   uint32_t gp = np ? uni(gsh[0]) : 0u;
@@ -593,6 +646,26 @@ __global__ __launch_bounds__(kNT, (occupancy<V, M>())) void tile_packed_kernel(
     }
   };
   if (U) load_pass();
+  if (dma) {  // (1c) D and the bucket table landed (with the element loads)
+    dma_wait();
+    __syncthreads();
+  }
+
+  // bucket of a key: the tile's key range [klo, khi] scaled onto [0, kNB) by
+  // one 32x32 high multiply; keys outside the range land in an end bucket
+  // and are not found there.  klo, khi from LDS: a global read here would
+  // wait for every load in flight
+  const uint64_t klo = uni64(dk[0]);
+  const uint64_t khi = uni64(dk[nt - 1]);
+  const uint64_t range = khi - klo;
+  const int bits = range ? 64 - __builtin_clzll(range) : 0;
+  const int s2 = bits > 32 ? bits - 32 : 0;
+  const uint64_t r32 = range >> s2;  // < 2^32
+  const uint32_t mul = dev::bucket_scale(r32, kNB);
+  auto bucket = [&](uint64_t k) -> uint32_t {
+    const uint64_t x = (k - klo) >> s2;
+    return x > r32 ? (uint32_t)(kNB - 1) : __umulhi((uint32_t)x, mul);
+  };
 
   // ---- bucket table: histogram, exclusive scan -> bt[b] = first slot of bucket b
   // (skipped when the plan's resident index supplied it).  D keys back from

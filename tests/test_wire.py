@@ -653,6 +653,50 @@ def test_gpu_snappy_deferred_literals():
 
 
 @pytest.mark.gpu
+def test_gpu_snappy_offsets_past_the_ring_and_many_deferred():
+    """The 8 KB output ring: element-dense parts (16-byte literals and copies
+    of every length 1..64) whose copies reach inside the ring, just past it
+    (8,193 .. 65,535 back: 2-byte offsets, read from global memory after a
+    flush) and far past it (4-byte offsets); many such parts at once (the
+    launch keeps ten parts per CU); and a part with more deferred literals
+    (>= 2048 bytes) than its 256-piece list holds, so the rest move in the
+    parse -- byte-exact against the spec oracle."""
+    rng = np.random.default_rng(12)
+    parts, datas = [], []
+    for v in range(24):
+        el, o = [], 0
+        while o < 200_000:
+            el.append(("lit", rng.integers(0, 256, 16, dtype=np.uint8).tobytes()))
+            o += 16
+            band = int(rng.integers(0, 4))
+            hi = [64, 8192, 65535, 200_000][band]
+            lo = [1, 65, 8193, 65536][band]
+            if o > lo:
+                off = int(rng.integers(lo, min(hi, o) + 1))
+                ln = int(rng.integers(1, 65))
+                el.append(("copy", off, ln))
+                o += ln
+        comp, want = _snappy_stream(el)
+        parts.append(comp)
+        datas.append(want)
+    el = []
+    for i in range(300):
+        el.append(("lit", rng.integers(0, 256, int(rng.choice([2048, 2100, 4096])),
+                                       dtype=np.uint8).tobytes()))
+        el.append(("copy", 2500, 64))
+        el.append(("copy", 9000, 17))
+    comp, want = _snappy_stream(el)
+    assert O.snappy_uncompress(comp) == want
+    parts.append(comp)
+    datas.append(want)
+    assert O.snappy_uncompress(parts[0]) == datas[0]
+    got, st = _gpu_snappy(parts, [len(d) for d in datas])
+    assert st == [0] * len(parts)
+    for g, d in zip(got, datas):
+        assert g == d
+
+
+@pytest.mark.gpu
 def test_gpu_push_compressed_matches_plain_push():
     """psg_push_compressed: snappy parts off the wire (keys + m value parts),
     decompressed on the device and merged -- the same bits as plain pushes;

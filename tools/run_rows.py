@@ -1,4 +1,5 @@
-"""MEASUREMENT AID: bench.py's 8(f)-row block alone (python tools/run_rows.py)."""
+"""MEASUREMENT AID: bench.py's 8(f)-row block alone (python tools/run_rows.py
+[group ...]; groups: nway gather crc snappy countmin darling, default all)."""
 import json
 import os
 import sys
@@ -9,4 +10,5 @@ import bench  # noqa: E402
 if __name__ == "__main__":
     import torch
     assert torch.cuda.is_available()
-    print(json.dumps(bench.bench_rows(0), indent=1))
+    only = set(sys.argv[1:]) or None
+    print(json.dumps(bench.bench_rows(0, only=only), indent=1))
