@@ -433,7 +433,10 @@ int psg_freq_insert(psg_ctx* ctx, int chl, const uint64_t* keys,
 int psg_freq_query(psg_ctx* ctx, int chl, const uint64_t* keys, size_t n,
                    int freq, uint64_t* out, size_t* nout);
 /* Device-resident forms on `stream`: *nout is a device word; scratch holds
- * psg_freq_query_scratch_bytes(n) device bytes. */
+ * psg_freq_query_scratch_bytes(n) device bytes (the binned query's records:
+ * about 50 B per key up to 8 M keys, then constant -- longer queries take
+ * several chunks).  A filter's operations run in call order whatever streams
+ * they are enqueued on (each waits for the previous one's event). */
 int psg_freq_insert_dev(psg_ctx* ctx, int chl, const uint64_t* keys,
                         const uint32_t* counts, size_t n, void* stream);
 size_t psg_freq_query_scratch_bytes(size_t n);
