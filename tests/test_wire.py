@@ -679,7 +679,7 @@ def test_gpu_snappy_offsets_past_the_ring_and_many_deferred():
         comp, want = _snappy_stream(el)
         parts.append(comp)
         datas.append(want)
-    el = []
+    el = [("lit", rng.integers(0, 256, 12000, dtype=np.uint8).tobytes())]
     for i in range(300):
         el.append(("lit", rng.integers(0, 256, int(rng.choice([2048, 2100, 4096])),
                                        dtype=np.uint8).tobytes()))
