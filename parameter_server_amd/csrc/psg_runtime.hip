@@ -848,12 +848,6 @@ struct psg_ctx {
   hipStream_t stream = nullptr;  // kernels, D2H
   hipStream_t copy = nullptr;    // H2D of pushes / keys / values
   hipEvent_t copy_ev = nullptr;
-  // compressed pushes decode as they land, on a stream of their own, so the
-  // next push's transfer on `copy` runs beside the decode (dec_ev: after the
-  // last decode; the merge joins it with the copies)
-  hipStream_t dec = nullptr;
-  hipEvent_t dec_ev = nullptr;
-  bool dec_pending = false;
 
   std::mutex mu;
   std::unordered_map<int, Channel> ch;
@@ -1233,10 +1227,6 @@ struct psg_ctx {
     if (int rc = zc_flush()) return rc;
     HIP_TRY(hipEventRecord(copy_ev, copy));
     HIP_TRY(hipStreamWaitEvent(stream, copy_ev, 0));
-    if (dec_pending) {
-      HIP_TRY(hipStreamWaitEvent(stream, dec_ev, 0));
-      dec_pending = false;
-    }
     return PSG_OK;
   }
 
@@ -1598,8 +1588,6 @@ int psg_create(int device, int dtype, unsigned flags, psg_ctx** out) {
   hipError_t e = hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking);
   if (e == hipSuccess) e = hipStreamCreateWithFlags(&c->copy, hipStreamNonBlocking);
   if (e == hipSuccess) e = hipEventCreateWithFlags(&c->copy_ev, hipEventDisableTiming);
-  if (e == hipSuccess) e = hipStreamCreateWithFlags(&c->dec, hipStreamNonBlocking);
-  if (e == hipSuccess) e = hipEventCreateWithFlags(&c->dec_ev, hipEventDisableTiming);
   if (e == hipSuccess) e = hipMalloc((void**)&c->d_small, 256);
   if (e == hipSuccess) e = hipHostMalloc((void**)&c->h_small, 256);
   if (e != hipSuccess) {
@@ -1619,7 +1607,6 @@ int psg_destroy(psg_ctx* c) {
   (void)hipSetDevice(c->device);
   c->zc.n = 0;  // held buffers of pushes never merged: not read any more
   if (c->copy) (void)hipStreamSynchronize(c->copy);
-  if (c->dec) (void)hipStreamSynchronize(c->dec);
   if (c->stream) (void)hipStreamSynchronize(c->stream);
   for (auto& kv : c->agg) c->drop(kv.second);
   c->agg.clear();
@@ -1646,8 +1633,6 @@ int psg_destroy(psg_ctx* c) {
   if (c->h_small) (void)hipHostFree(c->h_small);
   (void)hipFree(c->scratch);
   if (c->copy_ev) (void)hipEventDestroy(c->copy_ev);
-  if (c->dec_ev) (void)hipEventDestroy(c->dec_ev);
-  if (c->dec) (void)hipStreamDestroy(c->dec);
   if (c->copy) (void)hipStreamDestroy(c->copy);
   if (c->stream) (void)hipStreamDestroy(c->stream);
   delete c;
@@ -2122,26 +2107,17 @@ int psg_push_compressed(psg_ctx* c, int chl, int time, uint64_t kb, uint64_t ke,
   if (int rc = set_dev(c->device)) return rc;
   size_t lo, hi;
   if (int rc = check_push(c, chl, time, kb, ke, n, m, &lo, &hi)) return rc;
-  // staging block: the m + 1 compressed parts back to back.  Buffers not
-  // held: the parts decode as soon as they land, on `dec`, beside the next
-  // push's transfer (their decoder table, status and scratch after them in
-  // the block); held buffers (copied at the merge): decoded right before the
-  // merge that needs them (psg_ctx::flush), with every other compressed push
-  // pending then, in one launch
+  // staging block: the m + 1 compressed parts back to back; they are
+  // decoded right before the merge that needs them (psg_ctx::flush), with
+  // every other compressed push pending then, in one launch
   const int np = m + 1;
-  const bool now = !(c->flags & PSG_HOLD_BUFFERS);
   // part i at soff[i], 16-B aligned (the zero-copy read needs both ends
   // aligned), plen[i] bytes
   std::vector<uint64_t> soff(np + 1, 0), plen(np, 0);
   plen[0] = ckeys_bytes;
   for (int i = 0; i < m; ++i) plen[i + 1] = cvals_bytes[i];
   for (int i = 0; i < np; ++i) soff[i + 1] = align_up(soff[i] + plen[i], 16);
-  const size_t pb = align_up(soff[np], 256);
-  const size_t tab_off = pb, st_off = tab_off + align_up(32 * (size_t)np, 256), sc_off = st_off + 256;
-  const size_t tb = now ? sc_off + psg::snappy_scratch_bytes((uint64_t)np) : pb;
-  Aggregate* A = nullptr;  // the decode counts corrupt parts in its counters
-  if (now)
-    if (int rc = c->aggregate_for(chl, time, kb, ke, m, &A)) return rc;
+  const size_t tb = align_up(soff[np], 256);
   void* blk = nullptr;
   if (int rc = c->dev_get(tb, &blk, c->copy)) return rc;
   KeyRef k;
@@ -2150,50 +2126,29 @@ int psg_push_compressed(psg_ctx* c, int chl, int time, uint64_t kb, uint64_t ke,
   int rc = c->new_keys(n, &k);
   if (rc == PSG_OK) rc = c->dev_get(m * vb, &vblock, c->copy);
   char* b = (char*)blk;
+  // the parts in one zero-copy launch when the caller's buffers are pinned
+  c->zc_group = true;
+  if (rc == PSG_OK) rc = c->h2d(b, ckeys, ckeys_bytes, true);
+  for (int i = 0; rc == PSG_OK && i < m; ++i) rc = c->h2d(b + soff[i + 1], cvals[i], cvals_bytes[i], true);
+  c->zc_group = false;
+  if (rc == PSG_OK && !(c->flags & PSG_HOLD_BUFFERS)) rc = c->zc_flush();
+  // the caller's buffers are free once their copies land (unless held)
+  if (rc == PSG_OK) rc = c->h2d_finish();
+  if (rc != PSG_OK) {
+    if (!(c->flags & PSG_HOLD_BUFFERS)) c->zc.n = 0;  // this push's queued copies only
+    (void)hipStreamSynchronize(c->copy);
+    c->dev_put(blk, tb);
+    c->dev_put(vblock, m * vb);
+    return rc;
+  }
   PendingPush cp;
-  for (int i = 0; rc == PSG_OK && i < np; ++i) {
+  cp.cparts = np;
+  for (int i = 0; i < np; ++i) {
     cp.cbeg[i] = (uint64_t)(b + soff[i]);
     cp.cend[i] = (uint64_t)(b + soff[i] + plen[i]);
     cp.cdst[i] = i == 0 ? (uint64_t)k->d : (uint64_t)((char*)vblock + (i - 1) * vb);
     cp.ccap[i] = i == 0 ? (uint64_t)klen : (uint64_t)(n * sv);
   }
-  // [pairs 16 np][dst 8 np][cap 8 np] (kept until h2d_finish: staged below)
-  std::vector<uint64_t> img(now ? 4 * (size_t)np : 0);
-  for (int i = 0; now && i < np; ++i) {
-    img[2 * i] = cp.cbeg[i];
-    img[2 * i + 1] = cp.cend[i];
-    img[2 * np + i] = cp.cdst[i];
-    img[3 * np + i] = cp.ccap[i];
-  }
-  // the parts in one zero-copy launch when the caller's buffers are pinned
-  c->zc_group = true;
-  if (rc == PSG_OK) rc = c->h2d(b, ckeys, ckeys_bytes, true);
-  for (int i = 0; rc == PSG_OK && i < m; ++i) rc = c->h2d(b + soff[i + 1], cvals[i], cvals_bytes[i], true);
-  if (rc == PSG_OK && now) rc = c->h2d(b + tab_off, img.data(), 32 * (size_t)np);
-  c->zc_group = false;
-  if (rc == PSG_OK && now) rc = c->zc_flush();
-  if (rc == PSG_OK && now) {
-    const uint64_t* d = (const uint64_t*)(b + tab_off);
-    hipError_t e = hipEventRecord(c->copy_ev, c->copy);
-    if (e == hipSuccess) e = hipStreamWaitEvent(c->dec, c->copy_ev, 0);
-    if (e == hipSuccess)
-      e = psg::launch_snappy(nullptr, d, (uint64_t)np, nullptr, d + 2 * np, d + 3 * np,
-                             (int32_t*)(b + st_off), b + sc_off, c->dec, A->d_bad + 1, true);
-    if (e == hipSuccess) e = hipEventRecord(c->dec_ev, c->dec);
-    if (e != hipSuccess) rc = fail(PSG_ERR_DEVICE, "snappy: %s", hipGetErrorString(e));
-    c->dec_pending = true;
-  }
-  // the caller's buffers are free once their copies land (unless held)
-  if (rc == PSG_OK) rc = c->h2d_finish();
-  if (rc != PSG_OK) {
-    if (now) c->zc.n = 0;  // this push's queued copies only
-    (void)hipStreamSynchronize(c->copy);
-    (void)hipStreamSynchronize(c->dec);
-    c->dev_put(blk, tb);
-    c->dev_put(vblock, m * vb);
-    return rc;
-  }
-  cp.cparts = now ? 0 : np;  // decoded already, or at the merge
   return c->push_values(chl, time, kb, ke, k, m, nullptr, vblock, nullptr, blk, tb, &cp);
 }
 

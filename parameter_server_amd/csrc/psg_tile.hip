@@ -165,6 +165,9 @@ constexpr int occupancy() {
                       nw * 8 + 8;
   // waves per SIMD (the launch bound's unit): workgroups per CU x waves / 4
   constexpr int w = (163840 / lds) * nw / 4;
+#ifdef PSG_OCC64
+  if (kGroup == 64) return PSG_OCC64;  // A/B builds: fewer waves, more registers per round
+#endif
   return w >= 8 ? 8 : (w < 1 ? 1 : w);
 }
 
