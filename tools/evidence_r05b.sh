@@ -1,0 +1,13 @@
+# r05 evidence, part B: cfg5 PMC passes, the final default bench line, side lines.
+set -o pipefail
+export TMPDIR=/tmp
+R=${1:-r05}; O=gpurun_out/$R; mkdir -p $O $O/side
+PASSES="1 2 3" ./tools/pmc2.sh $O/pmc_cfg5 "--workload cfg5" > $O/pmc_cfg5.log 2>&1 || { echo "pmc cfg5 failed"; tail -5 $O/pmc_cfg5.log; exit 1; }
+timeout -k 10 600 python3 bench.py --no-cpu-baseline --workload cfg5 --steps 5 > $O/cfg5_bpl.json 2> $O/cfg5_bpl.err || exit 1
+BPL5=$(python3 -c "import json;print(json.load(open('$O/cfg5_bpl.json'))['roofline']['bytes_per_launch'])") || exit 1
+python3 tools/pmc_traffic.py $O/pmc_cfg5/summary.json $BPL5 tile_packed_kernel $O/pmc_summary_cfg5.json cfg5 > $O/pmc_traffic_cfg5.json || exit 1
+timeout -k 10 600 python3 bench.py > $O/bench.json 2> $O/bench.err || { echo "bench failed"; tail -5 $O/bench.err; exit 1; }
+python3 -c "import json;d=json.load(open('$O/bench.json'));r=d['roofline'];print('bench %.4e ms %.4f kern %.4f frac %.3f step %.3f'%(d['value'],d['ms_per_step'],r['kernel_ms'],r['frac'],r['step_frac']))"
+NOTEST=1 WLS="cfg3 cfg4" bash tools/quick_bench.sh $O/side || exit 1
+timeout -k 10 300 python3 bench.py --no-cpu-baseline --no-cfg5 --dtype f64 > $O/side/cfg2_f64.json 2> $O/side/cfg2_f64.err || { echo "f64 failed"; exit 1; }
+echo done
