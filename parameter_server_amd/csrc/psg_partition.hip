@@ -230,26 +230,13 @@ __device__ __forceinline__ void stream_item(const JobDev& J, uint32_t p, uint32_
     // (the push's last chunk fills every remaining boundary with n)
     if (!last && uni64((uint64_t)__shfl((long long)sv, 63, 64)) > klast) break;
   }
-  // order check: a key not above its predecessor cannot match
-  // (element j*64 + lane follows lane - 1's element j, or lane 63's
-  // element j - 1, or the previous chunk's last key)
-  uint32_t bad = 0;
-  {
-    const uint64_t before =
-        i0 > 0 ? uni64(((const __attribute__((address_space(1))) uint64_t*)S)[i0 - 1]) : 0ull;
-#pragma unroll
-    for (int j = 0; j < kKPL; ++j) {
-      const uint64_t up = (uint64_t)__shfl_up((long long)k[j], 1, 64);
-      const uint64_t l63 = j > 0 ? (uint64_t)__shfl((long long)k[j > 0 ? j - 1 : 0], 63, 64)
-                                 : before;
-      const uint64_t prev = lane == 0 ? l63 : up;
-      const bool has = lane > 0 || j > 0 || i0 > 0;
-      if (64u * j + (uint32_t)lane < cl && has && !(prev < k[j])) ++bad;
-    }
-  }
-  if (__ballot(bad != 0) && bad)
-    __hip_atomic_fetch_add(J.fail + p, (unsigned long long)bad, __ATOMIC_RELAXED,
-                           __HIP_MEMORY_SCOPE_AGENT);
+  // No order check here (r05): the aggregate kernel finds an unsorted push
+  // by itself -- every key must be found, at strictly increasing positions
+  // inside its piece, and a piece whose bounds run backwards is an
+  // overflow -- so the push's fail counter is only reset here, by its
+  // first chunk, ahead of the aggregate launch that adds to it (plans then
+  // need no per-run splitter pass, psg_runtime.hip run_stage)
+  if (c == 0 && lane == 0) J.fail[p] = 0ull;
 }
 
 __global__ __launch_bounds__(256) void partition_kernel(const JobDev* __restrict__ jobs,

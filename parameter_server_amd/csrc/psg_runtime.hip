@@ -193,6 +193,9 @@ struct JobTable {
   };
   std::vector<JobInfo> info;
   uint32_t ntiles = 0, nitems = 0, nsplit = 0;
+  // plans (D fixed for their lifetime): the stream jobs' splitters are
+  // written once, at build, and a run launches only the partition proper
+  bool split_once = false;
   void* blob = nullptr;
   size_t blob_bytes = 0;
   JobDev* d_jobs = nullptr;
@@ -602,6 +605,9 @@ struct JobTable {
     if (use_index)
       HIP_TRY(psg::launch_bucket_index(d_tiles, ntiles, tile,
                                        (uint32_t*)((char*)blob + index_off), strm));
+    split_once = index && nsplit > 0 && !dense && !cursor && !pcursor;
+    if (split_once)  // the splitter pass alone (it also clears the fail counters once)
+      HIP_TRY(psg::launch_partition(d_jobs, d_split_items, nsplit, nullptr, 0, strm));
     if (!async) HIP_TRY(hipStreamSynchronize(strm));
     return PSG_OK;
   }
@@ -611,7 +617,9 @@ struct JobTable {
     if (stage == 0) {
       if (cursor || pcursor)  // fail counters, boundaries
         HIP_TRY(hipMemsetAsync(d_zero, 0, zero_bytes, s));
-      else if (!dense) HIP_TRY(psg::launch_partition(d_jobs, d_split_items, nsplit, d_items, nitems, s));
+      else if (!dense)
+        HIP_TRY(psg::launch_partition(d_jobs, d_split_items, split_once ? 0u : nsplit, d_items,
+                                      nitems, s));
     } else if (cursor)
       HIP_TRY(psg::launch_aggregate_cursor(dtype, m, (int)ckr, d_cjobs, d_chunks, nchunks, d_bx, s));
     else if (dense)
