@@ -2,6 +2,15 @@
 set -o pipefail
 export TMPDIR=/tmp
 R=${1:-r05}; O=gpurun_out/$R; mkdir -p $O $O/side
+# A/B of the once-written splitters (sp0 = before, sp1 = after): one cfg5 shard, the whole cfg5
+if [ -d build/sp0 ] && [ -d build/sp1 ]; then
+  for rep in 1 2; do for v in sp0 sp1; do
+    PSG_LIB_PATH=$PWD/build/$v/libpsg.so timeout -k 10 300 python3 tools/shard_probe.py 30 > $O/sh_$v.txt 2> $O/sh_$v.err || { echo FAIL $v; tail -5 $O/sh_$v.err; exit 1; }
+    echo "$rep $v $(cat $O/sh_$v.txt)" | tee -a $O/ab_split.txt
+  done; done
+  bash tools/ab_run.sh "sp0 sp1" "cfg5" >> $O/ab_split.txt 2>&1 || { echo AB FAILED; tail -5 $O/ab_split.txt; exit 1; }
+  tail -4 $O/ab_split.txt
+fi
 PASSES="1 2 3" ./tools/pmc2.sh $O/pmc_cfg5 "--workload cfg5" > $O/pmc_cfg5.log 2>&1 || { echo "pmc cfg5 failed"; tail -5 $O/pmc_cfg5.log; exit 1; }
 timeout -k 10 600 python3 bench.py --no-cpu-baseline --workload cfg5 --steps 5 > $O/cfg5_bpl.json 2> $O/cfg5_bpl.err || exit 1
 BPL5=$(python3 -c "import json;print(json.load(open('$O/cfg5_bpl.json'))['roofline']['bytes_per_launch'])") || exit 1
