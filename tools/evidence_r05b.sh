@@ -11,6 +11,11 @@ if [ -d build/sp0 ] && [ -d build/sp1 ]; then
   bash tools/ab_run.sh "sp0 sp1" "cfg5" >> $O/ab_split.txt 2>&1 || { echo AB FAILED; tail -5 $O/ab_split.txt; exit 1; }
   tail -4 $O/ab_split.txt
 fi
+# the packed kernel's memory side alone (PSG_SKELETON=1: loads and stores, no search or fold)
+if [ -d build/pks ]; then
+  bash tools/ab_run.sh "sp1 pks" "cfg5" > $O/ab_packed_skeleton.txt 2>&1 || { echo AB FAILED; tail -5 $O/ab_packed_skeleton.txt; exit 1; }
+  cat $O/ab_packed_skeleton.txt
+fi
 PASSES="1 2 3" ./tools/pmc2.sh $O/pmc_cfg5 "--workload cfg5" > $O/pmc_cfg5.log 2>&1 || { echo "pmc cfg5 failed"; tail -5 $O/pmc_cfg5.log; exit 1; }
 timeout -k 10 600 python3 bench.py --no-cpu-baseline --workload cfg5 --steps 5 > $O/cfg5_bpl.json 2> $O/cfg5_bpl.err || exit 1
 BPL5=$(python3 -c "import json;print(json.load(open('$O/cfg5_bpl.json'))['roofline']['bytes_per_launch'])") || exit 1
