@@ -982,6 +982,7 @@ def bench_rows(device, reps=5, insts=None, only=None):
     import ctypes as C
     import torch
     from parameter_server_amd import _lib, synth
+    from parameter_server_amd.kv_vector import KVVector, Message
     L = _lib.lib()
     dev = torch.device("cuda", device)
     st = torch.cuda.current_stream()
@@ -1152,7 +1153,6 @@ def bench_rows(device, reps=5, insts=None, only=None):
         del dsrc, ddst
     if only is None or 'countmin' in only:
         # CountMin: insertKeys / queryKeys of 16.8 M keys, 2^26 counters, k = 4
-        from parameter_server_amd.kv_vector import KVVector, Message
         v = KVVector(device)
         nk = 1 << 24
         keys = torch.randint(0, 1 << 62, (nk,), dtype=torch.int64, device=dev)

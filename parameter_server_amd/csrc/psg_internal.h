@@ -194,10 +194,13 @@ hipError_t launch_unmatched(const JobDev* jobs, uint32_t job, uint32_t npush,
 struct DarlingParam {
   double eta, lambda, kkt, delta_max;
 };
+// slots: kVioSlots x 64 B of zeroed device memory (left zeroed); *vio is
+// written by the launch (the violation's bit pattern, 0 if none)
+constexpr int kVioSlots = 256;
 hipError_t launch_darling(const double* G, const double* U, double* w, double* delta,
                           uint32_t* active, uint64_t lo, uint64_t n, const DarlingParam& P,
-                          const unsigned long long* bad, unsigned long long* vio,
-                          hipStream_t stream);
+                          const unsigned long long* bad, unsigned long long* slots,
+                          unsigned long long* vio, hipStream_t stream);
 hipError_t launch_darling_init(double* delta, uint32_t* active, uint64_t n, double delta_init,
                                hipStream_t stream);
 hipError_t launch_bitmap_fill(uint32_t* active, uint64_t n, hipStream_t stream);

@@ -864,6 +864,7 @@ struct psg_ctx {
   std::unordered_map<int, Filter> ff;
   JobTable table;
   unsigned long long* d_small = nullptr;  // 32 device words: counters, crc args
+  unsigned long long* d_vio_slots = nullptr;  // psg::kVioSlots x 64 B, zero between updates
   unsigned long long* h_small = nullptr;  // 32 pinned host words
   void* scratch = nullptr;
   size_t scratch_bytes = 0;
@@ -1597,6 +1598,8 @@ int psg_create(int device, int dtype, unsigned flags, psg_ctx** out) {
   if (e == hipSuccess) e = hipStreamCreateWithFlags(&c->copy, hipStreamNonBlocking);
   if (e == hipSuccess) e = hipEventCreateWithFlags(&c->copy_ev, hipEventDisableTiming);
   if (e == hipSuccess) e = hipMalloc((void**)&c->d_small, 256);
+  if (e == hipSuccess) e = hipMalloc((void**)&c->d_vio_slots, 64 * psg::kVioSlots);
+  if (e == hipSuccess) e = hipMemsetAsync(c->d_vio_slots, 0, 64 * psg::kVioSlots, c->stream);
   if (e == hipSuccess) e = hipHostMalloc((void**)&c->h_small, 256);
   if (e != hipSuccess) {
     psg_destroy(c);
@@ -1638,6 +1641,7 @@ int psg_destroy(psg_ctx* c) {
   c->pool_release();
   if (c->ring) (void)hipHostFree(c->ring);
   (void)hipFree(c->d_small);
+  (void)hipFree(c->d_vio_slots);
   if (c->h_small) (void)hipHostFree(c->h_small);
   (void)hipFree(c->scratch);
   if (c->copy_ev) (void)hipEventDestroy(c->copy_ev);
@@ -2398,11 +2402,9 @@ int psg_darling_update(psg_ctx* c, int chl, int time, const psg_darling_param* p
   if (rc == PSG_OK) {
     const psg::DarlingParam P{p->eta, p->lambda, p->kkt_filter_threshold, p->delta_max};
     unsigned long long* dv = c->d_small + 4;
-    hipError_t e = hipMemsetAsync(dv, 0, 8, c->stream);
-    if (e == hipSuccess)
-      e = psg::launch_darling((const double*)A.d_out[0], (const double*)A.d_out[1],
-                              (double*)C.d_vals, C.d_delta, C.d_active, A.lo, A.hi - A.lo, P,
-                              A.d_bad, dv, c->stream);
+    hipError_t e = psg::launch_darling((const double*)A.d_out[0], (const double*)A.d_out[1],
+                                       (double*)C.d_vals, C.d_delta, C.d_active, A.lo,
+                                       A.hi - A.lo, P, A.d_bad, c->d_vio_slots, dv, c->stream);
     if (e == hipSuccess)
       e = hipMemcpyAsync(c->h_small + 4, dv, 8, hipMemcpyDeviceToHost, c->stream);
     if (e == hipSuccess)

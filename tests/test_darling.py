@@ -221,3 +221,51 @@ def test_gpu_darling_unmatched_leaves_model():
     rc, _ = darling_call(v, 0, 5, 1.0, 0.1, 1e20, 5.0)
     assert rc == _lib.PSG_ERR_ARG
     v.close()
+
+
+@pytest.mark.gpu
+def test_gpu_darling_large_block_grid_stride():
+    """One feature block of ~1.2 M positions (more than the 2,048 workgroups
+    x 256 positions one pass of the launch covers, so every workgroup loops),
+    starting at an unaligned bitmap word: two iterations, the second with the
+    KKT filter on; w / delta / active / violation bit-exact against the
+    oracle (the violation is one max over every workgroup's)."""
+    import torch
+    assert torch.cuda.is_available()
+    from parameter_server_amd import _lib
+    rng = np.random.default_rng(1202)
+    n = 1_300_000
+    D = np.unique(rng.integers(1, 1 << 50, n + 4096, dtype=np.uint64))[:n]
+    v = _ctx()
+    v.setValue(_msg(D, t=0))
+    w = np.zeros(n)
+    v.set_value_array(0, w)
+    _lib.check(v._L.psg_darling_init(v._h, 0, 1.0))
+    delta = np.full(n, 1.0)
+    active = np.ones(n, np.uint8)
+    lo, hi = 1007, n - 5
+    kb, ke = int(D[lo]), int(D[hi])
+    t = 3
+    for it in range(2):
+        kkt = 1e20 if it == 0 else 0.05
+        pushes = []
+        for wk in range(2):
+            pos = np.sort(rng.choice(np.arange(lo, hi), (hi - lo) * 3 // 4, replace=False))
+            g = rng.standard_normal(pos.size) * (0.3 + it)
+            u = rng.random(pos.size) * 2
+            pushes.append((D[pos], [g, u]))
+            v.setValue(_msg(D[pos], [g, u], t=t, rng=(kb, ke)))
+        rc, lo2, hi2, (G, U), _ = O.aggregate(D, kb, ke, pushes, dtype=np.float64)
+        assert rc == 0 and (lo2, hi2) == (lo, hi)
+        rc, vio = darling_call(v, 0, t, 0.8, 0.1, kkt, 5.0)
+        _lib.check(rc)
+        w, delta, active, vio_o = O.darling_update_weight(w, delta, active, lo, G, U, 0.8,
+                                                          0.1, kkt, 5.0, 0.0)
+        assert vio == vio_o and vio > 0
+        t += 1
+    got_d, got_a, nnz = darling_state(v, 0, n)
+    assert np.array_equal(bits64(v.value(0)), bits64(w))
+    assert np.array_equal(bits64(got_d), bits64(delta))
+    assert np.array_equal(got_a, active)
+    assert nnz == int(active.sum()) and nnz < n
+    v.close()

@@ -16,7 +16,8 @@ def rows(pattern):
 
 
 def short(name):
-    for k in ("cm_bin_count", "cm_bin_scan", "cm_bin_scatter", "cm_bin_apply", "nw_tile_kernel",
+    for k in ("cm_ibin_kernel", "cm_transpose_kernel", "cm_iapply_kernel", "cm_qbin_kernel",
+              "cm_qlook_kernel", "cm_qkeep_kernel", "cm_bin_count", "cm_bin_scan", "cm_bin_scatter", "cm_bin_apply", "nw_tile_kernel",
               "nw_gather", "nw_bucket", "nw_split", "nw_rank", "cursor_kernel", "tile_packed_kernel", "tile_kernel", "splitter_kernel", "partition_kernel",
               "unmatched_kernel", "gather_kernel", "union", "slice_kernel", "crc_kernel",
               "darling_kernel", "cm_insert", "cm_count", "cm_scan", "cm_scatter",
