@@ -290,14 +290,26 @@ __device__ unsigned long long g_nwprof[65536][8];
 #define NP_MARK(i) do { } while (0)
 #endif
 
+// LDS layout of the tile's keys and source indices: XOR swizzles inside
+// aligned blocks (no extra LDS).  Lane l's elements e = 8 l + x land in u64
+// bank slot 8 (l mod 4) + (x ^ (l / 4 mod 8)) for keys and in dword bank
+// 4 (l mod 8) + (x / 2 ^ (l / 8 mod 4)) for source indices, so the loads'
+// installs, the merge walks and write-backs of a wave's 32 lanes hit 32
+// different banks instead of 4 or 8 (r05: batch 1.49 -> 1.41 ms,
+// profiles/r05_ab_nway.txt)
+#define SWK(e) ((e) ^ (((e) >> 5) & 7u))
+#define SWI(e) ((e) ^ ((((e) >> 6) & 3u) << 1))
+
 
 // 5. the tile merge
 template <typename V, int M>
 __global__ __launch_bounds__(kNT) void nw_tile_kernel(NwBatch bt) {
   constexpr int kM = M > 0 ? M : 1;
   constexpr int kVC = M > 0 ? kCap : 1;
-  __shared__ __attribute__((aligned(16))) uint64_t sk[kCap];  // keys (merged in place)
-  __shared__ uint16_t si[kCap];                               // source position of each key
+  // keys (merged in place) and the source position of each key, at the
+  // swizzled indices SWK / SWI (above)
+  __shared__ __attribute__((aligned(16))) uint64_t sk[kCap];
+  __shared__ uint16_t si[kCap];
   __shared__ __attribute__((aligned(16))) V sv[kM][kVC];      // values by source position
   __shared__ uint32_t roff[kMaxRuns + 1];                     // run offsets (never changed)
   __shared__ const uint64_t* pkey[kMaxRuns];                  // piece starts (keys)
@@ -403,8 +415,8 @@ __global__ __launch_bounds__(kNT) void nw_tile_kernel(NwBatch bt) {
     for (int x = 0; x < kPer; ++x) {
       const uint32_t e = e0 + x;
       if (e < E) {
-        sk[e] = kk[x];
-        si[e] = (uint16_t)e;
+        sk[SWK(e)] = kk[x];
+        si[SWI(e)] = (uint16_t)e;
 #pragma unroll
         for (int mi = 0; mi < M; ++mi) sv[mi][e] = vv[x][mi];
         // within the thread's run: the previous element from registers; at
@@ -416,7 +428,7 @@ __global__ __launch_bounds__(kNT) void nw_tile_kernel(NwBatch bt) {
       }
     }
     __syncthreads();
-    if (e0 < E && e0 > 0 && !(qs & 1u) && !(sk[e0 - 1] < kk[0])) ++viol;
+    if (e0 < E && e0 > 0 && !(qs & 1u) && !(sk[SWK(e0 - 1)] < kk[0])) ++viol;
   }
   NP_MARK(2);
   // ---- merge-path tree: round `width` merges runs [r0, r0 + width) and
@@ -430,8 +442,8 @@ __global__ __launch_bounds__(kNT) void nw_tile_kernel(NwBatch bt) {
   if (K <= 1) {  // one run: already in order
 #pragma unroll
     for (int x = 0; x < kPer; ++x) {
-      rk[x] = k0 + x < E ? sk[k0 + x] : 0ull;
-      ri[x] = k0 + x < E ? si[k0 + x] : (uint16_t)0;
+      rk[x] = k0 + x < E ? sk[SWK(k0 + x)] : 0ull;
+      ri[x] = k0 + x < E ? si[SWI(k0 + x)] : (uint16_t)0;
     }
   }
   for (uint32_t width = 1; width < K; width <<= 1) {
@@ -456,25 +468,25 @@ __global__ __launch_bounds__(kNT) void nw_tile_kernel(NwBatch bt) {
           uint32_t lo = d > lb ? d - lb : 0u, hi = d < la ? d : la;
           while (lo < hi) {  // A elements among the first d outputs
             const uint32_t mid = (lo + hi) >> 1;
-            if (sk[A0 + mid] <= sk[B0 + d - mid - 1]) lo = mid + 1;
+            if (sk[SWK(A0 + mid)] <= sk[SWK(B0 + d - mid - 1)]) lo = mid + 1;
             else hi = mid;
           }
           i = lo;
           j = d - lo;
-          ka = i < la ? sk[A0 + i] : 0ull;
-          kb = j < lb ? sk[B0 + j] : 0ull;
+          ka = i < la ? sk[SWK(A0 + i)] : 0ull;
+          kb = j < lb ? sk[SWK(B0 + j)] : 0ull;
         }
         // one LDS key read per output: the side taken advances
         const uint32_t la = B0 - A0, lb = B1 - B0;
         const bool takeA = j >= lb || (i < la && ka <= kb);
         rk[x] = takeA ? ka : kb;
-        ri[x] = si[takeA ? A0 + i : B0 + j];
+        ri[x] = si[SWI(takeA ? A0 + i : B0 + j)];
         if (takeA) {
           ++i;
-          ka = i < la ? sk[A0 + i] : 0ull;
+          ka = i < la ? sk[SWK(A0 + i)] : 0ull;
         } else {
           ++j;
-          kb = j < lb ? sk[B0 + j] : 0ull;
+          kb = j < lb ? sk[SWK(B0 + j)] : 0ull;
         }
       }
     }
@@ -482,8 +494,8 @@ __global__ __launch_bounds__(kNT) void nw_tile_kernel(NwBatch bt) {
 #pragma unroll
     for (int x = 0; x < kPer; ++x)
       if (k0 + x < E) {
-        sk[k0 + x] = rk[x];
-        si[k0 + x] = ri[x];
+        sk[SWK(k0 + x)] = rk[x];
+        si[SWI(k0 + x)] = ri[x];
       }
     __syncthreads();
   }
@@ -492,7 +504,7 @@ __global__ __launch_bounds__(kNT) void nw_tile_kernel(NwBatch bt) {
   // ---- run heads (a key differing from the previous one), unique index
   uint32_t heads = 0, nh = 0;
   {
-    const uint64_t before = k0 > 0 && k0 < E ? sk[k0 - 1] : 0ull;
+    const uint64_t before = k0 > 0 && k0 < E ? sk[SWK(k0 - 1)] : 0ull;
 #pragma unroll
     for (int x = 0; x < kPer; ++x) {
       const uint32_t e = k0 + x;
@@ -559,8 +571,8 @@ __global__ __launch_bounds__(kNT) void nw_tile_kernel(NwBatch bt) {
           }
         }
         uint32_t f = k0 + kPer;
-        while (open && f < E && sk[f] == key) {
-          const uint32_t src = si[f];
+        while (open && f < E && sk[SWK(f)] == key) {
+          const uint32_t src = si[SWI(f)];
 #pragma unroll
           for (int mi = 0; mi < M; ++mi) acc[mi] = src < p0 ? sv[mi][src] : acc[mi] + sv[mi][src];
           ++cnt;
