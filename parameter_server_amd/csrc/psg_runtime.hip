@@ -849,6 +849,24 @@ struct Filter {
 
 }  // namespace
 
+#ifndef PSG_SPIN
+#define PSG_SPIN 1
+#endif
+// the host waits for the end of a call's device work by polling its event:
+// a pushing caller is blocked on it anyway, and the poll sees completion
+// sooner than a blocking wait's wake-up (the e2e pinned path waits once per
+// push)
+static hipError_t spin_wait(hipEvent_t e) {
+#if PSG_SPIN
+  for (;;) {
+    const hipError_t q = hipEventQuery(e);
+    if (q != hipErrorNotReady) return q;
+  }
+#else
+  return hipEventSynchronize(e);
+#endif
+}
+
 struct psg_ctx {
   int device = 0;
   int dtype = PSG_F32;
@@ -856,6 +874,7 @@ struct psg_ctx {
   hipStream_t stream = nullptr;  // kernels, D2H
   hipStream_t copy = nullptr;    // H2D of pushes / keys / values
   hipEvent_t copy_ev = nullptr;
+  hipEvent_t done_ev = nullptr;  // end of a call's work on `stream` (spin_wait)
 
   std::mutex mu;
   std::unordered_map<int, Channel> ch;
@@ -1227,7 +1246,7 @@ struct psg_ctx {
     if (!pinned_wait) return PSG_OK;
     pinned_wait = false;
     HIP_TRY(hipEventRecord(copy_ev, copy));
-    HIP_TRY(hipEventSynchronize(copy_ev));
+    HIP_TRY(spin_wait(copy_ev));
     return PSG_OK;
   }
 
@@ -1597,6 +1616,7 @@ int psg_create(int device, int dtype, unsigned flags, psg_ctx** out) {
   hipError_t e = hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking);
   if (e == hipSuccess) e = hipStreamCreateWithFlags(&c->copy, hipStreamNonBlocking);
   if (e == hipSuccess) e = hipEventCreateWithFlags(&c->copy_ev, hipEventDisableTiming);
+  if (e == hipSuccess) e = hipEventCreateWithFlags(&c->done_ev, hipEventDisableTiming);
   if (e == hipSuccess) e = hipMalloc((void**)&c->d_small, 256);
   if (e == hipSuccess) e = hipMalloc((void**)&c->d_vio_slots, 64 * psg::kVioSlots);
   if (e == hipSuccess) e = hipMemsetAsync(c->d_vio_slots, 0, 64 * psg::kVioSlots, c->stream);
@@ -1645,6 +1665,7 @@ int psg_destroy(psg_ctx* c) {
   if (c->h_small) (void)hipHostFree(c->h_small);
   (void)hipFree(c->scratch);
   if (c->copy_ev) (void)hipEventDestroy(c->copy_ev);
+  if (c->done_ev) (void)hipEventDestroy(c->done_ev);
   if (c->copy) (void)hipStreamDestroy(c->copy);
   if (c->stream) (void)hipStreamDestroy(c->stream);
   delete c;
@@ -2329,7 +2350,8 @@ int psg_received(psg_ctx* c, int time, int m, void* const* out) {
   unsigned long long corrupt = 0, badsig = 0;
   if (rc == PSG_OK && !(direct && pend)) rc = c->d2h(c->h_small, A.d_bad, kBadBytes);
   if (rc == PSG_OK) {
-    hipError_t e = hipStreamSynchronize(c->stream);
+    hipError_t e = hipEventRecord(c->done_ev, c->stream);
+    if (e == hipSuccess) e = spin_wait(c->done_ev);
     if (e != hipSuccess) rc = fail(PSG_ERR_DEVICE, "received: %s", hipGetErrorString(e));
     bad = c->h_small[0];
     corrupt = c->h_small[1];
