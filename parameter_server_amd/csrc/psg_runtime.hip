@@ -446,7 +446,11 @@ struct JobTable {
       else (void)hipGetLastError();
     }
     char* img = himg[ib];
-    memset(img, 0, off);
+    // only the region the kernels expect zeroed (fail counters, cursor
+    // boundary words): every other field of the image is written below, or
+    // (seg, splitters, bucket index) by a kernel before any read.  Zeroing
+    // the whole image cost ~0.1 ms per flush of a 16.8 M-slot aggregate
+    memset(img + zero_off, 0, zero_end - zero_off);
     psg::TileDesc* htiles = (psg::TileDesc*)(img + tiles_off);
     uint32_t* hsitems = (uint32_t*)(img + sitems_off);
     uint64_t* hitems = (uint64_t*)(img + items_off);
