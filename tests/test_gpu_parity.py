@@ -357,6 +357,42 @@ def test_gather_tile_forms(torch_cuda):
     assert_bitexact(m.value[0], want)
 
 
+def test_flush_job_tables_reused_across_shapes(torch_cuda):
+    """One context, received() after received() over shapes that repeat and
+    change: the flush reuses its device tile descriptors and work items only
+    when the shape repeats (range, push count, partition mode, the stream
+    mode's push lengths, the continued-sum flag of a split flush); every
+    result bit-exact against the oracle."""
+    rng = np.random.default_rng(77)
+    D = np.unique(rng.integers(1, 1 << 44, 60000, dtype=np.uint64))
+    v = kvv(np.float32)
+    v.setValue(msg(D))
+
+    def dense_pushes(lo, hi, npush, frac):
+        out = []
+        for _ in range(npush):
+            k = np.sort(rng.choice(D[lo:hi], int((hi - lo) * frac), replace=False))
+            out.append((k, [rng.standard_normal(k.size).astype(np.float32)]))
+        return out
+
+    shapes = [(0, 60000, 8, 0.5), (0, 60000, 8, 0.5), (1000, 41000, 3, 0.7),
+              (0, 60000, 8, 0.5), (0, 60000, 40, 0.002), (0, 60000, 40, 0.002),
+              (0, 60000, 40, 0.003), (1000, 41000, 3, 0.7)]
+    t = 3
+    for i, (lo, hi, npush, frac) in enumerate(shapes):
+        kb, ke = int(D[lo]), int(D[hi]) if hi < D.size else (1 << 64) - 1
+        pushes = dense_pushes(lo, hi, npush, frac)
+        v.set_flush_pushes(3 if i == 3 else 4096)  # one split flush: continued sums
+        for k, vals in pushes:
+            v.setValue(msg(k, vals, t=t, rng=(kb, ke)))
+        (r, a), = v.received(t)
+        rc, lo2, hi2, (want,), _ = O.aggregate(D, kb, ke, pushes)
+        assert rc == 0 and tuple(r) == (lo2, hi2) == (lo, hi)
+        assert_bitexact(a, want)
+        t += 1
+    v.close()
+
+
 # ------------------------------------------- device-resident plans (bench path)
 def to_dev(torch, a):
     a = np.ascontiguousarray(a)
