@@ -110,6 +110,7 @@ struct NwBatch {
   const uint64_t* tpre;     // [nm + 1] tiles before merge j
   unsigned int* ticket;     // tile tickets
   uint32_t nm;
+  uint32_t rr;              // tickets round-robin over the merges (1) or merge by merge (0)
 };
 
 // merge j of item x: the last j with pre[j] <= x (pre non-decreasing)
@@ -330,9 +331,22 @@ __global__ __launch_bounds__(kNT) void nw_tile_kernel(NwBatch bt) {
   }
   __syncthreads();
   const uint32_t g = uni(sh_t);
-  const uint32_t jm = uni(merge_of(bt.tpre, bt.nm, g));
+  // round robin (batches): ticket g is tile g / nm of merge g mod nm, so the
+  // tiles in flight spread over every merge and a tile's predecessor in its
+  // merge started nm tickets earlier -- its look-back finds an inclusive
+  // prefix at once instead of waiting down a chain of running neighbours
+  // (r05: profiles/r05_ab_nway.txt).  A ticket past a merge's last tile
+  // (merges of fewer tiles) is idle.
+  uint32_t jm, t;
+  if (bt.rr) {
+    jm = g % bt.nm;
+    t = g / bt.nm;
+  } else {
+    jm = uni(merge_of(bt.tpre, bt.nm, g));
+    t = (uint32_t)(g - bt.tpre[jm]);
+  }
   const NwArgs& a = bt.args[jm];
-  const uint32_t t = (uint32_t)(g - bt.tpre[jm]);
+  if (t >= a.T) return;
   const uint32_t K = a.K;
   const bool parallel = (a.flags & kFlagParallel) != 0;
 
@@ -725,6 +739,7 @@ struct NwLayout {
   std::vector<Off> off;
   size_t o_args = 0, o_pre = 0, o_zero = 0, o_ticket = 0, o_misc = 0, zero_len = 0, bytes = 0;
   uint64_t nwaves = 0, ncand = 0, nseg = 0, ntiles = 0;
+  uint64_t maxT = 0;  // the most tiles of one merge (round-robin tickets: maxT * nm)
   uint32_t rk_per = 16;  // rank-stage candidates per thread (16, 4 or 1)
 
   // pn: the merges' push lengths back to back, npush[j] per merge
@@ -764,7 +779,7 @@ struct NwLayout {
       o = al256(o + 8 * sh[j].ncand);
     }
     bytes = o;
-    nwaves = ncand = nseg = ntiles = 0;
+    nwaves = ncand = nseg = ntiles = maxT = 0;
     // the fewest candidates per thread that still gives >= 512 rank workgroups
     uint64_t w16 = 0, w4 = 0;
     for (const NwShape& x : sh) {
@@ -777,8 +792,14 @@ struct NwLayout {
       ncand += x.ncand;
       nseg += (uint64_t)(x.T + 1) * x.K;
       ntiles += x.T;
+      maxT = std::max<uint64_t>(maxT, x.T);
     }
   }
+#ifndef PSG_NW_RR
+#define PSG_NW_RR 1
+#endif
+  bool rr() const { return PSG_NW_RR && nm > 1; }
+  uint64_t tickets() const { return rr() ? maxT * nm : ntiles; }
 
   unsigned long long* misc(char* b, uint32_t j) const {
     return (unsigned long long*)(b + o_misc) + 2 * (size_t)j;
@@ -794,6 +815,7 @@ struct NwLayout {
     B.tpre = pre + 3 * (size_t)(nm + 1);
     B.ticket = (unsigned int*)(b + o_ticket);
     B.nm = nm;
+    B.rr = rr() ? 1u : 0u;
     return B;
   }
 
@@ -874,8 +896,8 @@ hipError_t nway_enqueue(char* b, const NwLayout& L, int dtype, hipStream_t st) {
     hipLaunchKernelGGL(nw_seg_kernel, dim3((uint32_t)((L.nseg + 255) / 256)), dim3(256), 0, st, B,
                        L.nseg);
   if ((e = hipGetLastError()) != hipSuccess) return e;
-  return dtype == PSG_F32 ? launch_tile_m<float>(L.m, B, L.ntiles, st)
-                          : launch_tile_m<double>(L.m, B, L.ntiles, st);
+  return dtype == PSG_F32 ? launch_tile_m<float>(L.m, B, L.tickets(), st)
+                          : launch_tile_m<double>(L.m, B, L.tickets(), st);
 }
 
 // One keys-only union on `st` into out_keys (>= sum(n) entries), scratch
