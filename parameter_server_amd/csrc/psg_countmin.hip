@@ -253,14 +253,28 @@ __global__ __launch_bounds__(kBlkNT) void cm_iapply_kernel(uint8_t* __restrict__
     __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
     __builtin_amdgcn_wave_barrier();
     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-    for (uint32_t i = lane; i < tot; i += 64u) {
-      uint32_t u = 0;
+    // kApU records per lane in flight: their loads issued together, then
+    // their adds (one record at a time waited ~a memory trip per 64)
+    constexpr int kApU = 8;
+    for (uint32_t i0 = lane; i0 < tot; i0 += 64u * kApU) {
+      uint32_t v[kApU];
 #pragma unroll
-      for (uint32_t st = 32; st > 0; st >>= 1)
-        if (wpre[w][u + st] <= i) u += st;
-      const uint32_t v = R[wst[w][u] + (i - wpre[w][u])];
-      __hip_atomic_fetch_add(&acc[v & (kRegBytes - 1u)], v >> kRegShift, __ATOMIC_RELAXED,
-                             __HIP_MEMORY_SCOPE_WORKGROUP);
+      for (int q = 0; q < kApU; ++q) {
+        const uint32_t i = i0 + 64u * q;
+        v[q] = 0xffffffffu;
+        if (i < tot) {
+          uint32_t u = 0;
+#pragma unroll
+          for (uint32_t st = 32; st > 0; st >>= 1)
+            if (wpre[w][u + st] <= i) u += st;
+          v[q] = R[wst[w][u] + (i - wpre[w][u])];
+        }
+      }
+#pragma unroll
+      for (int q = 0; q < kApU; ++q)
+        if (i0 + 64u * q < tot)
+          __hip_atomic_fetch_add(&acc[v[q] & (kRegBytes - 1u)], v[q] >> kRegShift,
+                                 __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
     }
     __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
     __builtin_amdgcn_wave_barrier();
