@@ -544,12 +544,13 @@ __global__ __launch_bounds__(kQNT) void cm_qlook_kernel(const uint8_t* __restric
   const uint8_t* tab8 = (const uint8_t*)tab;
   const uint32_t rb = kb * (uint32_t)k;
   // one block's run per wave step (about k * KB / nreg records): lanes over
-  // the run; four runs' loads issued before their lookups
-  for (uint32_t b0 = w * 4u; b0 < nb; b0 += (kQNT / 64) * 4u) {
-    uint32_t rec[4], at[4];
-    bool have[4];
+  // the run; kQLU runs' loads issued before their lookups
+  constexpr int kQLU = 8;
+  for (uint32_t b0 = w * (uint32_t)kQLU; b0 < nb; b0 += (kQNT / 64) * (uint32_t)kQLU) {
+    uint32_t rec[kQLU], at[kQLU];
+    bool have[kQLU];
 #pragma unroll
-    for (int u = 0; u < 4; ++u) {
+    for (int u = 0; u < kQLU; ++u) {
       const uint32_t b = b0 + (uint32_t)u;
       const uint32_t sg = b < nb ? seg[b] : 0u;
       const uint32_t len = sg >> 16;
@@ -558,7 +559,7 @@ __global__ __launch_bounds__(kQNT) void cm_qlook_kernel(const uint8_t* __restric
       rec[u] = have[u] ? R1[at[u]] : 0u;
     }
 #pragma unroll
-    for (int u = 0; u < 4; ++u) {
+    for (int u = 0; u < kQLU; ++u) {
       if (have[u]) {
         const uint32_t v = tab8[rec[u] & (kQRegBytes - 1u)];
         R2[at[u]] = (uint16_t)((rec[u] >> kQRegShift) | ((int)v <= freq ? 0x8000u : 0u));
@@ -566,7 +567,7 @@ __global__ __launch_bounds__(kQNT) void cm_qlook_kernel(const uint8_t* __restric
     }
     // runs longer than a wave (rare: about 64 records per run at k = 4)
 #pragma unroll
-    for (int u = 0; u < 4; ++u) {
+    for (int u = 0; u < kQLU; ++u) {
       const uint32_t b = b0 + (uint32_t)u;
       const uint32_t sg = b < nb ? seg[b] : 0u;
       const uint32_t len = sg >> 16;
@@ -598,9 +599,14 @@ __global__ __launch_bounds__(kQNT) void cm_qkeep_kernel(uint64_t nk, uint32_t kb
   __syncthreads();
   const uint32_t nrec = S[(size_t)b * (nreg + 1) + nreg];
   const uint16_t* in = R2 + (size_t)b * kb * (uint32_t)k;
-  for (uint32_t i = t; i < nrec; i += kQNT) {
-    const uint32_t v = in[i];
-    if (v & 0x8000u) atomicOr(&drop[(v & 0x1fffu) >> 5], 1u << (v & 31u));
+  constexpr int kKU = 8;  // results per thread in flight
+  for (uint32_t i0 = t; i0 < nrec; i0 += kQNT * kKU) {
+    uint32_t v[kKU];
+#pragma unroll
+    for (int q = 0; q < kKU; ++q) v[q] = i0 + kQNT * q < nrec ? in[i0 + kQNT * q] : 0u;
+#pragma unroll
+    for (int q = 0; q < kKU; ++q)
+      if (v[q] & 0x8000u) atomicOr(&drop[(v[q] & 0x1fffu) >> 5], 1u << (v[q] & 31u));
   }
   __syncthreads();
   // tile tt of the block, keep byte j (keys tt*kQTile + 8j .. +8)
