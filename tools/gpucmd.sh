@@ -2,12 +2,13 @@
 set -o pipefail
 export TMPDIR=/tmp
 O=gpurun_out/r05g; mkdir -p $O
-timeout -k 10 600 python3 -u -m pytest tests -m gpu -x -q --timeout 300 --timeout-method thread > $O/tests.log 2>&1 || { echo TESTS FAILED; tail -30 $O/tests.log; exit 1; }
-tail -2 $O/tests.log
-for rep in 1 2; do for v in sp0 sp1; do
-  PSG_LIB_PATH=$PWD/build/$v/libpsg.so timeout -k 10 300 python3 tools/shard_probe.py 30 > $O/sh_$v.txt 2> $O/sh_$v.err || { echo FAIL $v; tail -5 $O/sh_$v.err; exit 1; }
-  echo "$rep $v $(cat $O/sh_$v.txt)"
+R=$GRAFT_REPO_ROOT
+PSG_LIB_PATH=$R/build/c1/libpsg.so timeout -k 10 300 python3 -u -m pytest tests/test_freq_filter.py -m gpu -x -q --timeout 120 --timeout-method thread > $O/tests_c1.log 2>&1 || { echo TESTS FAILED; tail -30 $O/tests_c1.log; exit 1; }
+echo "c1 $(tail -1 $O/tests_c1.log)"
+for rep in 1 2; do for v in c0 c1; do
+  PSG_LIB_PATH=$R/build/$v/libpsg.so timeout -k 10 300 python3 tools/run_rows.py countmin > $O/rows_$v.json 2> $O/rows_$v.err || { echo FAIL $v; tail -5 $O/rows_$v.err; exit 1; }
+  echo "$rep $v $(python3 -c "import json;d=json.load(open('$O/rows_$v.json'));print(d['countmin_insert']['ms'], d['countmin_query']['ms'])")"
 done; done
-bash tools/ab_run.sh "sp0 sp1" "cfg5" > $O/ab_split.txt 2>&1 || { echo AB FAILED; tail -5 $O/ab_split.txt; exit 1; }
-cat $O/ab_split.txt
+cd /tmp && PSG_LIB_PATH=$R/build/c1/libpsg.so timeout -k 10 120 rocprofv3 --kernel-trace --stats --output-format csv -d $R/$O/kt_c1 -o run -- python3 $R/tools/run_rows.py countmin > $R/$O/kt_c1.log 2>&1 || { echo KT FAIL; exit 1; }
+cd $R; grep -i "cm_" $O/kt_c1/run_kernel_stats.csv | cut -d, -f1-4
 echo done
