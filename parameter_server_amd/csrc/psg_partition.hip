@@ -70,9 +70,11 @@ __device__ __forceinline__ void search_item(const JobDev& J, uint32_t p, uint32_
   const uint64_t n = J.pn[p];
   const uint32_t bc = valid ? b : J.ntiles;
   const bool up = bc == J.ntiles;
-  const uint64_t x = up ? J.dkeys[J.nslots - 1] : J.dkeys[(uint64_t)bc * J.tile];
-  // upper_bound(x) == lower_bound(x + 1): D never holds 2^64-1
-  const uint64_t xl = up ? x + 1ull : x;
+  // boundary key: lower_bound(D[bc * tile]); past the last tile
+  // upper_bound(D[nslots - 1]) == lower_bound(D[nslots - 1] + 1) (D never
+  // holds 2^64-1) -- exactly the splitter array a plan writes once
+  const uint64_t xl = J.split ? J.split[bc]
+                      : up ? J.dkeys[J.nslots - 1] + 1ull : J.dkeys[(uint64_t)bc * J.tile];
   const uint64_t k0 = S[0], kn = S[n - 1];
   // the wave's last valid lane (invalid lanes repeat boundary ntiles)
   const int last = (int)((J.ntiles - (g << 6)) < 63u ? (J.ntiles - (g << 6)) : 63u);

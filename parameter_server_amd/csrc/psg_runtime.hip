@@ -317,6 +317,10 @@ struct JobTable {
       if (I.ntiles && I.np && !s.dense) {  // dense: seg filled here, nothing to search
         if (d.mode == psg::kSearch) {
           items += (uint64_t)((I.ntiles + 64) / 64) * I.np;
+          if (index) {  // plans: the boundary keys as a splitter array, written once
+            d.split_begin = (uint32_t)sitems;
+            sitems += (std::max<uint64_t>(I.ntiles + 1, I.np) + 255) / 256;
+          }
         } else {
           d.split_begin = (uint32_t)sitems;
           sitems += (std::max<uint64_t>(I.ntiles + 1, I.np) + 255) / 256;
@@ -426,7 +430,8 @@ struct JobTable {
       o.fail = fail_cur; fail_cur += 8 * np;
       o.seg = off; off = align_up(off + 4 * (nt + 1) * np, 256);
       o.split = off;
-      if (h[j].mode == psg::kStream) off = align_up(off + 8 * (nt + 1), 256);
+      const bool has_split = h[j].mode == psg::kStream || (index && !jobs[j].dense && nt && np);
+      if (has_split) off = align_up(off + 8 * (nt + 1), 256);
       o.dpos = off;
       if (jobs[j].dense) off = align_up(off + 8 * np, 256);
     }
@@ -516,12 +521,20 @@ struct JobTable {
       d.pn = (const uint64_t*)(base + o.pn);
       d.seg = (uint32_t*)(base + o.seg);
       d.fail = (unsigned long long*)(base + o.fail);
-      d.split = d.mode == psg::kStream ? (uint64_t*)(base + o.split) : nullptr;
+      // search-mode jobs of plans read their boundary keys from the splitter
+      // array (64 consecutive boundaries: one coalesced read per wave instead
+      // of one line of D per boundary)
+      const bool has_split = d.mode == psg::kStream || (index && !s.dense && nt && np);
+      d.split = has_split ? (uint64_t*)(base + o.split) : nullptr;
       I.seg = d.seg;
       I.fail = d.fail;
       if (same) continue;  // descriptors and items already on the device
       if (nt && np && !s.dense) {  // as counted above: dense jobs have no items
         if (d.mode == psg::kSearch) {
+          if (index) {
+            const uint64_t ns = (std::max<uint64_t>(nt + 1, np) + 255) / 256;
+            for (uint64_t b = 0; b < ns; ++b) hsitems[scur++] = (uint32_t)j;
+          }
           const uint64_t ng = (nt + 64) / 64;
           for (uint64_t g = 0; g < ng; ++g)  // group-major: a boundary group's pushes adjacent
             for (uint32_t p = 0; p < np; ++p)
