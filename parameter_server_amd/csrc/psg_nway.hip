@@ -166,9 +166,12 @@ __global__ __launch_bounds__(256) void nw_rank_kernel(NwBatch b) {
   const uint32_t t = threadIdx.x;
   uint64_t mine[kRkPer];
   uint32_t acc[kRkPer];
+  // thread t holds kRkPer consecutive candidates (sorted while they lie in
+  // one push's run): a list is then searched once per thread and walked for
+  // the rest, not searched kRkPer times (r05: profiles/r05_ab_nway.txt)
 #pragma unroll
   for (uint32_t i = 0; i < kRkPer; ++i) {
-    const uint64_t c = c0 + t + 256u * i;
+    const uint64_t c = c0 + kRkPer * t + i;
     mine[i] = c < a.ncand ? G(a.candk)[c] : ~0ull;
     acc[i] = 0;
   }
@@ -181,18 +184,30 @@ __global__ __launch_bounds__(256) void nw_rank_kernel(NwBatch b) {
       __syncthreads();  // the previous list's searches are done
       for (uint32_t x = t; x < L; x += 256) lst[x] = G(a.candk)[q0 + x];
       __syncthreads();
+      uint32_t pos = 0;  // lower_bound(lst[0, L), mine[i - 1])
 #pragma unroll
       for (uint32_t i = 0; i < kRkPer; ++i) {
-        uint32_t lo = 0, n = L;  // lower_bound(lst[0, L), mine[i])
+        const uint64_t k = mine[i];
+        // from the previous candidate's position when k does not go back
+        // (same push run): a few steps forward, else a bisection of the rest
+        uint32_t lo = (i > 0 && k >= mine[i - 1]) ? pos : 0u;
+#pragma unroll
+        for (int st = 0; st < 2; ++st) lo += (lo < L && lst[lo] < k) ? 1u : 0u;
+        uint32_t n = lo < L && lst[lo] < k ? L - lo : 0u;
+        if (i == 0 || k < mine[i - 1]) {  // a new run (or the first): the whole list
+          lo = 0;
+          n = L;
+        }
         while (n > 0) {
           const uint32_t h = n >> 1;
-          if (lst[lo + h] < mine[i]) {
+          if (lst[lo + h] < k) {
             lo += h + 1;
             n -= h + 1;
           } else {
             n = h;
           }
         }
+        pos = lo;
         acc[i] += lo;
       }
     } else {
@@ -203,7 +218,7 @@ __global__ __launch_bounds__(256) void nw_rank_kernel(NwBatch b) {
   }
 #pragma unroll
   for (uint32_t i = 0; i < kRkPer; ++i) {
-    const uint64_t c = c0 + t + 256u * i;
+    const uint64_t c = c0 + kRkPer * t + i;
     if (c < a.ncand) GW(a.rank)[c] = a.s * acc[i];
   }
 }
