@@ -92,12 +92,16 @@ static_assert(ts_of(64) <= 0x7ffe, "u16 positions");
 
 typedef unsigned long long u64x2 __attribute__((ext_vector_type(2)));
 typedef uint32_t u32x2 __attribute__((ext_vector_type(2)));
+typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
 
 __device__ __forceinline__ uint32_t uni(uint32_t v) { return __builtin_amdgcn_readfirstlane(v); }
 __device__ __forceinline__ uint64_t uni64(uint64_t v) {
   return ((uint64_t)uni((uint32_t)(v >> 32)) << 32) | uni((uint32_t)v);
 }
 
+#ifndef PSG_FUSECNT
+#define PSG_FUSECNT 1  // A/B builds: 0 = sums and contributor counts in separate arrays
+#endif
 #ifndef PSG_DDMA
 #define PSG_DDMA 1  // A/B builds: 0 = D and the resident bucket table through registers
 #endif
@@ -189,7 +193,12 @@ __global__ __launch_bounds__(nt_of(kGroup), (occupancy<V, M, kGroup>())) void ti
   // bucket starts (u16); the histogram counts in it as packed pairs by 32-bit atomics
   __shared__ __attribute__((aligned(16))) uint32_t bt32[(kNB + 8) / 2];
   uint16_t* const bt = (uint16_t*)bt32;
-  __shared__ __attribute__((aligned(16))) V acc[M][kTS];
+  // 1024-slot single-value f32 form: the sum and the contributor count of a
+  // slot interleaved in one 8-B word (cnt32[2s], cnt32[2s + 1]), so the fold
+  // updates both with one 8-B read and one 8-B write and the order check
+  // issues no LDS atomic
+  constexpr bool kFuse = PSG_FUSECNT && kGroup == 32 && M == 1 && sizeof(V) == 4;
+  __shared__ __attribute__((aligned(16))) V acc[kFuse ? 1 : M][kFuse ? 1 : kTS];
   // serial mode: pushes holding the slot (u16 pairs, counted by non-returning
   // LDS adds during the search, off the fold's dependency chain): the fold
   // adds the "+0.0" of absent pushes as ONE trailing +0.0 when the count is
@@ -197,7 +206,8 @@ __global__ __launch_bounds__(nt_of(kGroup), (occupancy<V, M, kGroup>())) void ti
   // 1024-slot form: one u32 per slot (the add is a constant 1); the
   // 2048-slot form keeps u16 pairs (LDS: 4 workgroups per CU)
   constexpr bool kCntW = kGroup == 32;
-  __shared__ __attribute__((aligned(16))) uint32_t cnt32[kCntW ? kTS : kTS / 2];
+  __shared__ __attribute__((aligned(16))) uint32_t cnt32[kFuse ? 2 * kTS : kCntW ? kTS : kTS / 2];
+#define ACC(mi, s) (*(kFuse ? (V*)&cnt32[2u * (s)] : &acc[mi][s]))
   __shared__ uint32_t rpre[kGroup + 1];             // rounds before push q of the group
   __shared__ uint32_t pln[kGroup];                  // piece length
   __shared__ uint64_t pkp[kGroup], pvp[kGroup * M];  // piece starts (keys, values)
@@ -326,18 +336,26 @@ __global__ __launch_bounds__(nt_of(kGroup), (occupancy<V, M, kGroup>())) void ti
       for (int j = 0; j < 4; ++j)
         a0[mi][j] = s0 + j < nt ? G((const V*)T.out[mi] + T.slot0)[s0 + j] : V(0);
     __builtin_amdgcn_s_waitcnt(0x0f70);  // vmcnt(0), on this branch only (see above)
+    if constexpr (kFuse) {
+      *(u32x4*)&cnt32[8 * tid] = u32x4{__float_as_uint(a0[0][0]), 0u, __float_as_uint(a0[0][1]), 0u};
+      *(u32x4*)&cnt32[8 * tid + 4] = u32x4{__float_as_uint(a0[0][2]), 0u, __float_as_uint(a0[0][3]), 0u};
+    } else {
 #pragma unroll
-    for (int mi = 0; mi < M; ++mi)
+      for (int mi = 0; mi < M; ++mi)
 #pragma unroll
-      for (int j = 0; j < 4; ++j) acc[mi][s0 + j] = a0[mi][j];
+        for (int j = 0; j < 4; ++j) acc[mi][s0 + j] = a0[mi][j];
+    }
+  } else if constexpr (kFuse) {
+    *(u32x4*)&cnt32[8 * tid] = u32x4{0u, 0u, 0u, 0u};
+    *(u32x4*)&cnt32[8 * tid + 4] = u32x4{0u, 0u, 0u, 0u};
   } else {
 #pragma unroll
     for (int mi = 0; mi < M; ++mi)
 #pragma unroll
       for (int j = 0; j < 4; ++j) acc[mi][s0 + j] = V(0);
   }
-  if constexpr (kCntW) {
-    typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
+  if constexpr (kFuse) {
+  } else if constexpr (kCntW) {
     *(u32x4*)&cnt32[4 * tid] = u32x4{0u, 0u, 0u, 0u};
   } else {
     cnt32[2 * tid] = 0u;
@@ -513,7 +531,7 @@ __global__ __launch_bounds__(nt_of(kGroup), (occupancy<V, M, kGroup>())) void ti
 #pragma unroll
       for (int r = 0; r < kCap; ++r)
         if ((uint32_t)r < nrw && ((hv >> r) & 1u)) t += ev[r][0] + (V)(uint32_t)(ek[r] & 1u);
-      acc[0][s0] += t;
+      ACC(0, s0) += t;
       done += kNW * Rw;
       if (done < U) {
         load_pass();
@@ -593,7 +611,7 @@ __global__ __launch_bounds__(nt_of(kGroup), (occupancy<V, M, kGroup>())) void ti
 #pragma unroll
       for (int r = 0; r < kCap; ++r)
         if ((uint32_t)r < nrw && ((fd >> r) & 1u)) t += ev[r][0] + (V)pos[r];
-      acc[0][s0] += t;
+      ACC(0, s0) += t;
       done += kNW * Rw;
       if (done < U) {
         load_pass();
@@ -619,7 +637,7 @@ __global__ __launch_bounds__(nt_of(kGroup), (occupancy<V, M, kGroup>())) void ti
         const bool ok = ((hv & fd) >> r & 1u) && (int)pos[r] > prev;
 #endif
         okb |= (uint32_t)ok << r;
-        if (!parallel && ok)
+        if (!kFuse && !parallel && ok)
           __hip_atomic_fetch_add(kCntW ? &cnt32[pos[r]] : &cnt32[pos[r] >> 1],
                                  kCntW ? 1u : 1u << (16u * (pos[r] & 1u)),
                                  __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
@@ -656,8 +674,15 @@ __global__ __launch_bounds__(nt_of(kGroup), (occupancy<V, M, kGroup>())) void ti
             const uint32_t q = re[r] >> kCB;
             const uint32_t s = pos[r];
             const bool first = g0 + q == 0u && !cont;
+            if constexpr (kFuse) {
+              u32x2* const p = (u32x2*)&cnt32[2u * s];
+              const u32x2 x = *p;
+              const V sum = first ? ev[r][0] : __uint_as_float(x.x) + ev[r][0];
+              *p = u32x2{__float_as_uint(sum), x.y + 1u};
+            } else {
 #pragma unroll
-            for (int mi = 0; mi < M; ++mi) acc[mi][s] = first ? ev[r][mi] : acc[mi][s] + ev[r][mi];
+              for (int mi = 0; mi < M; ++mi) acc[mi][s] = first ? ev[r][mi] : acc[mi][s] + ev[r][mi];
+            }
           }
         }
         if (w == wl && lane == 63) pcarry = mylast;
@@ -686,11 +711,13 @@ __global__ __launch_bounds__(nt_of(kGroup), (occupancy<V, M, kGroup>())) void ti
   V res[M][4];
 #pragma unroll
   for (int j = 0; j < 4; ++j) {
-    const uint32_t ncontrib = kCntW ? cnt32[s0 + j] : (uint32_t)((const uint16_t*)cnt32)[s0 + j];
+    const uint32_t ncontrib = kFuse   ? cnt32[2u * (s0 + j) + 1u]
+                              : kCntW ? cnt32[s0 + j]
+                                      : (uint32_t)((const uint16_t*)cnt32)[s0 + j];
     const bool gap = !parallel && ncontrib != np;
 #pragma unroll
     for (int mi = 0; mi < M; ++mi) {
-      const V a = acc[mi][s0 + j];
+      const V a = ACC(mi, s0 + j);
       res[mi][j] = gap ? a + V(0) : a;
     }
   }
