@@ -152,18 +152,27 @@ struct Raw {
   uint64_t n, kp, vp, out0;
 };
 // A tile's plan: per lane q < np the piece (first key / value address,
-// length, unit prefixes of its key and value segments in the stage, round
-// end); per tile the scalars the DMA, compute and store steps need.
+// length) and the prefixes that place it in a stage; per tile the scalars
+// the DMA, compute and store steps need.  The pieces are staged in groups of
+// consecutive pushes whose units fit the stage: one group for every tile of
+// the bench shapes (cfg2 uses ~60 % of a stage); a tile of more piece bytes
+// stages its later groups itself, synchronously (rare, slower, same result).
 struct Plan {
   uint64_t ks, vs;    // per lane: global addresses of the piece's first key / value
   uint32_t len;       // per lane: piece length
-  uint32_t pk, pv;    // per lane: first stage unit (from the piece base) of its keys / values
+  uint32_t kx, vx;    // per lane: exclusive prefixes of key units / value units (totals past np)
+  uint32_t ci;        // per lane: inclusive prefix of key + value units
   uint32_t rend;      // per lane: inclusive prefix of rounds (~0 past np)
   uint64_t dg, bg;    // D of the tile, its resident bucket index (0: built here)
   float* out;         // the tile's first output slot
   uint32_t nt, np, par;  // slots, pushes, parallel match
-  uint32_t npu, nr;   // piece units, rounds
-  uint32_t ovf;       // pieces exceed the stage: read them from global memory
+  uint32_t nr;        // rounds
+};
+// One group's placement in the stage: pushes [q0, q1), per lane q in it the
+// first unit (from the piece base) of its keys and of its values.
+struct Layout {
+  uint32_t q0, q1, npu;
+  uint32_t pk, pv;
 };
 
 __device__ __forceinline__ uint32_t load_desc(const TileDesc* tiles, uint32_t t, uint32_t t_end,
@@ -199,11 +208,11 @@ __device__ __forceinline__ Plan make_plan(uint32_t d, const Raw& r, bool valid, 
                                           bool count) {
   Plan p;
   p.ks = p.vs = 0;
-  p.len = p.pk = p.pv = 0;
+  p.len = p.kx = p.vx = p.ci = 0;
   p.rend = 0xffffffffu;
   p.dg = p.bg = 0;
   p.out = nullptr;
-  p.nt = p.np = p.par = p.npu = p.nr = p.ovf = 0;
+  p.nt = p.np = p.par = p.nr = 0;
   if (!valid) return p;
   p.nt = DF32(d, nt);
   p.np = DF32(d, np);
@@ -233,28 +242,43 @@ __device__ __forceinline__ Plan make_plan(uint32_t d, const Raw& r, bool valid, 
     nr = (len + 63u) >> 6;
   }
   const uint32_t ki = wave_scan_incl(ku), vi = wave_scan_incl(vu), ri = wave_scan_incl(nr);
-  const uint32_t KU = rl(ki, 63), VU = rl(vi, 63);
-  p.pk = ki - ku;
-  p.pv = KU + vi - vu;
-  p.npu = KU + VU;
+  p.kx = ki - ku;
+  p.vx = vi - vu;
+  p.ci = ki + vi;
   p.nr = rl(ri, 63);
   p.rend = (uint32_t)lane < p.np ? ri : 0xffffffffu;
-  p.ovf = p.npu > (uint32_t)kPC ? 1u : 0u;
   return p;
 }
 
+// The group of pushes starting at q0: the longest run whose units fit the
+// stage (a piece is at most 513 + 257 units, so every group holds a push)
+__device__ __forceinline__ Layout layout(const Plan& p, uint32_t q0, int lane) {
+  Layout g;
+  g.q0 = q0;
+  const uint32_t base = q0 ? rl(p.ci, q0 - 1u) : 0u;
+  const bool in = (uint32_t)lane >= q0 && (uint32_t)lane < p.np && p.ci - base <= (uint32_t)kPC;
+  g.q1 = q0 + (uint32_t)__popcll(__ballot(in));
+  const uint32_t k0 = rl(p.kx, q0), v0 = rl(p.vx, q0);
+  const uint32_t KU = rl(p.kx, g.q1) - k0, VU = rl(p.vx, g.q1) - v0;
+  g.pk = p.kx - k0;
+  g.pv = KU + p.vx - v0;
+  g.npu = KU + VU;
+  return g;
+}
 
-// This wave's share of plan p's DMA into stage S: instructions g = w, w + 4,
-// ... over [D units][bucket index units][piece units], 64 units each.  D and
-// the index are read by this tile only (nontemporal); the pieces' edge lines
-// are shared with the neighbouring tiles of the run (default policy).
-__device__ __forceinline__ void issue_dma(const Plan& p, uint8_t* S, uint32_t w, int lane) {
+// This wave's share of the DMA of a group's pieces into stage S (and, with
+// `head`, of the tile's D and bucket index first): instructions g = w, w+4,
+// ... over [D units][index units][piece units], 64 units each.  D and the
+// index are read by this tile only (nontemporal); the pieces' edge lines are
+// shared with the neighbouring tiles of the run (default policy).
+__device__ __forceinline__ void issue_dma(const Plan& p, const Layout& L, uint8_t* S, uint32_t w,
+                                          int lane, bool head) {
   const uint64_t dga = p.dg & ~15ull;
-  const uint32_t nud = (uint32_t)(((p.dg + 8ull * p.nt + 15ull) >> 4) - (p.dg >> 4));
+  const uint32_t nud = head ? (uint32_t)(((p.dg + 8ull * p.nt + 15ull) >> 4) - (p.dg >> 4)) : 0u;
   const uint32_t iD = (nud + 63u) >> 6;
-  const uint32_t iB = p.bg ? 2u : 0u;
-  const uint32_t iP = p.ovf ? 0u : (p.npu + 63u) >> 6;
-  const uint32_t nI = iD + iB + iP, np = p.np;
+  const uint32_t iB = head && p.bg ? 2u : 0u;
+  const uint32_t iP = (L.npu + 63u) >> 6;
+  const uint32_t nI = iD + iB + iP, q0 = L.q0, nq = L.q1 - L.q0;
   for (uint32_t g = w; g < nI; g += kNW) {
     if (g < iD) {
       const uint32_t u = 64u * g + (uint32_t)lane;
@@ -264,25 +288,25 @@ __device__ __forceinline__ void issue_dma(const Plan& p, uint8_t* S, uint32_t w,
       dma16_nt((const void*)(p.bg + 1024ull * j + 16ull * (uint32_t)lane), S + 16u * kDU + 1024u * j);
     } else {
       const uint32_t u0 = 64u * (g - iD - iB), u = u0 + (uint32_t)lane;
-      // unit u's segment: the last of the 2 np segments (keys of pushes
-      // 0..np-1, then their values) whose first unit is <= u; the walk visits
-      // only the segment starts inside [u0, u0 + 64)
-      const bool lv = (uint32_t)lane < np;
-      const uint32_t c0 = (uint32_t)__popcll(__ballot(lv && p.pk <= u0)) +
-                          (uint32_t)__popcll(__ballot(lv && p.pv <= u0));
+      // unit u's segment: the last of the 2 nq segments (keys of pushes
+      // q0..q1-1, then their values) whose first unit is <= u; the walk
+      // visits only the segment starts inside [u0, u0 + 64)
+      const bool lv = (uint32_t)lane >= q0 && (uint32_t)lane < L.q1;
+      const uint32_t c0 = (uint32_t)__popcll(__ballot(lv && L.pk <= u0)) +
+                          (uint32_t)__popcll(__ballot(lv && L.pv <= u0));
       // unit address of segment k's first unit, minus that unit's index
       auto segbase = [&](uint32_t k) -> uint64_t {
-        return k < np ? (rl64(p.ks, k) >> 4) - rl(p.pk, k)
-                      : (rl64(p.vs, k - np) >> 4) - rl(p.pv, k - np);
+        return k < nq ? (rl64(p.ks, q0 + k) >> 4) - rl(L.pk, q0 + k)
+                      : (rl64(p.vs, q0 + k - nq) >> 4) - rl(L.pv, q0 + k - nq);
       };
       uint64_t gm = segbase(c0 - 1u);
-      for (uint32_t k = c0; k < 2u * np; ++k) {
-        const uint32_t P = k < np ? rl(p.pk, k) : rl(p.pv, k - np);
+      for (uint32_t k = c0; k < 2u * nq; ++k) {
+        const uint32_t P = k < nq ? rl(L.pk, q0 + k) : rl(L.pv, q0 + k - nq);
         if (P > u0 + 63u) break;
         const uint64_t gk = segbase(k);
         if (u >= P) gm = gk;
       }
-      if (u < p.npu) dma16((const void*)((gm + u) << 4), S + 16u * (kPU0 + u0));
+      if (u < L.npu) dma16((const void*)((gm + u) << 4), S + 16u * (kPU0 + u0));
     }
   }
 }
@@ -349,7 +373,7 @@ __global__ __launch_bounds__(kNT, 2) void staged_kernel(const TileDesc* __restri
     p0 = make_plan(d0, r0, true, lane, w == 0);
     p1 = make_plan(d1, r1, t_begin + 1 < t_end, lane, w == 0);
   }
-  issue_dma(p0, stg[0], w, lane);
+  issue_dma(p0, layout(p0, 0u, lane), stg[0], w, lane, true);
 #pragma unroll
   for (int b = 0; b < 2; ++b) {
     *(u32x4*)&sums[b][8 * tid] = u32x4{0u, 0u, 0u, 0u};
@@ -386,7 +410,7 @@ __global__ __launch_bounds__(kNT, 2) void staged_kernel(const TileDesc* __restri
     __syncthreads();
 
     // ---- (B) tile t+1's DMA, t+2's plan, t+3's push table, t+4's descriptor
-    issue_dma(p1, stg[(i + 1u) & 1u], w, lane);
+    issue_dma(p1, layout(p1, 0u, lane), stg[(i + 1u) & 1u], w, lane, true);
     const Raw r3 = load_raw(d3, t + 3 < t_end, lane);
     const uint32_t d4 = load_desc(tiles, t + 4, t_end, lane);
     const Plan p2 = make_plan(d2, r2, t + 2 < t_end, lane, w == 0);
@@ -445,172 +469,176 @@ __global__ __launch_bounds__(kNT, 2) void staged_kernel(const TileDesc* __restri
       lds_barrier();
     }
 
-#if PSG_STAGED_SKELETON == 1
-    {  // diagnostic: the stage is read (one key and value per lane per round), no search/fold
-      float tsum = 0.f;
-      const uint32_t U = p0.nr;
-      for (uint32_t ru = w; ru < U; ru += kNW) {
-        const uint32_t q = (uint32_t)__popcll(__ballot(p0.rend <= ru));
-        const uint32_t rs = q ? rl(p0.rend, q - 1u) : 0u;
-        const uint32_t ii = 64u * (ru - rs) + (uint32_t)lane;
-        if (ii < rl(p0.len, q) && !p0.ovf) {
-          const uint32_t kb = 16u * (kPU0 + rl(p0.pk, q)) + (rl((uint32_t)p0.ks, q) & 15u);
-          const uint32_t vb = 16u * (kPU0 + rl(p0.pv, q)) + (rl((uint32_t)p0.vs, q) & 15u);
-          tsum += *(const float*)(S + vb + 4u * ii) + (float)(uint32_t)(*(const uint64_t*)(S + kb + 8u * ii) & 1u);
-        }
+    // ---- (E) groups of pushes (one unless the pieces exceed the stage),
+    // passes: this wave's run of rounds (64 consecutive keys of one push,
+    // push-major), keys and values from the stage.  No compiler-visible
+    // vector-memory load in here: a wait for one would also wait for tile
+    // t+1's DMA.
+    for (uint32_t q0 = 0;;) {
+      const Layout Lg = layout(p0, q0, lane);
+      if (q0 > 0) {  // a later group: its pieces into the stage now (rare)
+        issue_dma(p0, Lg, S, w, lane, false);
+        dma_wait();
+        lds_barrier();
       }
-      SU[2u * s0] = __float_as_uint(__uint_as_float(SU[2u * s0]) + tsum + (float)(uint32_t)dk[s0]);
-      SU[2u * s0 + 1u] = np;
-      lds_barrier();
-    }
-#else
-    // ---- (E) passes: this wave's run of rounds (64 consecutive keys of one
-    // push, push-major), keys and values from the stage
-    const uint32_t U = p0.nr;
-    for (uint32_t done = 0; done < U;) {
-      uint32_t Rw = (U - done + kNW - 1) / kNW;
-      Rw = Rw < (uint32_t)kCap ? Rw : (uint32_t)kCap;
-      const uint32_t ua = done + w * Rw;
-      const uint32_t ub = ua + Rw < U ? ua + Rw : U;
-      const uint32_t nrw = ub > ua ? ub - ua : 0u;
-      uint32_t re[kCap];
-      uint64_t ek[kCap];
-      float ev[kCap];
-      uint32_t hv = 0;
-#pragma unroll
-      for (int r = 0; r < kCap; ++r) {
-        re[r] = 0;
-        ek[r] = 0;
-        ev[r] = 0.f;
-        if ((uint32_t)r < nrw) {
-          const uint32_t ru = ua + (uint32_t)r;
+      const uint32_t R0 = q0 ? rl(p0.rend, q0 - 1u) : 0u;
+      const uint32_t R1 = Lg.q1 ? rl(p0.rend, Lg.q1 - 1u) : 0u;
+      const uint32_t U = R1 - R0;
+#if PSG_STAGED_SKELETON == 1
+      {  // diagnostic: the stage is read (one key and value per lane per round), no search/fold
+        float tsum = 0.f;
+        for (uint32_t ru = R0 + w; ru < R1; ru += kNW) {
           const uint32_t q = (uint32_t)__popcll(__ballot(p0.rend <= ru));
           const uint32_t rs = q ? rl(p0.rend, q - 1u) : 0u;
-          const uint32_t c = ru - rs;
-          re[r] = q << 5 | c;
-          const uint32_t ii = 64u * c + (uint32_t)lane;
-          const bool have = ii < rl(p0.len, q);
-          hv |= (uint32_t)have << r;
-          if (!p0.ovf) {
-            const uint32_t kb = 16u * (kPU0 + rl(p0.pk, q)) + (rl((uint32_t)p0.ks, q) & 15u);
-            const uint32_t vb = 16u * (kPU0 + rl(p0.pv, q)) + (rl((uint32_t)p0.vs, q) & 15u);
+          const uint32_t ii = 64u * (ru - rs) + (uint32_t)lane;
+          if (ii < rl(p0.len, q)) {
+            const uint32_t kb = 16u * (kPU0 + rl(Lg.pk, q)) + (rl((uint32_t)p0.ks, q) & 15u);
+            const uint32_t vb = 16u * (kPU0 + rl(Lg.pv, q)) + (rl((uint32_t)p0.vs, q) & 15u);
+            tsum += *(const float*)(S + vb + 4u * ii) +
+                    (float)(uint32_t)(*(const uint64_t*)(S + kb + 8u * ii) & 1u);
+          }
+        }
+        SU[2u * s0] = __float_as_uint(__uint_as_float(SU[2u * s0]) + tsum + (float)(uint32_t)dk[s0]);
+        SU[2u * s0 + 1u] = np;
+        lds_barrier();
+      }
+#else
+      for (uint32_t done = 0; done < U;) {
+        uint32_t Rw = (U - done + kNW - 1) / kNW;
+        Rw = Rw < (uint32_t)kCap ? Rw : (uint32_t)kCap;
+        const uint32_t ua = R0 + done + w * Rw;
+        const uint32_t ub = ua + Rw < R1 ? ua + Rw : R1;
+        const uint32_t nrw = ub > ua ? ub - ua : 0u;
+        uint32_t re[kCap];
+        uint64_t ek[kCap];
+        float ev[kCap];
+        uint32_t hv = 0;
+#pragma unroll
+        for (int r = 0; r < kCap; ++r) {
+          re[r] = 0;
+          ek[r] = 0;
+          ev[r] = 0.f;
+          if ((uint32_t)r < nrw) {
+            const uint32_t ru = ua + (uint32_t)r;
+            const uint32_t q = (uint32_t)__popcll(__ballot(p0.rend <= ru));
+            const uint32_t rs = q ? rl(p0.rend, q - 1u) : 0u;
+            const uint32_t c = ru - rs;
+            re[r] = q << 5 | c;
+            const uint32_t ii = 64u * c + (uint32_t)lane;
+            const bool have = ii < rl(p0.len, q);
+            hv |= (uint32_t)have << r;
+            const uint32_t kb = 16u * (kPU0 + rl(Lg.pk, q)) + (rl((uint32_t)p0.ks, q) & 15u);
+            const uint32_t vb = 16u * (kPU0 + rl(Lg.pv, q)) + (rl((uint32_t)p0.vs, q) & 15u);
             if (have) {
               ek[r] = *(const uint64_t*)(S + kb + 8u * ii);
               ev[r] = *(const float*)(S + vb + 4u * ii);
             }
-          } else {  // pieces too large for the stage: from global memory
-            const uint64_t* kp = (const uint64_t*)rl64(p0.ks, q);
-            const float* vp = (const float*)rl64(p0.vs, q);
-            if (have) {
-              ek[r] = G(kp)[ii];
-              ev[r] = G(vp)[ii];
-            }
           }
         }
-      }
-      // search: psg_tile.hip's window over the 4 keys at the bucket start,
-      // bisection past it for the rare long bucket
-      uint32_t pos[kCap];
-      uint32_t fd = 0, okb = 0, deep = 0;
-#pragma unroll
-      for (int r = 0; r < kCap; ++r) {
-        pos[r] = 0;
-        if ((uint32_t)r < nrw) {
-          const uint64_t k = ek[r];
-          const uint32_t b = bucket(k);
-          const uint32_t l = bt[b];
-          const uint32_t n = (uint32_t)bt[b + 1] - l;
-          const uint64_t* wk = dk + l;
-          const uint64_t k0 = wk[0], k1 = wk[1], k2 = wk[2], k3 = wk[3];
-          const uint32_t c = (uint32_t)(k0 < k) + (uint32_t)(k1 < k) + (uint32_t)(k2 < k) +
-                             (uint32_t)(k3 < k);
-          const uint32_t p = l + c;
-          pos[r] = p;
-          const uint64_t eq = __ballot(k0 == k) | __ballot(k1 == k) | __ballot(k2 == k) |
-                              __ballot(k3 == k);
-          const bool hit = ((eq >> lane) & 1ull) && p < nt;
-          fd |= (uint32_t)hit << r;
-          deep |= (uint32_t)(c == 4u && n > 4u) << r;
-        }
-      }
-      if (__ballot(deep != 0u)) {
+        // search: psg_tile.hip's window over the 4 keys at the bucket start,
+        // bisection past it for the rare long bucket
+        uint32_t pos[kCap];
+        uint32_t fd = 0, okb = 0, deep = 0;
 #pragma unroll
         for (int r = 0; r < kCap; ++r) {
-          if ((deep >> r) & 1u) {
+          pos[r] = 0;
+          if ((uint32_t)r < nrw) {
             const uint64_t k = ek[r];
             const uint32_t b = bucket(k);
-            uint32_t l = bt[b] + 4u;
-            uint32_t n = (uint32_t)bt[b + 1] - l;
-            while (n > 0u) {
-              const uint32_t half = n >> 1;
-              if (dk[l + half] < k) {
-                l += half + 1u;
-                n -= half + 1u;
-              } else {
-                n = half;
-              }
-            }
-            pos[r] = l;
-            fd |= (uint32_t)(l < nt && dk[l] == k) << r;
+            const uint32_t l = bt[b];
+            const uint32_t n = (uint32_t)bt[b + 1] - l;
+            const uint64_t* wk = dk + l;
+            const uint64_t k0 = wk[0], k1 = wk[1], k2 = wk[2], k3 = wk[3];
+            const uint32_t c = (uint32_t)(k0 < k) + (uint32_t)(k1 < k) + (uint32_t)(k2 < k) +
+                               (uint32_t)(k3 < k);
+            const uint32_t p = l + c;
+            pos[r] = p;
+            const uint64_t eq = __ballot(k0 == k) | __ballot(k1 == k) | __ballot(k2 == k) |
+                                __ballot(k3 == k);
+            const bool hit = ((eq >> lane) & 1ull) && p < nt;
+            fd |= (uint32_t)hit << r;
+            deep |= (uint32_t)(c == 4u && n > 4u) << r;
           }
         }
-      }
-      int mylast = 0;
-#pragma unroll
-      for (int r = 0; r < kCap; ++r)
-        if ((uint32_t)r + 1u == nrw) mylast = (int)pos[r];
-      if (nrw && lane == 63) lastpos[w] = mylast;
-      lds_barrier();  // lastpos of every wave
-
-      // order check: matched positions strictly increase inside a piece
-#pragma unroll
-      for (int r = 0; r < kCap; ++r) {
-        if ((uint32_t)r < nrw) {
-          int prev0;
-          if ((re[r] & 31u) == 0u) prev0 = -1;  // first round of the piece
-          else if (r > 0) prev0 = __builtin_amdgcn_readlane((int)pos[r - 1], 63);
-          else prev0 = w > 0 ? lastpos[w - 1] : pcarry;
-          const int prev = __builtin_amdgcn_update_dpp(prev0, (int)pos[r], 0x138, 0xf, 0xf, false);
-          const bool ok = ((hv & fd) >> r & 1u) && (int)pos[r] > prev;
-          okb |= (uint32_t)ok << r;
-        }
-      }
-      if (__ballot((hv & ~okb) != 0u)) {
-        unsigned long long* fail = nullptr;
-#pragma unroll
-        for (int r = 0; r < kCap; ++r) {
-          const uint64_t bad = __ballot(((hv & ~okb) >> r & 1u) != 0u);
-          if ((uint32_t)r < nrw && bad && lane == 0) {
-            if (!fail) fail = (unsigned long long*)DF64(d0, fail);
-            __hip_atomic_fetch_add(GW(fail) + (re[r] >> 5), (unsigned long long)__popcll(bad),
-                                   __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-          }
-        }
-      }
-
-      // fold, wave by wave (rounds are push-major: arrival order per slot)
-      const uint32_t inpass = (U - done) < kNW * Rw ? U - done : kNW * Rw;
-      const uint32_t wl = (inpass - 1) / Rw;
-      for (uint32_t st = 0; st < (uint32_t)kNW; ++st) {
-        if (st == w) {
+        if (__ballot(deep != 0u)) {
 #pragma unroll
           for (int r = 0; r < kCap; ++r) {
-            if ((uint32_t)r < nrw && ((okb >> r) & 1u)) {
-              const uint32_t q = re[r] >> 5;
-              u32x2* const sp = (u32x2*)&SU[2u * pos[r]];
-              const u32x2 x = *sp;
-              const float sum = q == 0u ? ev[r] : __uint_as_float(x.x) + ev[r];
-              *sp = u32x2{__float_as_uint(sum), x.y + 1u};
+            if ((deep >> r) & 1u) {
+              const uint64_t k = ek[r];
+              const uint32_t b = bucket(k);
+              uint32_t l = bt[b] + 4u;
+              uint32_t n = (uint32_t)bt[b + 1] - l;
+              while (n > 0u) {
+                const uint32_t half = n >> 1;
+                if (dk[l + half] < k) {
+                  l += half + 1u;
+                  n -= half + 1u;
+                } else {
+                  n = half;
+                }
+              }
+              pos[r] = l;
+              fd |= (uint32_t)(l < nt && dk[l] == k) << r;
             }
           }
-          if (w == wl && lane == 63) pcarry = mylast;
         }
-        lds_barrier();
+        int mylast = 0;
+#pragma unroll
+        for (int r = 0; r < kCap; ++r)
+          if ((uint32_t)r + 1u == nrw) mylast = (int)pos[r];
+        if (nrw && lane == 63) lastpos[w] = mylast;
+        lds_barrier();  // lastpos of every wave
+
+        // order check: matched positions strictly increase inside a piece
+#pragma unroll
+        for (int r = 0; r < kCap; ++r) {
+          if ((uint32_t)r < nrw) {
+            int prev0;
+            if ((re[r] & 31u) == 0u) prev0 = -1;  // first round of the piece
+            else if (r > 0) prev0 = __builtin_amdgcn_readlane((int)pos[r - 1], 63);
+            else prev0 = w > 0 ? lastpos[w - 1] : pcarry;
+            const int prev = __builtin_amdgcn_update_dpp(prev0, (int)pos[r], 0x138, 0xf, 0xf, false);
+            const bool ok = ((hv & fd) >> r & 1u) && (int)pos[r] > prev;
+            okb |= (uint32_t)ok << r;
+          }
+        }
+        if (__ballot((hv & ~okb) != 0u)) {
+          unsigned long long* const fail = (unsigned long long*)DF64(d0, fail);
+#pragma unroll
+          for (int r = 0; r < kCap; ++r) {
+            const uint64_t bad = __ballot(((hv & ~okb) >> r & 1u) != 0u);
+            if ((uint32_t)r < nrw && bad && lane == 0)
+              __hip_atomic_fetch_add(GW(fail) + (re[r] >> 5), (unsigned long long)__popcll(bad),
+                                     __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+          }
+        }
+
+        // fold, wave by wave (rounds are push-major: arrival order per slot)
+        const uint32_t inpass = (U - done) < kNW * Rw ? U - done : kNW * Rw;
+        const uint32_t wl = (inpass - 1) / Rw;
+        for (uint32_t st = 0; st < (uint32_t)kNW; ++st) {
+          if (st == w) {
+#pragma unroll
+            for (int r = 0; r < kCap; ++r) {
+              if ((uint32_t)r < nrw && ((okb >> r) & 1u)) {
+                const uint32_t q = re[r] >> 5;
+                u32x2* const sp = (u32x2*)&SU[2u * pos[r]];
+                const u32x2 x = *sp;
+                const float sum = q == 0u ? ev[r] : __uint_as_float(x.x) + ev[r];
+                *sp = u32x2{__float_as_uint(sum), x.y + 1u};
+              }
+            }
+            if (w == wl && lane == 63) pcarry = mylast;
+          }
+          lds_barrier();
+        }
+        done += kNW * Rw;
       }
-      done += kNW * Rw;
-    }
-    if (U == 0) lds_barrier();  // (the stage is released by the barrier that ends the tile)
 #endif
+      q0 = Lg.q1;
+      if (q0 >= np) break;
+    }
+    lds_barrier();  // the stage and the sums are complete (and free)
 
     // ---- rotate the pipeline
     pm_out = p0.out;
@@ -625,7 +653,7 @@ __global__ __launch_bounds__(kNT, 2) void staged_kernel(const TileDesc* __restri
     p0 = p1;
     p1 = p2;
   }
-  // the run's last tile (its fold ended with a barrier)
+  // the run's last tile
   store_tile(sums[(t_end - t_begin - 1u) & 1u], pm_out, pm_nt, pm_np, pm_par, tid);
 }
 

@@ -23,8 +23,10 @@ pytestmark = pytest.mark.gpu
 
 
 def _flags():
-    from parameter_server_amd._lib import PSG_FORM_STAGED
-    return PSG_FORM_STAGED
+    # uniform (push-per-round) rounds forced: jobs of short pieces would take
+    # the packed kernel by default
+    from parameter_server_amd._lib import PSG_FORM_STAGED, PSG_FORM_UNIFORM
+    return PSG_FORM_STAGED | PSG_FORM_UNIFORM
 
 
 def _check_plan(torch, cases, parallel, reps=2, want_form=True):
