@@ -123,7 +123,8 @@ hipError_t launch_partition(const JobDev* d_jobs, const uint32_t* d_split_item_j
 // aggregate: one workgroup per tile of kTileSlots slots.  psg_tile.hip:
 // every round holds one push (long pieces); psg_tile_packed.hip: rounds may
 // hold several pushes (many short pieces)
-// form: 0 = groups of 32 pushes (1024-slot tiles), 1 = groups of 64 (2048-slot
+// form: 2 = the persistent form of 0 (jobs of <= 32 pushes, m = 1),
+// 0 = groups of 32 pushes (1024-slot tiles), 1 = groups of 64 (2048-slot
 // tiles)
 hipError_t launch_aggregate_tile(int dtype, int m, const TileDesc* d_tiles, uint32_t ntiles,
                                  int form, hipStream_t stream);

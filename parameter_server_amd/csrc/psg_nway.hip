@@ -813,7 +813,10 @@ struct NwLayout {
 #ifndef PSG_NW_RR
 #define PSG_NW_RR 1
 #endif
-  bool rr() const { return PSG_NW_RR && nm > 1; }
+  // round-robin tickets run maxT * nm workgroups: only where that stays
+  // within a small factor of the tiles (a skewed batch -- one large merge and
+  // many one-tile merges -- would launch mostly idle workgroups)
+  bool rr() const { return PSG_NW_RR && nm > 1 && maxT * nm <= 2 * ntiles; }
   uint64_t tickets() const { return rr() ? maxT * nm : ntiles; }
 
   unsigned long long* misc(char* b, uint32_t j) const {

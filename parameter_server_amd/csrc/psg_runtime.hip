@@ -8,6 +8,7 @@
 // a mutex gives the reference's threading contract (setValue on the
 // executor thread, received() from the app thread, kv_vector.h:45,67).
 #include <hip/hip_runtime.h>
+#include <chrono>
 
 #include <algorithm>
 #include <cmath>
@@ -151,8 +152,9 @@ struct JobTable {
   int device = -1;
   int knob_part = -1, knob_pack = -1, knob_wide = -1;  // forced (read_knobs), -1 = chosen
   int knob_cursor = -1;
-  int knob_staged = -1;
+  int knob_staged = -1, knob_persist = -1;
   void read_knobs(unsigned f) {
+    knob_persist = (f & PSG_FORM_PERSIST) ? 1 : (f & PSG_NO_PERSIST) ? 0 : -1;
     knob_staged = (f & PSG_FORM_STAGED) ? 1 : (f & PSG_NO_STAGED) ? 0 : -1;
     knob_cursor = (f & PSG_FORM_CURSOR) ? 1 : (f & PSG_NO_CURSOR) ? 0 : -1;
     knob_part = (f & PSG_PART_SEARCH) ? (int)psg::kSearch
@@ -173,6 +175,9 @@ struct JobTable {
   // staged form (psg_tile_staged.hip): long pieces of <= 31 pushes per job,
   // f32, one value array, no continued aggregates
   bool staged = false;
+  // persistent form of the tile kernel (psg_tile.hip kP): jobs of <= 32
+  // pushes, one value array
+  bool persist = false;
   uint32_t bxs = 32;          // boundary words per chunk boundary (pushes per job at most)
   uint32_t nchunks = 0;
   psg::CursorJob* d_cjobs = nullptr;
@@ -387,6 +392,10 @@ struct JobTable {
       if (jobs[j].dense || (jobs[j].flags & psg::kFlagCont) ||
           !psg::staged_fits(info[j].np, dtype, m))
         staged = false;
+    persist = !dense && !pack && !wide && !cursor && !pcursor && !staged && tiles > 0 && m == 1 &&
+              knob_persist == 1;
+    for (size_t j = 0; persist && j < jobs.size(); ++j)
+      if (jobs[j].dense || info[j].np > 32u) persist = false;
     if (cursor || pcursor) {
       // about one chunk per workgroup slot of the chip (256 CUs x 8
       // workgroups of the cursor kernel, x 4 of the packed one)
@@ -706,7 +715,7 @@ struct JobTable {
     else if (staged)
       HIP_TRY(psg::launch_aggregate_staged(d_tiles, ntiles, s));
     else
-      HIP_TRY(psg::launch_aggregate_tile(dtype, m, d_tiles, ntiles, wide ? 1 : 0, s));
+      HIP_TRY(psg::launch_aggregate_tile(dtype, m, d_tiles, ntiles, wide ? 1 : persist ? 2 : 0, s));
     return PSG_OK;
   }
 
@@ -930,16 +939,23 @@ struct Filter {
 #ifndef PSG_SPIN
 #define PSG_SPIN 1
 #endif
-// the host waits for the end of a call's device work by polling its event:
-// a pushing caller is blocked on it anyway, and the poll sees completion
-// sooner than a blocking wait's wake-up (the e2e pinned path waits once per
-// push)
+// the host waits for the end of a call's device work by polling its event
+// for a bounded time: a pushing caller is blocked on it anyway, and the poll
+// sees a short wait's completion sooner than a blocking wait's wake-up (the
+// e2e pinned path waits once per push).  Past ~50 us it
+// yields to a blocking wait, so threads waiting on long device work (the
+// loopback exchange's ranks, several contexts) do not each burn a core
+// (ADVICE r05).
 static hipError_t spin_wait(hipEvent_t e) {
 #if PSG_SPIN
-  for (;;) {
+  const auto t0 = std::chrono::steady_clock::now();
+  for (int i = 0;; ++i) {
     const hipError_t q = hipEventQuery(e);
     if (q != hipErrorNotReady) return q;
+    if ((i & 15) == 15 && std::chrono::steady_clock::now() - t0 > std::chrono::microseconds(50))
+      break;
   }
+  return hipEventSynchronize(e);
 #else
   return hipEventSynchronize(e);
 #endif
@@ -1567,6 +1583,7 @@ int psg_plan_form(psg_plan* plan, int* form) {
           : T.pack  ? PSG_KERNEL_PACKED
           : T.wide  ? PSG_KERNEL_TILE64
           : T.staged ? PSG_KERNEL_STAGED
+          : T.persist ? PSG_KERNEL_PERSIST
                     : PSG_KERNEL_TILE;
   return PSG_OK;
 }
@@ -2556,6 +2573,11 @@ int psg_darling_state(psg_ctx* c, int chl, size_t off, size_t n, double* delta, 
 }
 
 // ------------------------------------------------------ frequency filter --
+namespace {
+int filter_order(Filter* F, hipStream_t s);
+int filter_mark(psg_ctx* c, Filter* F, hipStream_t s);
+}  // namespace
+
 int psg_freq_resize(psg_ctx* c, int chl, int n, int k) {
   if (!c) return fail(PSG_ERR_ARG, "null ctx");
   std::lock_guard<std::mutex> l(c->mu);
@@ -2571,8 +2593,13 @@ int psg_freq_resize(psg_ctx* c, int chl, int n, int k) {
     F.n = nn;
   }
   F.k = std::min(30, std::max(1, k));  // countmin.h:18
+  // the clear joins the filter's call order: after the filter's
+  // previous operation on any stream, and before the next one on any stream
+  // (a caller stream, the null stream included, does not wait for the
+  // non-blocking context stream by itself)
+  if (int rc = filter_order(&F, c->stream)) return rc;
   HIP_TRY(hipMemsetAsync(F.d_table, 0, psg::cm_table_bytes(F.n), c->stream));
-  return PSG_OK;
+  return filter_mark(c, &F, c->stream);
 }
 
 int psg_freq_clear(psg_ctx* c, int chl) {

@@ -234,6 +234,35 @@ def test_gpu_freq_filter_inserts_on_two_streams_in_call_order():
 
 
 @pytest.mark.gpu
+def test_gpu_freq_filter_resize_then_insert_on_side_stream():
+    """psg_freq_resize clears the table on the context stream; an insert on a
+    caller stream enqueued right after it (no host wait) must see the cleared
+    table (the clear joins the filter's call order).  A second
+    resize of an already filled filter, then an insert on the same side
+    stream, must also start from zero."""
+    import torch
+    assert torch.cuda.is_available()
+    from parameter_server_amd import _lib
+    rng = np.random.default_rng(19)
+    v = _ctx()
+    n = 1 << 22
+    s1 = torch.cuda.Stream()
+    for rep in range(2):  # a new filter, then a resize of a filled one
+        keys = np.unique(zipf_keys(rng, 400_000))
+        counts = rng.integers(1, 300, keys.size).astype(np.uint32)
+        dk = torch.from_numpy(keys.view(np.int64)).cuda()
+        dc = torch.from_numpy(counts.view(np.int32)).cuda()
+        torch.cuda.synchronize()
+        _lib.check(v._L.psg_freq_resize(v._h, 6, n, 3))
+        _lib.check(v._L.psg_freq_insert_dev(v._h, 6, dk.data_ptr(), dc.data_ptr(), keys.size,
+                                            C.c_void_p(s1.cuda_stream)))
+        t, nn, kk = O.cm_resize(n, 3)
+        O.cm_insert(t, nn, kk, keys, counts)
+        assert np.array_equal(_table(v, 6, nn), t)
+    v.close()
+
+
+@pytest.mark.gpu
 @pytest.mark.timeout(600)
 @pytest.mark.parametrize("k,nq", [(1, 400_000), (3, 1_000_003), (4, 2_000_000), (5, 700_001),
                                   (8, 9_000_000)])

@@ -281,3 +281,49 @@ def test_nway_batch_of_merges_vs_oracle():
         u.result()
     assert e.value.status == PSG_ERR_UNSORTED
     u.close()
+
+
+def test_nway_skewed_batch_vs_oracle():
+    """A skewed batch (one cfg2-shaped merge of ~150 tiles and 40 one-tile
+    merges of 1-3 short pushes): the tickets map one per tile instead of
+    round-robin over the merges (maxT x nm would be ~40 x the
+    tiles); unions and sums bit-exact against the oracle, both modes."""
+    import torch
+    from parameter_server_amd import synth
+    from parameter_server_amd._lib import PSG_F32
+    from parameter_server_amd.kv_vector import NWayMergeBatch
+    dev = torch.device("cuda", 0)
+    rng = np.random.default_rng(23)
+    cases = [synth.overlap_pushes(51, npush=8, n=40000)[1]]
+    for j in range(40):
+        ps = []
+        for _ in range(int(rng.integers(1, 4))):
+            k = np.unique(rng.integers(0, 1 << 40, int(rng.integers(1, 60)), dtype=np.uint64))
+            ps.append((k, [rng.standard_normal(k.size).astype(np.float32)]))
+        cases.append(ps)
+    keep, merges = [], []
+    for pushes in cases:
+        dk = [torch.from_numpy(np.ascontiguousarray(k).view(np.int64)).to(dev) for k, _ in pushes]
+        dv = [[torch.from_numpy(np.ascontiguousarray(v, np.float32)).to(dev) for v in vs[:1]]
+              for _, vs in pushes]
+        tot = max(1, sum(k.size for k, _ in pushes))
+        ok = torch.full((tot,), -1, dtype=torch.int64, device=dev)
+        ov = torch.empty(tot, dtype=torch.float32, device=dev)
+        keep += [dk, dv, ok, ov]
+        merges.append(dict(push_keys=[t.data_ptr() for t in dk], push_n=[k.size for k, _ in pushes],
+                           push_vals=[[t.data_ptr() for t in vs] for vs in dv],
+                           out_keys=ok.data_ptr(), out_vals=[ov.data_ptr()]))
+    for parallel in (False, True):
+        u = NWayMergeBatch(0, PSG_F32, merges, parallel)
+        u.run()
+        counts = u.result()
+        for j, pushes in enumerate(cases):
+            D = _union(pushes)
+            assert counts[j] == D.size
+            ok, ov = keep[4 * j + 2], keep[4 * j + 3]
+            assert np.array_equal(ok.cpu().numpy()[: D.size].view(np.uint64), D)
+            rc, lo, hi_, want, _ = O.aggregate(D, *ALL, [(k, vs[:1]) for k, vs in pushes],
+                                               parallel, 1, np.float32)
+            assert rc == 0
+            assert np.array_equal(_bits(ov.cpu().numpy()[lo:hi_]), _bits(want[0]))
+        u.close()

@@ -13,6 +13,7 @@ disturbed); printed as a share of the summed clocks and as clocks per tile.  Pha
   4 -> order check + wave-ordered fold of a pass (4 barriers)
   5 -> after the last pass
   6 -> stores issued
+  7 -> (persistent form) the end-of-tile barrier
 """
 import argparse
 import ctypes as C
@@ -31,9 +32,11 @@ def main():
     ap.add_argument("--workload", default="cfg2")
     ap.add_argument("--batch", type=int, default=64)
     ap.add_argument("--reps", type=int, default=10)
+    ap.add_argument("--plan-flags", type=lambda x: int(x, 0), default=0)
     a = ap.parse_args()
     import torch
     import bench
+    bench.PLAN_FLAGS = a.plan_flags
     from parameter_server_amd import synth, _lib
     dev = torch.device("cuda", 0)
     if a.workload == "cfg2":
@@ -61,9 +64,9 @@ def main():
     tot = rows.sum()
     out = {"workload": a.workload, "kernel_ms": e0.elapsed_time(e1) / a.reps,
            "tiles": int(rows.shape[0]), "clocks_per_tile": tot / max(rows.shape[0], 1),
-           "share": {str(i): float(rows[:, i].sum() / tot) for i in range(7)},
-           "clocks_per_tile_by_phase": {str(i): float(rows[:, i].mean()) for i in range(7)},
-           "p90_by_phase": {str(i): float(np.percentile(rows[:, i], 90)) for i in range(7)}}
+           "share": {str(i): float(rows[:, i].sum() / tot) for i in range(8)},
+           "clocks_per_tile_by_phase": {str(i): float(rows[:, i].mean()) for i in range(8)},
+           "p90_by_phase": {str(i): float(np.percentile(rows[:, i], 90)) for i in range(8)}}
     print(json.dumps(out))
 
 
