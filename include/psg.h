@@ -85,10 +85,6 @@ typedef enum psg_dtype { PSG_F32 = 0, PSG_F64 = 1 } psg_dtype;
 #define PSG_NO_INDEX 0x100000u    /* plan: no resident bucket index (tables built per run) */
 #define PSG_FORM_CURSOR 0x400000u /* plan: a cursor form (no partition pass) where it applies */
 #define PSG_NO_CURSOR 0x800000u   /* plan: never a cursor form (the default) */
-#define PSG_FORM_STAGED 0x1000000u /* long pieces: the staged (LDS-DMA, one tile ahead) kernel where it applies */
-#define PSG_NO_STAGED 0x2000000u   /* long pieces: never the staged kernel */
-#define PSG_FORM_PERSIST 0x4000000u /* long pieces: the persistent tile walk where it applies */
-#define PSG_NO_PERSIST 0x8000000u   /* long pieces: one workgroup per tile */
 /* Plan option (psg_plan_create): the caller promises that the push KEYS at
  * the job's device pointers stay as they were at creation for the plan's
  * lifetime (values may change between runs).  Only then may the plan take
@@ -256,8 +252,6 @@ int psg_plan_matched(psg_plan* plan, uint64_t* matched);
 #define PSG_KERNEL_DENSE 3   /* contiguous slices: no key reads */
 #define PSG_KERNEL_CURSOR 4  /* no partition: per-push cursors across tile chunks */
 #define PSG_KERNEL_PACKED_CURSOR 5  /* no partition: packed rounds, cursors across tile chunks */
-#define PSG_KERNEL_STAGED 6  /* partition + persistent tile walk, pieces staged by LDS-DMA a tile ahead */
-#define PSG_KERNEL_PERSIST 7 /* partition + persistent tile walk, push tables prefetched a tile ahead */
 int psg_plan_form(psg_plan* plan, int* form);
 /* Algorithmic HBM bytes of one run (SURVEY.md 8d general form). */
 int psg_plan_bytes(psg_plan* plan, uint64_t* bytes, uint64_t* kv_pairs);

@@ -54,14 +54,10 @@ PSG_NO_INDEX = 0x100000
 # plan option: push keys fixed for the plan's lifetime (enables the dense kernel)
 PSG_STATIC_KEYS = 0x200000
 PSG_FORM_CURSOR = 0x400000
-PSG_FORM_STAGED = 0x1000000
-PSG_NO_STAGED = 0x2000000
-PSG_FORM_PERSIST = 0x4000000
-PSG_NO_PERSIST = 0x8000000
 PSG_NO_CURSOR = 0x800000
 # psg_plan_form: the aggregate kernel a plan runs
 (PSG_KERNEL_TILE, PSG_KERNEL_TILE64, PSG_KERNEL_PACKED, PSG_KERNEL_DENSE, PSG_KERNEL_CURSOR,
- PSG_KERNEL_PACKED_CURSOR, PSG_KERNEL_STAGED, PSG_KERNEL_PERSIST) = range(8)
+ PSG_KERNEL_PACKED_CURSOR) = range(6)
 MAX_VALUE_ARRAYS = 4
 
 # Every symbol include/psg.h declares, with its ctypes signature.

@@ -123,16 +123,10 @@ hipError_t launch_partition(const JobDev* d_jobs, const uint32_t* d_split_item_j
 // aggregate: one workgroup per tile of kTileSlots slots.  psg_tile.hip:
 // every round holds one push (long pieces); psg_tile_packed.hip: rounds may
 // hold several pushes (many short pieces)
-// form: 2 = the persistent form of 0 (jobs of <= 32 pushes, m = 1),
-// 0 = groups of 32 pushes (1024-slot tiles), 1 = groups of 64 (2048-slot
+// form: 0 = groups of 32 pushes (1024-slot tiles), 1 = groups of 64 (2048-slot
 // tiles)
 hipError_t launch_aggregate_tile(int dtype, int m, const TileDesc* d_tiles, uint32_t ntiles,
                                  int form, hipStream_t stream);
-// the staged form of the same (psg_tile_staged.hip): persistent workgroups,
-// 1024-slot tiles, each tile's D, index and pieces moved into LDS one tile
-// ahead; jobs of <= 31 pushes, f32, m = 1, no continued aggregates
-bool staged_fits(uint32_t np, int dtype, int m);
-hipError_t launch_aggregate_staged(const TileDesc* d_tiles, uint32_t ntiles, hipStream_t stream);
 // the bucket tables of the tile kernel's tiles (psg_tile.hip), built from D
 // alone: bucket_index_words(wide) u32 per tile at out + tile * words
 uint32_t bucket_index_words(uint32_t tile_slots);

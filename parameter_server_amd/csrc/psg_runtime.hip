@@ -152,10 +152,7 @@ struct JobTable {
   int device = -1;
   int knob_part = -1, knob_pack = -1, knob_wide = -1;  // forced (read_knobs), -1 = chosen
   int knob_cursor = -1;
-  int knob_staged = -1, knob_persist = -1;
   void read_knobs(unsigned f) {
-    knob_persist = (f & PSG_FORM_PERSIST) ? 1 : (f & PSG_NO_PERSIST) ? 0 : -1;
-    knob_staged = (f & PSG_FORM_STAGED) ? 1 : (f & PSG_NO_STAGED) ? 0 : -1;
     knob_cursor = (f & PSG_FORM_CURSOR) ? 1 : (f & PSG_NO_CURSOR) ? 0 : -1;
     knob_part = (f & PSG_PART_SEARCH) ? (int)psg::kSearch
                 : (f & PSG_PART_STREAM) ? (int)psg::kStream : -1;
@@ -172,12 +169,6 @@ struct JobTable {
   // packed cursor form (psg_tile_packed.hip CUR): short pieces of <= 256
   // pushes, no partition pass either
   bool pcursor = false;
-  // staged form (psg_tile_staged.hip): long pieces of <= 31 pushes per job,
-  // f32, one value array, no continued aggregates
-  bool staged = false;
-  // persistent form of the tile kernel (psg_tile.hip kP): jobs of <= 32
-  // pushes, one value array
-  bool persist = false;
   uint32_t bxs = 32;          // boundary words per chunk boundary (pushes per job at most)
   uint32_t nchunks = 0;
   psg::CursorJob* d_cjobs = nullptr;
@@ -387,15 +378,6 @@ struct JobTable {
       }
     }
     bxs = pcursor ? (uint32_t)psg::kPackCursorPushes : 32u;
-    staged = !dense && !pack && !wide && !cursor && !pcursor && tiles > 0 && knob_staged == 1;
-    for (size_t j = 0; staged && j < jobs.size(); ++j)
-      if (jobs[j].dense || (jobs[j].flags & psg::kFlagCont) ||
-          !psg::staged_fits(info[j].np, dtype, m))
-        staged = false;
-    persist = !dense && !pack && !wide && !cursor && !pcursor && !staged && tiles > 0 && m == 1 &&
-              knob_persist == 1;
-    for (size_t j = 0; persist && j < jobs.size(); ++j)
-      if (jobs[j].dense || info[j].np > 32u) persist = false;
     if (cursor || pcursor) {
       // about one chunk per workgroup slot of the chip (256 CUs x 8
       // workgroups of the cursor kernel, x 4 of the packed one)
@@ -712,10 +694,8 @@ struct JobTable {
     else if (pack)
       HIP_TRY(psg::launch_aggregate_tile_packed(dtype, m, d_tiles, ntiles, s,
                                                 pcursor ? d_chunks : nullptr, nchunks, d_bx));
-    else if (staged)
-      HIP_TRY(psg::launch_aggregate_staged(d_tiles, ntiles, s));
     else
-      HIP_TRY(psg::launch_aggregate_tile(dtype, m, d_tiles, ntiles, wide ? 1 : persist ? 2 : 0, s));
+      HIP_TRY(psg::launch_aggregate_tile(dtype, m, d_tiles, ntiles, wide ? 1 : 0, s));
     return PSG_OK;
   }
 
@@ -1582,8 +1562,6 @@ int psg_plan_form(psg_plan* plan, int* form) {
           : T.dense ? PSG_KERNEL_DENSE
           : T.pack  ? PSG_KERNEL_PACKED
           : T.wide  ? PSG_KERNEL_TILE64
-          : T.staged ? PSG_KERNEL_STAGED
-          : T.persist ? PSG_KERNEL_PERSIST
                     : PSG_KERNEL_TILE;
   return PSG_OK;
 }

@@ -102,9 +102,6 @@ __device__ __forceinline__ uint64_t uni64(uint64_t v) {
 #ifndef PSG_FUSECNT
 #define PSG_FUSECNT 1  // A/B builds: 0 = sums and contributor counts in separate arrays
 #endif
-#ifndef PSG_WIN128
-#define PSG_WIN128 0  // A/B builds: 1 = the search window by two aligned 16-B reads
-#endif
 #ifndef PSG_DDMA
 #define PSG_DDMA 1  // A/B builds: 0 = D and the resident bucket table through registers
 #endif
@@ -123,18 +120,6 @@ __device__ __forceinline__ void dma16(const void* g, void* lds) {
   asm volatile(
       "s_mov_b32 %0, m0\n\ts_mov_b32 m0, %2\n\ts_nop 0\n\t"
       "global_load_lds_dwordx4 %1, off nt\n\ts_mov_b32 m0, %0"
-      : "=&s"(keep)
-      : "v"(g), "s"(la)
-      : "memory");
-}
-// 4 B per lane (lane l writes lds + 4 l), default policy: the persistent
-// form's prefetch of the next tile's push table
-__device__ __forceinline__ void dma4(const void* g, void* lds) {
-  const uint32_t la = __builtin_amdgcn_readfirstlane((uint32_t)(uintptr_t)(LdsPtr)lds);
-  uint32_t keep;
-  asm volatile(
-      "s_mov_b32 %0, m0\n\ts_mov_b32 m0, %2\n\ts_nop 0\n\t"
-      "global_load_lds_dword %1, off\n\ts_mov_b32 m0, %0"
       : "=&s"(keep)
       : "v"(g), "s"(la)
       : "memory");
@@ -190,18 +175,9 @@ constexpr int occupancy() {
   return w >= 8 ? 8 : (w < 1 ? 1 : w);
 }
 
-// kP: the persistent form (1024-slot tiles, jobs of <= 32 pushes, one value
-// array): a workgroup walks an XCD-contiguous run of tiles, and the last wave
-// prefetches the next tile's push table (seg bounds, lengths, key and value
-// pointers) into LDS by LDS-DMA while this tile runs, so a tile starts with
-// its table in LDS instead of two dependent round trips (its descriptor,
-// then the table: 23 % of a tile's clocks, r05 phase clocks).  That wave
-// stores no sums (the other three store its slots), so its wait for the
-// prefetch at the next tile's start never waits for a store.
-template <typename V, int M, int kGroup, bool kP = false>
+template <typename V, int M, int kGroup>
 __global__ __launch_bounds__(nt_of(kGroup), (occupancy<V, M, kGroup>())) void tile_kernel(
     const TileDesc* __restrict__ tiles, uint32_t ntiles) {
-  static_assert(!kP || (kGroup == 32 && M == 1), "persistent form: 32-push groups, one value array");
   constexpr int kTS = ts_of(kGroup);   // slots per tile
   constexpr int kNT = nt_of(kGroup);   // threads
   constexpr int kNW = kNT / 64;        // waves
@@ -238,59 +214,12 @@ __global__ __launch_bounds__(nt_of(kGroup), (occupancy<V, M, kGroup>())) void ti
   __shared__ int lastpos[kNW];
   __shared__ int pcarry;
   __shared__ uint32_t wsum[kNW];
-  // kP: the next tile's push table as loaded (u32 words): [0, 32) piece
-  // starts, [32, 64) piece ends, then push lengths, key pointers and value
-  // pointers (u64 as word pairs), 64 words each
-  __shared__ __attribute__((aligned(16))) uint32_t raw[kP ? 256 : 1];
 
-  uint32_t t_first, t_last, t_step;
-  if constexpr (kP) {
-    // the XCD's share of the tiles [x n / 8, (x+1) n / 8) (blocks b and b+8
-    // share an XCD: speed only), dealt to its workgroups round robin: the
-    // tiles in flight on an XCD at any time are one contiguous window of the
-    // address space, as in the one-tile-per-workgroup launch (r06: contiguous
-    // runs per workgroup spread them over 8 aggregates and ran 17 % slower)
-    const uint32_t x = blockIdx.x & 7u, nx = (gridDim.x + 7u - x) >> 3;
-    const uint32_t lo = (uint32_t)((uint64_t)x * ntiles / 8u);
-    t_last = (uint32_t)((uint64_t)(x + 1u) * ntiles / 8u);
-    t_first = lo + (blockIdx.x >> 3);
-    t_step = nx;
-#ifdef PSG_RUNS
-    {  // A/B: a contiguous run per workgroup
-      const uint32_t nb = gridDim.x;
-      const uint32_t L = (blockIdx.x & 7u) * (nb >> 3) + (blockIdx.x >> 3);
-      t_first = (uint32_t)((uint64_t)L * ntiles / nb);
-      t_last = (uint32_t)((uint64_t)(L + 1) * ntiles / nb);
-      t_step = 1;
-    }
-#endif
-    if (t_first >= t_last) return;
-  } else {
-    t_first = xcd_tile(blockIdx.x, gridDim.x);
-    t_last = t_first + 1u;
-    t_step = 1;
-    if (t_first >= ntiles) return;
-  }
-  for (uint32_t ti = t_first; ti < t_last; ti += t_step) {
-  // the thread id, opaque per tile: otherwise the persistent loop hoists every
-  // thread-derived LDS and global address out of the loop and keeps them
-  // live across the tile (spills at 64 VGPRs)
-  int tid = (int)threadIdx.x;
-  if constexpr (kP) asm volatile("" : "+v"(tid));
+  const uint32_t w = uni((uint32_t)threadIdx.x >> 6);
+  const int tid = threadIdx.x;
   const int lane = tid & 63;
-  const uint32_t w = uni((uint32_t)tid >> 6);
-  // kP: the push table of tile tj into raw[] (the last wave)
-  auto fetch_raw = [&](uint32_t tj) {
-    const TileDesc& Tn = tiles[tj];
-    const uint32_t npn = Tn.np < (uint32_t)kGroup ? Tn.np : (uint32_t)kGroup;
-    const uint32_t q = (uint32_t)lane & 31u;
-    if (q < npn) dma4(Tn.seg + (size_t)q * Tn.stride + (lane < 32 ? 0u : Tn.segb), raw);
-    if ((uint32_t)lane < 2u * npn) {
-      dma4((const uint32_t*)Tn.pn + lane, raw + 64);
-      dma4((const uint32_t*)Tn.pkeys + lane, raw + 128);
-      dma4((const uint32_t*)Tn.pvals + lane, raw + 192);
-    }
-  };
+  const uint32_t ti = xcd_tile(blockIdx.x, gridDim.x);
+  if (ti >= ntiles) return;
 #ifdef PSG_PHASES
   unsigned long long ph_t = clock64();
   uint32_t ph_acc[8] = {0, 0, 0, 0, 0, 0, 0, 0};
@@ -344,39 +273,6 @@ __global__ __launch_bounds__(nt_of(kGroup), (occupancy<V, M, kGroup>())) void ti
       if (lane == 0) rpre[0] = 0;
     }
   };
-  // kP: the same table from raw[] (the last wave, after its wait for the
-  // prefetch), then the next tile's prefetch
-  auto tables_from_raw = [&]() {
-    if (w == (uint32_t)kNW - 1u) {
-      if (ti == t_first) fetch_raw(ti);
-      dma_wait();
-      int lane = tid & 63;
-      asm volatile("" : "+v"(lane));
-      const uint32_t gp = np < (uint32_t)kGroup ? np : (uint32_t)kGroup;
-      uint32_t nr = 0;
-      if ((uint32_t)lane < gp) {
-        const uint32_t q = (uint32_t)lane;
-        const uint32_t n = raw[64 + 2 * q];  // (uint32_t) of the u64 length, as load_tables
-        uint32_t a = raw[q], b = raw[32 + q];
-        const uint64_t kp = (uint64_t)raw[128 + 2 * q] | (uint64_t)raw[129 + 2 * q] << 32;
-        const uint64_t vp = (uint64_t)raw[192 + 2 * q] | (uint64_t)raw[193 + 2 * q] << 32;
-        a = a < n ? a : n;
-        b = b < n ? b : n;
-        const uint32_t over = b < a ? 1u : (b - a > (uint32_t)kTS ? b - a - (uint32_t)kTS : 0u);
-        if (over)
-          __hip_atomic_fetch_add(GW(T.fail) + q, (unsigned long long)over, __ATOMIC_RELAXED,
-                                 __HIP_MEMORY_SCOPE_AGENT);
-        const uint32_t len = b > a ? (b - a < (uint32_t)kTS ? b - a : (uint32_t)kTS) : 0u;
-        pln[lane] = len;
-        pkp[lane] = kp + 8ull * a;
-        pvp[lane] = vp + (uint64_t)sizeof(V) * a;
-        nr = (len + 63u) >> 6;
-      }
-      const uint32_t x = wave_scan_incl(nr);
-      if (lane < kGroup) rpre[lane + 1] = x;
-      if (lane == 0) rpre[0] = 0;
-    }
-  };
   // ---- D keys, continued sums: thread t owns slots 4t..4t+3
   const uint32_t s0 = 4u * (uint32_t)tid;
   const uint32_t* Bg = T.bt;
@@ -397,13 +293,9 @@ __global__ __launch_bounds__(nt_of(kGroup), (occupancy<V, M, kGroup>())) void ti
     if (Bg && w < (uint32_t)kNB / 512u)
       dma16((const char*)Bg + 1024u * w + 16u * (uint32_t)lane, (char*)bt32 + 1024u * w);
   };
-  // the wave that builds the table issues its D share after its wait for the
-  // table's loads, so that wait does not wait for D
-  constexpr uint32_t wtab = kP ? (uint32_t)kNW - 1u : 0u;
-  if (dma && w != wtab) issue_dma();
-  if constexpr (kP) tables_from_raw();
-  else if (np) load_tables(0);
-  if (dma && w == wtab) issue_dma();
+  if (dma && w != 0) issue_dma();
+  if (np) load_tables(0);
+  if (dma && w == 0) issue_dma();  // after wave 0's table loads: its wait for them does not wait for D
   // through registers (partial or unaligned tiles): loaded and installed
   // on this branch only, so no load of it is pending where the LDS-DMA
   // path rejoins (a pending one would make the compiler wait for all, D's
@@ -545,11 +437,6 @@ __global__ __launch_bounds__(nt_of(kGroup), (occupancy<V, M, kGroup>())) void ti
     }
   };
   if (U) load_pass();
-  // kP: the next tile's push table, behind this tile's element loads (its
-  // descriptor's scalar loads then wait beside them, not before barrier (1));
-  // raw[] was read before barrier (1)
-  if constexpr (kP)
-    if (w == (uint32_t)kNW - 1u && ti + t_step < t_last) fetch_raw(ti + t_step);
   if (dma) {  // (1b) D and the bucket table landed (with the element loads)
     dma_wait();
     __syncthreads();
@@ -672,20 +559,10 @@ __global__ __launch_bounds__(nt_of(kGroup), (occupancy<V, M, kGroup>())) void ti
       if ((uint32_t)r < nrw) {
         const uint64_t k = ek[r];
         const uint32_t b = bucket(k);
-#if PSG_WIN128
-        // the window from the even slot at or below the bucket start: two
-        // aligned 16-B reads (4 LDS cycles each) instead of two read2_b64
-        // (8 each); the slot below the start, when read, is a smaller bucket's
-        // key (the bucket map is monotone), so it counts below k and never
-        // equals it
-        const uint32_t l = bt[b] & ~1u;
-        const u64x2 wa = *(const u64x2*)(dk + l), wb = *(const u64x2*)(dk + l + 2);
-        const uint64_t k0 = wa.x, k1 = wa.y, k2 = wb.x, k3 = wb.y;
-#else
         const uint32_t l = bt[b];
+        const uint32_t n = (uint32_t)bt[b + 1] - l;
         const uint64_t* wk = dk + l;
         const uint64_t k0 = wk[0], k1 = wk[1], k2 = wk[2], k3 = wk[3];
-#endif
         const uint32_t c = (uint32_t)(k0 < k) + (uint32_t)(k1 < k) + (uint32_t)(k2 < k) +
                            (uint32_t)(k3 < k);
         const uint32_t p = l + c;
@@ -695,9 +572,7 @@ __global__ __launch_bounds__(nt_of(kGroup), (occupancy<V, M, kGroup>())) void ti
                             __ballot(k3 == k);
         const bool hit = ((eq >> lane) & 1ull) && p < nt;
         fd |= (uint32_t)hit << r;
-        // (reading the bucket's end only where the window is exhausted
-        // measured 3 % slower: profiles/r06_ab_window.txt)
-        deep |= (uint32_t)(c == 4u && (uint32_t)bt[b + 1] > l + 4u) << r;
+        deep |= (uint32_t)(c == 4u && n > 4u) << r;
       }
     }
     if (__ballot(deep != 0u)) {  // long buckets: bisect the rest of the bucket
@@ -706,7 +581,7 @@ __global__ __launch_bounds__(nt_of(kGroup), (occupancy<V, M, kGroup>())) void ti
         if ((deep >> r) & 1u) {
           const uint64_t k = ek[r];
           const uint32_t b = bucket(k);
-          uint32_t l = (PSG_WIN128 ? bt[b] & ~1u : bt[b]) + 4u;
+          uint32_t l = bt[b] + 4u;
           uint32_t n = (uint32_t)bt[b + 1] - l;
           while (n > 0u) {
             const uint32_t half = n >> 1;
@@ -833,60 +708,45 @@ __global__ __launch_bounds__(nt_of(kGroup), (occupancy<V, M, kGroup>())) void ti
   // and once either happened later adds keep the result, so the fold over
   // the present values followed by ONE +0.0 iff some push lacked the key is
   // bit-identical to the reference's dense fold
-  // slots u0..u0+3 of the tile out
-  auto store4 = [&](uint32_t u0) {
-    V res[M][4];
+  V res[M][4];
 #pragma unroll
-    for (int j = 0; j < 4; ++j) {
-      const uint32_t ncontrib = kFuse   ? cnt32[2u * (u0 + j) + 1u]
-                                : kCntW ? cnt32[u0 + j]
-                                        : (uint32_t)((const uint16_t*)cnt32)[u0 + j];
-      const bool gap = !parallel && ncontrib != np;
-#pragma unroll
-      for (int mi = 0; mi < M; ++mi) {
-        const V a = ACC(mi, u0 + j);
-        res[mi][j] = gap ? a + V(0) : a;
-      }
-    }
+  for (int j = 0; j < 4; ++j) {
+    const uint32_t ncontrib = kFuse   ? cnt32[2u * (s0 + j) + 1u]
+                              : kCntW ? cnt32[s0 + j]
+                                      : (uint32_t)((const uint16_t*)cnt32)[s0 + j];
+    const bool gap = !parallel && ncontrib != np;
 #pragma unroll
     for (int mi = 0; mi < M; ++mi) {
-      V* o = (V*)T.out[mi] + T.slot0 + u0;
-      if (u0 + 3u < nt && ((uintptr_t)o & 15u) == 0u) {
-        if constexpr (sizeof(V) == 4) {
-          typedef float f4 __attribute__((ext_vector_type(4)));
-          const f4 v = {res[mi][0], res[mi][1], res[mi][2], res[mi][3]};
-          __builtin_nontemporal_store(v, (AS1 f4*)GW(o));
-        } else {
-          typedef double d2 __attribute__((ext_vector_type(2)));
-          const d2 v0 = {res[mi][0], res[mi][1]};
-          const d2 v1 = {res[mi][2], res[mi][3]};
-          __builtin_nontemporal_store(v0, (AS1 d2*)GW(o));
-          __builtin_nontemporal_store(v1, (AS1 d2*)GW(o) + 1);
-        }
-      } else {
-#pragma unroll
-        for (int j = 0; j < 4; ++j)
-          if (u0 + j < nt) GW(o)[j] = res[mi][j];
-      }
+      const V a = ACC(mi, s0 + j);
+      res[mi][j] = gap ? a + V(0) : a;
     }
-  };
-  if constexpr (kP) {
-    // waves 0..kNW-2 store every slot (the table wave stores none)
-    if (w < (uint32_t)kNW - 1u)
-      for (uint32_t u = (uint32_t)tid; u < (uint32_t)kNT; u += 64u * (kNW - 1)) store4(4u * u);
-  } else {
-    store4(s0);
+  }
+#pragma unroll
+  for (int mi = 0; mi < M; ++mi) {
+    V* o = (V*)T.out[mi] + T.slot0 + s0;
+    if (s0 + 3u < nt && ((uintptr_t)o & 15u) == 0u) {
+      if constexpr (sizeof(V) == 4) {
+        typedef float f4 __attribute__((ext_vector_type(4)));
+        const f4 v = {res[mi][0], res[mi][1], res[mi][2], res[mi][3]};
+        __builtin_nontemporal_store(v, (AS1 f4*)GW(o));
+      } else {
+        typedef double d2 __attribute__((ext_vector_type(2)));
+        const d2 v0 = {res[mi][0], res[mi][1]};
+        const d2 v1 = {res[mi][2], res[mi][3]};
+        __builtin_nontemporal_store(v0, (AS1 d2*)GW(o));
+        __builtin_nontemporal_store(v1, (AS1 d2*)GW(o) + 1);
+      }
+    } else {
+#pragma unroll
+      for (int j = 0; j < 4; ++j)
+        if (s0 + j < nt) GW(o)[j] = res[mi][j];
+    }
   }
   PH(6);
-  // kP: every store has read the sums before the next tile clears them (and
-  // every wave is past the tile's LDS before the next D lands in it)
-  if constexpr (kP) lds_barrier();
-  PH(7);
 #ifdef PSG_PHASES
   if (tid == 0 && ti < (uint32_t)kPhTiles)
     for (int i = 0; i < 8; ++i) g_phase[ti][i] = ph_acc[i];
 #endif
-  }  // tiles of the run
 }
 
 // The bucket table of every tile, from D alone (a plan's resident index,
@@ -959,38 +819,8 @@ __global__ __launch_bounds__(kTSl / 4) void bucket_index_kernel(
 #define PSG_PAD_LDS 0  // diagnostic A/B builds only: dynamic LDS per workgroup that
                        // lowers the workgroups per CU at unchanged code
 #endif
-int cu_count() {
-  static const int ncu = [] {
-    int dev = 0, n = 0;
-    if (hipGetDevice(&dev) != hipSuccess ||
-        hipDeviceGetAttribute(&n, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || n <= 0)
-      n = 256;
-    return n;
-  }();
-  return ncu;
-}
-
 template <typename V, int M>
 hipError_t go(const TileDesc* t, uint32_t n, int form, hipStream_t s) {
-  if (form == 2) {
-    if constexpr (M == 1) {
-      // persistent: the workgroups the chip holds at once (LDS and register
-      // occupancy), a multiple of 8 for the XCD-major run order
-      static const int per = [] {  // workgroups per CU, as the hardware admits them
-        int b = 0;
-        if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&b, tile_kernel<V, 1, 32, true>, nt_of(32),
-                                                         0) != hipSuccess || b <= 0)
-          b = 1;
-        return b;
-      }();
-      uint32_t g = (uint32_t)(per * cu_count()) & ~7u;
-      if (g == 0) g = 8;
-      if (n < g) g = (n + 7u) & ~7u;
-      hipLaunchKernelGGL((tile_kernel<V, 1, 32, true>), dim3(g), dim3(nt_of(32)), 0, s, t, n);
-      return hipGetLastError();
-    }
-    return hipErrorInvalidValue;
-  }
   if (form == 1)
     hipLaunchKernelGGL((tile_kernel<V, M, 64>), dim3(n), dim3(nt_of(64)), PSG_PAD_LDS, s, t, n);
   else
