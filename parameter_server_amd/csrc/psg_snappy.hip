@@ -42,6 +42,9 @@
 #include "psg_internal.h"
 
 #define AS1 __attribute__((address_space(1)))
+#ifndef PSG_SNAPPY_IR
+#define PSG_SNAPPY_IR 1  // A/B: 0 = launches of few parts take snappy_kernel too
+#endif
 #ifndef PSG_SNAPPY_PREFETCH
 #define PSG_SNAPPY_PREFETCH 1  // A/B: 0 = no L2 prefetch of the parts
 #endif
@@ -426,6 +429,418 @@ __global__ __launch_bounds__(64) void snappy_kernel(const uint8_t* __restrict__ 
   }
 }
 
+// ---------------------------------------------------------------------------
+// The streamed form (launches of few parts: a message's, the compressed-push
+// path).  r06 parse clocks of one cfg2 value part (512 KB, 176 elements,
+// profiles/r06_snappy_parse_clocks.json): ~540 K clocks per part, the parse
+// waiting on a global round trip per element -- its window refills, its
+// inline literals read 64 B at a time from memory, copies whose source lies
+// in deferred literals read byte by byte from memory, and the output ring
+// (indexed by output position) flushed every few KB of output even though
+// the deferred literals put almost no bytes in it: each flush's stores then
+// hold vmcnt for the next load.  Here:
+//   * the part's compressed bytes stream into a 128 KB LDS ring by LDS-DMA
+//     (1 KB per wave instruction, up to 63 KB ahead of the parse; counted
+//     vmcnt waits), so tags, inline literals and the input bytes behind
+//     deferred pieces are LDS reads;
+//   * the output bytes the parse produces itself (short literals, copies)
+//     are APPENDED to a 16 KB LDS stage with a map (output position, stage
+//     offset, length), written out only when the stage fills and at the
+//     part's end -- a long-literal part flushes once;
+//   * a copy's source byte comes from the input ring (inside a deferred
+//     piece), the stage, or (rare: written out already) memory.
+// One part per workgroup, one workgroup per CU (LDS); deferral and the
+// copy kernel as in snappy_kernel.
+constexpr uint32_t kIRB = 128u << 10;   // input ring bytes
+constexpr uint32_t kIRC = kIRB >> 10;   // input ring chunks (1 KB each)
+constexpr uint32_t kLA = 48;            // chunks issued ahead of the parse position's chunk
+constexpr uint32_t kSkip = 4;           // a tag this many chunks past the issued front restarts the stream
+constexpr uint32_t kRestart = 16u << 10;  // a deferred literal this long restarts the stream past it
+constexpr uint32_t kSB = 16u << 10;     // output stage bytes
+constexpr uint32_t kMaxSt = 512;        // staged elements
+constexpr uint32_t kIRBigLit = 512;     // literals deferred to the copy kernel
+
+typedef __attribute__((address_space(3))) void* LdsPtr;
+// 16 B per lane from global memory into LDS: lane l writes lds + 16 l (M0
+// saved and restored; the compiler does not see the load, every reader
+// waits for it explicitly)
+__device__ __forceinline__ void ir_dma16(const void* g, const void* lds) {
+  const uint32_t la = __builtin_amdgcn_readfirstlane((uint32_t)(uintptr_t)(LdsPtr)lds);
+  uint32_t keep;
+  asm volatile(
+      "s_mov_b32 %0, m0\n\ts_mov_b32 m0, %2\n\ts_nop 0\n\t"
+      "global_load_lds_dwordx4 %1, off\n\ts_mov_b32 m0, %0"
+      : "=&s"(keep)
+      : "v"(g), "s"(la)
+      : "memory");
+}
+// wait until at most ~n of this wave's vector-memory operations are
+// outstanding (n rounded down to a step: waiting for more is safe, they
+// complete in issue order); returns the step
+#define IRW(k) else if (n >= k##u) { asm volatile("s_waitcnt vmcnt(" #k ")" ::: "memory"); return k##u; }
+__device__ __forceinline__ uint32_t ir_wait(uint32_t n) {
+  if (n >= 63u) { asm volatile("s_waitcnt vmcnt(63)" ::: "memory"); return 63u; }
+  IRW(60) IRW(56) IRW(52) IRW(48) IRW(44) IRW(40) IRW(36) IRW(32) IRW(28) IRW(24) IRW(20)
+  IRW(16) IRW(14) IRW(12) IRW(10) IRW(8) IRW(7) IRW(6) IRW(5) IRW(4) IRW(3) IRW(2) IRW(1)
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  return 0u;
+}
+#undef IRW
+
+__global__ __launch_bounds__(64) void snappy_ir_kernel(const uint8_t* __restrict__ src,
+                                                       const uint64_t* __restrict__ soff,
+                                                       uint8_t* __restrict__ dst,
+                                                       const uint64_t* __restrict__ doff,
+                                                       const uint64_t* __restrict__ dcap,
+                                                       uint64_t nmsg, int32_t* __restrict__ status,
+                                                       SnappyLit* __restrict__ lits,
+                                                       uint32_t* __restrict__ nlits,
+                                                       uint32_t lit_cap,
+                                                       unsigned long long* __restrict__ nbad,
+                                                       int pairs) {
+  __shared__ __attribute__((aligned(16))) uint8_t ir[kIRB];
+  __shared__ __attribute__((aligned(16))) uint8_t sb[kSB];
+  __shared__ uint32_t so[kMaxSt], ss[kMaxSt], sl[kMaxSt];   // staged: output pos, stage offset, length
+  __shared__ uint32_t tdst[kMaxDef], tsrc[kMaxDef], tlen[kMaxDef];  // deferred pieces
+  const uint32_t lane = threadIdx.x;
+  for (uint64_t msg = blockIdx.x; msg < nmsg; msg += gridDim.x) {
+    const AS1 uint8_t* const s0 =
+        (const AS1 uint8_t*)(pairs ? (const uint8_t*)soff[2 * msg] : src + soff[msg]);
+    const uint64_t slen = pairs ? soff[2 * msg + 1] - soff[2 * msg] : soff[msg + 1] - soff[msg];
+    AS1 uint8_t* const out = (AS1 uint8_t*)(dst + doff[msg]);
+    const uint64_t cap = dcap ? dcap[msg] : doff[msg + 1] - doff[msg];
+    if (slen == 0) {
+      if (lane == 0) status[msg] = cap == 0 ? 0 : PSG_ERR_SIZE;
+      continue;
+    }
+    if (slen >= (1ull << 31)) {
+      if (lane == 0) status[msg] = PSG_ERR_ARG;
+      continue;
+    }
+    const uint32_t e = (uint32_t)slen;
+    int32_t st = 0;
+#ifdef PSG_SNAPPY_PROF
+    unsigned long long sp[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+    const unsigned long long sp_part = clock64();
+#endif
+    // ---- the input ring: input position q is byte q + mis of the 16-B
+    // aligned stream, in chunk (q + mis) >> 10
+    const uint32_t mis = (uint32_t)((uintptr_t)s0 & 15u);
+    const AS1 uint8_t* const A = s0 - mis;
+    const uint32_t nch = (e + mis + 1023u) >> 10;
+    uint32_t lo = 0, iss = 0, wt = 0;  // chunks [lo, iss) issued since a restart, [lo, wt) landed
+    auto issue = [&](uint32_t c) {
+      const uint32_t u = 64u * c + lane;  // 16-B unit of the aligned stream
+      if (16u * u < e + mis) ir_dma16((const void*)(A + 16u * u), &ir[(c << 10) & (kIRB - 1u)]);
+    };
+    // issue up to `ahead` chunks past the parse chunk pc: kLA while the
+    // elements are short (value parts of floats: ~3 KB literals), 2 after a
+    // deferred literal of >= kRestart bytes (key parts, incompressible
+    // parts: the stream restarts past each one instead of carrying its
+    // bytes through the ring)
+    uint32_t ahead = kLA;
+    auto topup = [&](uint32_t pc) {
+      const uint32_t capc = pc + ahead + 1u < nch ? pc + ahead + 1u : nch;
+#ifdef PSG_SNAPPY_PROF
+      const unsigned long long _t0 = clock64();
+#endif
+      while (iss < capc) issue(iss++);
+#ifdef PSG_SNAPPY_PROF
+      sp[5] += clock64() - _t0;  // (r06 diagnostic: issue clocks in the literal slot)
+#endif
+    };
+    auto land = [&](uint32_t c) {
+      if (c < wt) return;
+      SP_T0();
+#ifdef PSG_SNAPPY_PROF
+      sp[3] += 1;
+#endif
+      wt = iss - ir_wait(iss - 1u - c);
+      SP_ADD(0);
+    };
+    auto resident = [&](uint32_t c) -> bool { return c >= lo && c < iss && c + kIRC >= iss; };
+    // input bytes [a, b] (b - a < 63 KB) resident and landed; the stream
+    // restarts at a's chunk when it lies far past the issued front (a long
+    // deferred literal skipped).  false: read them from memory
+    // the stream restarted at chunk ca (past a long deferred literal: its
+    // bytes are not streamed through the ring).  The old stream's DMAs still
+    // in flight hold the slots of chunks iss-63 .. iss-1: the new chunks
+    // ca .. ca+kLA reuse none of them unless the jump is long
+    auto restart = [&](uint32_t ca) {
+      if (ca - iss + kLA + 64u > kIRC) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      lo = iss = wt = ca;
+    };
+    auto ensure = [&](uint32_t a, uint32_t b) -> bool {
+      const uint32_t ca = (a + mis) >> 10, cb = (b + mis) >> 10;
+      if (ca < lo) return false;
+      if (cb >= iss + kSkip) restart(ca);
+      topup(ca);
+      if (!resident(ca) || !resident(cb)) return false;
+      land(cb);
+      return true;
+    };
+    auto irb = [&](uint32_t q) -> uint32_t { return ir[(q + mis) & (kIRB - 1u)]; };
+    // one input byte q behind the parse (deferred-piece sources)
+    auto inb = [&](uint32_t q) -> uint32_t {
+      const uint32_t c = (q + mis) >> 10;
+      return resident(c) && c < wt ? irb(q) : (uint32_t)s0[q];
+    };
+    uint32_t lp = 0xffffffffu - 64u, la = 0;
+    auto ub = [&](uint32_t q) -> uint32_t {
+      if (q - lp >= 64u) {
+#ifdef PSG_SNAPPY_PROF
+        const unsigned long long _u0 = clock64();
+#endif
+        const uint32_t q1 = q + 63u < e ? q + 63u : e - 1u;
+        lp = q;
+        la = ensure(q, q1) ? irb(q + lane) : (q + lane < e ? (uint32_t)s0[q + lane] : 0u);
+#ifdef PSG_SNAPPY_PROF
+        (void)__builtin_amdgcn_readfirstlane((int)la);
+        sp[7] += clock64() - _u0;  // r06 diagnostic: lookahead loads in the end slot
+#endif
+      }
+      return (uint32_t)__builtin_amdgcn_readlane((int)la, (int)(q - lp));
+    };
+    uint64_t ulen = 0;
+    bool done = false;
+    uint32_t p = 0;
+    while (p < 5 && p < e && !done) {
+      const uint32_t b = ub(p);
+      ulen |= (uint64_t)(b & 0x7f) << (7 * p);
+      done = !(b & 0x80);
+      ++p;
+    }
+    if (!done || ulen > 0xffffffffull) st = PSG_ERR_ARG;
+    if (!st && ulen != cap) st = PSG_ERR_SIZE;
+    const uint32_t ucap = (uint32_t)ulen;
+    uint32_t o = 0;
+    // deferred pieces (output order); [dlo, dhi) spans them all
+    uint32_t nd = 0, dlo = 0xffffffffu, dhi = 0;
+    // the stage: nst elements, nsb bytes; output below fo that is neither
+    // staged nor deferred is in memory
+    uint32_t nst = 0, nsb = 0, fo = 0;
+    bool wrote = false;  // stores since the last fence (a read of memory waits for them)
+    auto flush_stage = [&]() {
+      __builtin_amdgcn_wave_barrier();
+      for (uint32_t i = 0; i < nst; ++i) {
+        const uint32_t d = so[i], s = ss[i], n = sl[i];
+        for (uint32_t l = lane; l < n; l += 64) out[d + l] = sb[s + l];
+      }
+      wrote = wrote || nst > 0;
+      nst = 0;
+      nsb = 0;
+      fo = o;
+      __builtin_amdgcn_wave_barrier();
+    };
+    // room in the stage for n bytes (n <= kSB) and one element
+    auto room = [&](uint32_t n) {
+      if (nsb + n > kSB || nst == kMaxSt) flush_stage();
+    };
+    auto add_stage = [&](uint32_t n) {  // the n bytes just written at sb[nsb]
+      if (lane == 0) {
+        so[nst] = o;
+        ss[nst] = nsb;
+        sl[nst] = n;
+      }
+      __builtin_amdgcn_wave_barrier();
+      ++nst;
+      nsb += n;
+      o += n;
+    };
+    // last deferred piece / staged element starting at or before x (-1: none)
+    auto find_def = [&](uint32_t x) -> int {
+      if (nd && tdst[nd - 1] <= x) return (int)nd - 1;
+      int l0 = -1, hi = (int)nd;
+      while (hi - l0 > 1) {
+        const int mid = (l0 + hi) >> 1;
+        if (tdst[mid] <= x) l0 = mid; else hi = mid;
+      }
+      return l0;
+    };
+    auto find_st = [&](uint32_t x) -> int {
+      if (nst && so[nst - 1] <= x) return (int)nst - 1;
+      int l0 = -1, hi = (int)nst;
+      while (hi - l0 > 1) {
+        const int mid = (l0 + hi) >> 1;
+        if (so[mid] <= x) l0 = mid; else hi = mid;
+      }
+      return l0;
+    };
+    auto defer = [&](uint32_t len, uint32_t in) {
+#ifdef PSG_SNAPPY_PROF
+      sp[4] += 1;
+#endif
+      if (lane == 0) {
+        tdst[nd] = o;
+        tsrc[nd] = in;
+        tlen[nd] = len;
+      }
+      __builtin_amdgcn_wave_barrier();
+      ++nd;
+      dlo = dlo < o ? dlo : o;
+      o += len;
+      dhi = o;
+    };
+    while (!st && p < e) {
+#ifdef PSG_SNAPPY_PROF
+      sp[6] += 1;
+#endif
+      topup((p + mis) >> 10);  // keep the stream kLA chunks ahead
+      const uint32_t tag = ub(p++);
+      uint32_t len, off;
+      if ((tag & 3u) == 0u) {  // literal
+        len = (tag >> 2) + 1u;
+        if (len > 60u) {
+          const uint32_t n = len - 60u;
+          if (e - p < n) { st = PSG_ERR_ARG; break; }
+          len = 0;
+          for (uint32_t b = 0; b < n; ++b) len |= ub(p + b) << (8 * b);
+          p += n;
+          if (len == 0xffffffffu) { st = PSG_ERR_ARG; break; }
+          len += 1u;
+        }
+        if (e - p < len || ucap - o < len) { st = PSG_ERR_ARG; break; }
+        if (lits && len >= kIRBigLit && nd < kMaxDef) {
+          defer(len, p);
+          p += len;
+          if (len >= kRestart) {
+            ahead = 2u;
+            if (((p + mis) >> 10) >= iss && p < e) restart((p + mis) >> 10);
+          } else {
+            ahead = kLA;
+          }
+          continue;
+        }
+        ahead = kLA;
+        // staged in pieces of <= 4 KB (from the input ring, or memory)
+        for (uint32_t c = 0; c < len; c += 4096u) {
+          const uint32_t n = len - c < 4096u ? len - c : 4096u;
+          const bool inr = ensure(p + c, p + c + n - 1u);
+          room(n);
+          if (inr) {
+            for (uint32_t l = lane; l < n; l += 64) sb[nsb + l] = (uint8_t)irb(p + c + l);
+          } else {
+            for (uint32_t l = lane; l < n; l += 64) sb[nsb + l] = s0[p + c + l];
+          }
+          add_stage(n);
+        }
+        p += len;
+        continue;
+      }
+      if ((tag & 3u) == 1u) {
+        if (e - p < 1) { st = PSG_ERR_ARG; break; }
+        len = 4u + ((tag >> 2) & 7u);
+        off = (tag >> 5) << 8 | ub(p);
+        p += 1;
+      } else if ((tag & 3u) == 2u) {
+        if (e - p < 2) { st = PSG_ERR_ARG; break; }
+        len = 1u + (tag >> 2);
+        off = ub(p) | ub(p + 1) << 8;
+        p += 2;
+      } else {
+        if (e - p < 4) { st = PSG_ERR_ARG; break; }
+        len = 1u + (tag >> 2);
+        off = ub(p) | ub(p + 1) << 8 | ub(p + 2) << 16 | ub(p + 3) << 24;
+        p += 4;
+      }
+      if (off == 0 || off > o || ucap - o < len) { st = PSG_ERR_ARG; break; }
+      // len <= 64: one step; source byte of lane l is output o - off + (l mod off)
+      const uint32_t slo = o - off;
+      SP_T0();
+      if (nd && slo < dhi && slo + (len < off ? len : off) > dlo) {
+        // wholly inside one deferred piece (and clear of its own output):
+        // deferred too, as that piece's input bytes
+        const int j = find_def(slo);
+        if (j >= 0 && off >= len && slo - tdst[j] + len <= tlen[j] && nd < kMaxDef) {
+          SP_ADD(1);
+          defer(len, tsrc[j] + (slo - tdst[j]));
+          continue;
+        }
+      }
+      const uint32_t li = off >= 64u ? lane : lane % off;
+      const uint32_t pos = slo + li;
+      // where this lane's source byte is: 0 deferred piece (input), 1 the
+      // stage, 2 memory (written out).  Usually the whole source span
+      // [slo, shi) lies in one staged element or one deferred piece: one
+      // uniform lookup then
+      const uint32_t shi = slo + (len < off ? len : off);
+      uint32_t where = 2u, at = 0u;
+      bool one = false;
+      {
+        const int js = nst && slo >= fo ? find_st(slo) : -1;
+        if (js >= 0 && shi - so[js] <= sl[js]) {
+          one = true;
+          where = 1u;
+          at = ss[js] + (pos - so[js]);
+        } else if (nd && slo >= dlo && slo < dhi) {
+          const int jd = find_def(slo);
+          if (jd >= 0 && shi - tdst[jd] <= tlen[jd]) {
+            one = true;
+            where = 0u;
+            at = tsrc[jd] + (pos - tdst[jd]);
+          }
+        }
+      }
+      if (!one && lane < len) {
+        const int jd = nd && pos < dhi && pos >= dlo ? find_def(pos) : -1;
+        if (jd >= 0 && pos - tdst[jd] < tlen[jd]) {
+          where = 0u;
+          at = tsrc[jd] + (pos - tdst[jd]);
+        } else {
+          const int js = nst && pos >= fo ? find_st(pos) : -1;
+          if (js >= 0 && pos - so[js] < sl[js]) {
+            where = 1u;
+            at = ss[js] + (pos - so[js]);
+          } else {
+            at = pos;
+          }
+        }
+      }
+      if (wrote && __ballot(lane < len && where == 2u)) {
+        // bytes written out earlier by this wave: visible to its loads
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        __threadfence();
+        wrote = false;
+      }
+      const uint32_t b = lane < len ? (where == 0u ? inb(at) : where == 1u ? (uint32_t)sb[at]
+                                                                         : (uint32_t)out[at])
+                                    : 0u;
+      SP_ADD(1);
+      room(len);
+      if (lane < len) sb[nsb + lane] = (uint8_t)b;
+      add_stage(len);
+    }
+#ifdef PSG_SNAPPY_PROF
+    const unsigned long long sp_end = clock64();
+#endif
+    if (!st && o != ucap) st = PSG_ERR_ARG;
+    if (!st) flush_stage();
+    if (!st && nd) {
+      uint32_t base = 0;
+      if (lane == 0) base = atomicAdd(nlits, nd);
+      base = (uint32_t)__builtin_amdgcn_readfirstlane((int)base);
+      for (uint32_t i = lane; i < nd; i += 64)
+        if (base + i < lit_cap)
+          lits[base + i] = SnappyLit{(const uint8_t*)(s0 + tsrc[i]), (uint8_t*)(out + tdst[i]), tlen[i]};
+      for (uint32_t i = (base < lit_cap ? lit_cap - base : 0u); i < nd; ++i)
+        for (uint32_t b = lane; b < tlen[i]; b += 64) out[tdst[i] + b] = s0[tsrc[i] + b];
+    }
+    if (lane == 0) {
+      status[msg] = st;
+      if (st && nbad) atomicAdd(nbad, 1ull);
+    }
+    // every DMA of this part has landed before the next part reuses the ring
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+#ifdef PSG_SNAPPY_PROF
+    sp[2] = clock64() - sp_part;
+    (void)sp_end;
+    if (lane == 0 && msg < 4096)
+      for (int i = 0; i < 8; ++i) g_sprof[msg][i] = sp[i];
+#endif
+    __builtin_amdgcn_wave_barrier();
+  }
+}
+
 // The deferred literals, chip-wide: a literal is cut into 16-B units
 // aligned to its destination; a workgroup moves 256 units (4 KB) per chunk,
 // chunks numbered across literals and dealt round-robin to the grid (the
@@ -543,9 +958,15 @@ hipError_t launch_snappy(const uint8_t* src, const uint64_t* soff, uint64_t nmsg
   constexpr uint64_t kPerCU = 163840ull / kLdsPerPart > 0 ? 163840ull / kLdsPerPart : 1;
   const uint64_t grid_cap = 256ull * kPerCU;
   const uint64_t blocks = nmsg < grid_cap ? nmsg : grid_cap;
-  hipLaunchKernelGGL(snappy_kernel, dim3((uint32_t)blocks), dim3(64), 0, stream, src, soff, dst,
-                     doff, dcap, nmsg, status, nlits ? lits : nullptr, nlits, cap, nbad,
-                     pairs ? 1 : 0, nmsg <= kPrefetchParts ? PSG_SNAPPY_PREFETCH : 0);
+  if (PSG_SNAPPY_IR && nmsg <= kPrefetchParts)
+    // few parts (a message's): the streamed form, one part per CU
+    hipLaunchKernelGGL(snappy_ir_kernel, dim3((uint32_t)nmsg), dim3(64), 0, stream, src, soff, dst,
+                       doff, dcap, nmsg, status, nlits ? lits : nullptr, nlits, cap, nbad,
+                       pairs ? 1 : 0);
+  else
+    hipLaunchKernelGGL(snappy_kernel, dim3((uint32_t)blocks), dim3(64), 0, stream, src, soff, dst,
+                       doff, dcap, nmsg, status, nlits ? lits : nullptr, nlits, cap, nbad,
+                       pairs ? 1 : 0, nmsg <= kPrefetchParts ? PSG_SNAPPY_PREFETCH : 0);
   if (!nlits) return hipGetLastError();
   hipLaunchKernelGGL(snappy_lit_kernel, dim3(1024), dim3(256), 0, stream, lits, nlits, cap);
   return hipGetLastError();

@@ -1194,3 +1194,72 @@ def test_plan_packed_cursor_unsorted_push_is_reported(torch_cuda):
         mt = plan.matched().tolist()
         assert mt[9] < n[9] and mt[:9] == n[:9] and mt[10:] == n[10:]
         plan.close()
+
+
+def _stream_case(seed):
+    """Sparse pushes over a 2 M-slot D: ~10 keys per push per 1024 slots, so
+    the partition runs in stream mode (512-key chunks of each push)."""
+    rng = np.random.default_rng(seed)
+    D = np.unique(rng.integers(0, 1 << 50, 2_100_000, dtype=np.uint64))
+    pushes = []
+    for p in range(24):
+        k = np.sort(rng.choice(D, 20000, replace=False))
+        pushes.append((k, [rng.standard_normal(k.size).astype(np.float32)]))
+    return D, pushes
+
+
+def _swap_blocks(k):
+    """Two 4,096-key blocks swapped: unsorted across several 512-key chunks."""
+    k = k.copy()
+    a, b = slice(2048, 2048 + 4096), slice(12000, 12000 + 4096)
+    k[a], k[b] = k[b].copy(), k[a].copy()
+    return k
+
+
+def test_stream_partition_unsorted_push_across_chunks_plan(torch_cuda):
+    """the stream partition no longer order-checks; an unsorted
+    push (4 K-key blocks swapped, across chunk boundaries) must still be
+    reported by the aggregate kernel's order check and coverage.  The plan
+    runs once sorted (seg and the descriptors written), then the same push's
+    device keys are swapped in place and the plan re-runs on the stale seg
+    image: that push reported, the others exact."""
+    torch = torch_cuda
+    from parameter_server_amd._lib import PSG_PART_STREAM
+    D, pushes = _stream_case(61)
+    for parallel in (False, True):
+        plan, keep = plan_for(torch, [(D, pushes)], parallel=parallel, flags=PSG_PART_STREAM)
+        plan.run()
+        assert plan.matched().tolist() == [20000] * 24
+        _, _, _, want, _ = O.aggregate(D, *ALL, pushes, parallel=parallel)
+        assert_bitexact(keep[3][0].cpu().numpy()[: D.size], want[0])
+        bad = _swap_blocks(pushes[5][0])
+        keep[1][5].copy_(torch.from_numpy(bad.view(np.int64)).cuda())
+        plan.run()
+        mt = plan.matched().tolist()
+        assert mt[5] < 20000 and mt[:5] + mt[6:] == [20000] * 23
+        plan.close()
+
+
+def test_stream_partition_unsorted_push_across_chunks_context(torch_cuda):
+    """The same through the server API (context flushes, stream partition
+    forced): time 1 sorted (the flush's job tables and seg written), time 2
+    of the same shape with one push unsorted across chunks (the reused
+    descriptors, stale seg words): reported PSG_ERR_UNMATCHED; time 3 sorted
+    again is exact."""
+    from parameter_server_amd._lib import PSGError, PSG_ERR_UNMATCHED, PSG_PART_STREAM
+    D, pushes = _stream_case(62)
+    v = kvv(flags=PSG_PART_STREAM)
+    v.setValue(msg(D))
+    _, _, _, want, _ = O.aggregate(D, *ALL, pushes)
+    for t, unsorted in ((1, False), (2, True), (3, False)):
+        for p, (k, vals) in enumerate(pushes):
+            kk = _swap_blocks(k) if unsorted and p == 7 else k
+            v.setValue(msg(kk, vals, t=t))
+        if unsorted:
+            with pytest.raises(PSGError) as e:
+                v.received(t)
+            assert e.value.status == PSG_ERR_UNMATCHED
+        else:
+            (rng, a), = v.received(t)
+            assert_bitexact(a, want[0])
+    v.close()

@@ -745,3 +745,52 @@ def test_gpu_push_compressed_matches_plain_push():
     _, _, _, want, _ = O.aggregate(D, 0, (1 << 64) - 1, pushes[:2])
     assert np.array_equal(got.view(np.uint32), want[0].view(np.uint32))
     v.close()
+
+
+@pytest.mark.gpu
+def test_gpu_snappy_streamed_and_per_wave_forms_agree():
+    """Launches of <= 64 parts take the streamed decoder (the compressed
+    bytes stream through a 128 KB LDS ring; the parse's own output is staged
+    in LDS), larger launches the per-wave one: the same streams decoded both
+    ways, byte-exact against the spec oracle.  The streams mix long literals
+    (>= 16 KB: the stream restarts past each) with short literals and copies
+    that reach back across the restarts (into skipped input: read from
+    memory), into staged and into already written-out output, run-length
+    copies, 4-byte offsets, and parts starting at every 16-B phase."""
+    rng = np.random.default_rng(31)
+    parts, datas = [], []
+    for v in range(6):
+        el, o = [], 0
+        while o < 400_000:
+            kind = int(rng.integers(0, 6))
+            if kind == 0:
+                ln = int(rng.choice([16384, 20000, 65536, 70001]))
+            elif kind == 1:
+                ln = int(rng.integers(600, 4000))
+            else:
+                ln = int(rng.integers(1, 61))
+            el.append(("lit", rng.integers(0, 256, ln, dtype=np.uint8).tobytes()))
+            o += ln
+            for _ in range(int(rng.integers(0, 3))):
+                off = int(rng.integers(1, min(o, 150_000) + 1))
+                cl = int(rng.integers(1, 65))
+                el.append(("copy", off, cl))
+                o += cl
+        comp, want = _snappy_stream(el)
+        assert O.snappy_uncompress(comp) == want
+        parts.append(comp)
+        datas.append(want)
+    # odd-sized leading parts shift the later parts' 16-B phase
+    leads = [_snappy_stream([("lit", bytes(range(i + 1)))]) for i in range(5)]
+    streamed = [c for c, _ in leads] + parts
+    want_all = [d for _, d in leads] + datas
+    got, st = _gpu_snappy(streamed, [len(d) for d in want_all])
+    assert st == [0] * len(streamed)
+    assert all(g == d for g, d in zip(got, want_all))
+    # the same parts in a launch of 70 (> 64: the per-wave decoder)
+    filler = [_snappy_stream([("lit", bytes([i]) * 3)]) for i in range(70 - len(streamed))]
+    many = streamed + [c for c, _ in filler]
+    want_many = want_all + [d for _, d in filler]
+    got, st = _gpu_snappy(many, [len(d) for d in want_many])
+    assert st == [0] * len(many)
+    assert all(g == d for g, d in zip(got, want_many))

@@ -8,8 +8,15 @@ import json
 import sys
 
 
-def main(src, bpl, kernel="tile_kernel", out="profiles/pmc_summary.json", workload="cfg2"):
+def main(src, bpl, kernel="tile_kernel", out="profiles/pmc_summary.json", workload="cfg2",
+         tracked=None):
+    """tracked: the committed copy of `src` under profiles/ (the line's
+    traffic_source names it; gpurun_out/ is scratch)."""
     allc = json.load(open(src))["counters"]
+    if tracked:
+        import shutil
+        shutil.copyfile(src, tracked)
+        src = tracked
     d = allc[kernel]
     hbm = (2 * d["FETCH_SIZE"] + d["WRITE_SIZE"]) * 1024
     res = {"kernel": kernel, "workload": workload, "bytes_per_launch": int(bpl),
