@@ -182,7 +182,8 @@ __global__ __launch_bounds__(kNT) void crc_kernel(const uint8_t* __restrict__ da
 // against the carried signature; a mismatch counts into *bad (reported by
 // psg_received), so the host does not wait for it.  One wave.
 __global__ __launch_bounds__(64) void sig_kernel(const uint8_t* __restrict__ data, uint32_t len,
-                                                 uint32_t want, unsigned long long* bad) {
+                                                 uint32_t want, unsigned long long* bad,
+                                                 unsigned long long* bad2) {
   __shared__ uint32_t t[16][256];
   __shared__ uint32_t sh[4][256];
   __shared__ uint32_t x8[1024];
@@ -192,16 +193,19 @@ __global__ __launch_bounds__(64) void sig_kernel(const uint8_t* __restrict__ dat
   __syncthreads();
   const uint32_t raw = chunk_raw(data, len, threadIdx.x, t, sh, x8);
   const uint32_t got = raw ^ ~shift_bytes(~0u, len);  // Extend(0, data, len)
-  if (threadIdx.x == 0 && got != want) atomicAdd(bad, 1ull);
+  if (threadIdx.x == 0 && got != want) {
+    atomicAdd(bad, 1ull);
+    if (bad2) atomicAdd(bad2, 1ull);
+  }
 }
 
 }  // namespace
 
 hipError_t launch_sig_check(const uint8_t* data, uint64_t len, uint64_t max_len, uint32_t want,
-                            unsigned long long* bad, hipStream_t s) {
+                            unsigned long long* bad, hipStream_t s, unsigned long long* bad2) {
   const uint64_t l = len < max_len ? len : max_len;
   if (l > kChunk) return hipErrorInvalidValue;
-  hipLaunchKernelGGL(sig_kernel, dim3(1), dim3(64), 0, s, data, (uint32_t)l, want, bad);
+  hipLaunchKernelGGL(sig_kernel, dim3(1), dim3(64), 0, s, data, (uint32_t)l, want, bad, bad2);
   return hipGetLastError();
 }
 

@@ -245,9 +245,10 @@ uint64_t crc32c_chunks_per_segment(uint64_t max_len);
 hipError_t launch_crc32c(const uint8_t* data, const uint64_t* off, uint64_t nseg,
                          uint64_t max_len, const uint32_t* init, uint32_t* out,
                          hipStream_t stream);
-// *bad += 1 unless crc32c::Value(data, min(len, max_len)) == want (one
-// wave; max_len <= 64 KB)
+// *bad += 1 (and *bad2, when given) unless crc32c::Value(data,
+// min(len, max_len)) == want (one wave; max_len <= 64 KB)
 hipError_t launch_sig_check(const uint8_t* data, uint64_t len, uint64_t max_len, uint32_t want,
-                            unsigned long long* bad, hipStream_t stream);
+                            unsigned long long* bad, hipStream_t stream,
+                            unsigned long long* bad2 = nullptr);
 
 }  // namespace psg

@@ -859,7 +859,9 @@ struct CacheKey {
 // keys is restorable only once the check passed; the reference checks before
 // it stores (remote_node.cc:161-165).
 struct SigCheck {
-  unsigned long long* d = nullptr;
+  unsigned long long* d = nullptr;  // the device counter (a slot of a counter slab)
+  unsigned long long* h = nullptr;  // its pinned host copy, landed before `ev`
+  uint32_t slot = 0;
   hipEvent_t ev = nullptr;
 };
 using SigCheckRef = std::shared_ptr<SigCheck>;
@@ -959,6 +961,12 @@ struct psg_ctx {
   unsigned long long* d_small = nullptr;  // 32 device words: counters, crc args
   unsigned long long* d_vio_slots = nullptr;  // psg::kVioSlots x 64 B, zero between updates
   unsigned long long* h_small = nullptr;  // 32 pinned host words
+  // signature-check counters, pooled: slabs of kCtrSlab device
+  // words and as many pinned host words their results are copied back into;
+  // slot i lives in slab i / kCtrSlab
+  static constexpr uint32_t kCtrSlab = 256;
+  std::vector<unsigned long long*> ctr_d, ctr_h;
+  std::vector<uint32_t> ctr_free;
   void* scratch = nullptr;
   size_t scratch_bytes = 0;
   size_t flush_pushes = psg::kMaxPush;  // pushes per aggregate launch
@@ -1163,39 +1171,68 @@ struct psg_ctx {
   }
 
   // the carried signature of resident keys checked on `copy` into a counter
-  // of its own (the entry's), after the key copy
-  int sig_check_pending(const KeyRef& k, uint32_t sig, SigCheckRef* out) {
+  // of its own (the entry's), after the key copy, and -- one CRC for both
+  //  -- into the aggregate's signature counter `agg` when given
+  int ctr_get(uint32_t* slot) {
+    if (ctr_free.empty()) {
+      unsigned long long *d = nullptr, *h = nullptr;
+      HIP_TRY(hipMalloc((void**)&d, 8 * kCtrSlab));
+      if (hipHostMalloc((void**)&h, 8 * kCtrSlab) != hipSuccess) {
+        (void)hipFree(d);
+        return fail(PSG_ERR_DEVICE, "signature counter slab");
+      }
+      const uint32_t base = (uint32_t)ctr_d.size() * kCtrSlab;
+      ctr_d.push_back(d);
+      ctr_h.push_back(h);
+      for (uint32_t i = kCtrSlab; i-- > 0;) ctr_free.push_back(base + i);
+    }
+    *slot = ctr_free.back();
+    ctr_free.pop_back();
+    return PSG_OK;
+  }
+  void ctr_release() {
+    for (auto* d : ctr_d) (void)hipFree(d);
+    for (auto* h : ctr_h) (void)hipHostFree(h);
+    ctr_d.clear();
+    ctr_h.clear();
+    ctr_free.clear();
+  }
+  int sig_check_pending(const KeyRef& k, uint32_t sig, SigCheckRef* out,
+                        unsigned long long* agg = nullptr) {
     SigCheck* s = new SigCheck();
-    if (int rc = dev_get(8, (void**)&s->d, copy)) {
+    if (int rc = ctr_get(&s->slot)) {
       delete s;
       return rc;
     }
+    s->d = ctr_d[s->slot / kCtrSlab] + s->slot % kCtrSlab;
+    s->h = ctr_h[s->slot / kCtrSlab] + s->slot % kCtrSlab;
     int rc = event(&s->ev);
     if (rc == PSG_OK && (hipMemsetAsync(s->d, 0, 8, copy) != hipSuccess ||
                          psg::launch_sig_check((const uint8_t*)k->d, 8 * k->n, PSG_MAX_SIG_LEN,
-                                               sig, s->d, copy) != hipSuccess ||
+                                               sig, s->d, copy, agg) != hipSuccess ||
+                         hipMemcpyAsync(s->h, s->d, 8, hipMemcpyDeviceToHost, copy) != hipSuccess ||
                          hipEventRecord(s->ev, copy) != hipSuccess))
       rc = fail(PSG_ERR_DEVICE, "signature check launch");
     if (rc != PSG_OK) {
       (void)hipStreamSynchronize(copy);
       if (s->ev) free_ev.push_back(s->ev);
-      dev_put(s->d, 8);
+      ctr_free.push_back(s->slot);
       delete s;
       return rc;
     }
     *out = SigCheckRef(s, [this](SigCheck* q) {
-      (void)hipEventSynchronize(q->ev);  // the counter block is not reused under the check
+      (void)hipEventSynchronize(q->ev);  // the counter slot is not reused under the check
       free_ev.push_back(q->ev);
-      dev_put(q->d, 8);
+      ctr_free.push_back(q->slot);
       delete q;
     });
     return PSG_OK;
   }
-  // the result of a pending check (host wait, once per stored entry)
+  // the result of a pending check: a wait for its event (once per stored
+  // entry); the count is already in pinned host memory
   int sig_check_result(const SigCheckRef& s, bool* ok) {
     HIP_TRY(hipEventSynchronize(s->ev));
-    HIP_TRY(hipMemcpy(h_small + 11, s->d, 8, hipMemcpyDeviceToHost));
-    *ok = h_small[11] == 0;
+    *ok = *(volatile unsigned long long*)s->h == 0;
     return PSG_OK;
   }
 
@@ -1733,6 +1770,7 @@ int psg_destroy(psg_ctx* c) {
   c->fly.clear();
   c->table.release();
   c->pool_release();
+  c->ctr_release();
   if (c->ring) (void)hipHostFree(c->ring);
   (void)hipFree(c->d_small);
   (void)hipFree(c->d_vio_slots);
@@ -2302,10 +2340,8 @@ int push_cached_impl(psg_ctx* c, int sender, int chl, int time, uint64_t kb, uin
     // pending on that check: a restore waits for its result and fails (and
     // drops the entry) if it failed.  A key-only message merges into the
     // channel's keys at once, so it is checked before that
-    SigCheckRef pend;
     if (nkeys && m > 0) {
-      if (int rc = c->sig_check_pending(k, sig, &pend)) return rc;
-      sigcheck = true;
+      sigcheck = true;  // launched below, into the entry's and the aggregate's counters
       got = sig;
     } else if (nkeys) {
       c->h_small[8] = 0;
@@ -2322,7 +2358,7 @@ int push_cached_impl(psg_ctx* c, int sender, int chl, int time, uint64_t kb, uin
     CacheEntry& e = c->kcache[ck];
     e.sig = sig;
     e.keys = k;
-    e.chk = pend;
+    e.chk.reset();
   } else {
     // keys restored from the cache (remote_node.cc:172-176)
     auto it = c->kcache.find(ck);
@@ -2346,6 +2382,20 @@ int push_cached_impl(psg_ctx* c, int sender, int chl, int time, uint64_t kb, uin
                   chl, (unsigned long long)kb, (unsigned long long)ke, sig, have);
     if (it != c->kcache.end()) k = it->second.keys;
   }
+  // the stored entry's pending check (keys carried with values): ONE device
+  // CRC of the keys, counted into the entry's counter (a later restore waits
+  // for it) and into the aggregate's (psg_received reports a mismatch).  If
+  // the message is refused before its aggregate exists, the check still
+  // runs, into the entry's counter alone: the entry is never restorable
+  // unchecked
+  auto store_check = [&](unsigned long long* agg) -> int {
+    auto it = c->kcache.find(ck);
+    if (it == c->kcache.end() || it->second.keys != k) return PSG_OK;  // erased meanwhile
+    SigCheckRef pend;
+    if (int rc = c->sig_check_pending(k, sig, &pend, agg)) return rc;
+    it->second.chk = pend;
+    return PSG_OK;
+  };
   if (kc & PSG_KC_ERASE) c->kcache.erase(ck);  // remote_node.cc:183
   const size_t n = k ? k->n : 0;
   if (n == 0) return PSG_OK;  // kv_vector.h:90,177: no keys, message ignored
@@ -2353,15 +2403,25 @@ int push_cached_impl(psg_ctx* c, int sender, int chl, int time, uint64_t kb, uin
     // key-only message: setUnion with the (possibly restored) keys, on the device
     return key_union_impl(c, chl, {k->d}, {(uint64_t)n});
   }
-  if (nvals != n)  // CHECK_EQ(recv_data.size(), recv_key.size()) kv_vector.h:108,187
+  if (nvals != n) {  // CHECK_EQ(recv_data.size(), recv_key.size()) kv_vector.h:108,187
+    if (sigcheck) (void)store_check(nullptr);
     return fail(PSG_ERR_SIZE, "%zu values for %zu keys", nvals, n);
+  }
   size_t lo, hi;
-  if (int rc = check_push(c, chl, time, kb, ke, n, m, &lo, &hi)) return rc;
-  if (sigcheck) {  // into the aggregate's counters, on `copy` after the key copy
+  if (int rc = check_push(c, chl, time, kb, ke, n, m, &lo, &hi)) {
+    if (sigcheck) (void)store_check(nullptr);
+    return rc;
+  }
+  if (sigcheck) {  // on `copy` after the key copy
     Aggregate* A = nullptr;
-    if (int rc = c->aggregate_for(chl, time, kb, ke, m, &A)) return rc;
-    HIP_TRY(psg::launch_sig_check((const uint8_t*)k->d, 8 * n, PSG_MAX_SIG_LEN, sig, A->d_bad + 2,
-                                  c->copy));
+    if (int rc = c->aggregate_for(chl, time, kb, ke, m, &A)) {
+      (void)store_check(nullptr);
+      return rc;
+    }
+    if (int rc = store_check(A->d_bad + 2)) return rc;
+    if (!c->kcache.count(ck))  // the entry was erased (PSG_KC_ERASE): the aggregate's check alone
+      HIP_TRY(psg::launch_sig_check((const uint8_t*)k->d, 8 * n, PSG_MAX_SIG_LEN, sig,
+                                    A->d_bad + 2, c->copy));
   }
   return c->push_values(chl, time, kb, ke, k, m, vals);
 }

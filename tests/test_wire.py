@@ -296,12 +296,54 @@ def test_key_cache_bad_signature_is_never_restored():
     with pytest.raises(PSGError) as e:
         v.setValue(_msg(None, [x], t=3, sig=bad, has_key=False, sender=4))
     assert e.value.status == PSG_ERR_SIGNATURE
+    # stored and erased by the same message (:183): the one device check is
+    # still counted into the aggregate and reported by received(t)
+    v.setValue(_msg(k, [x], t=4, sig=bad, sender=6, erase=True))
+    assert v.key_cache_bytes(6) == 0
+    with pytest.raises(PSGError) as e:
+        v.received(4)
+    assert e.value.status == PSG_ERR_SIGNATURE
     # a good signature: stored pending, restored once its check passed
     good = O.key_signature(k)
     v.setValue(_msg(k, [x], t=5, sig=good, sender=5))
     v.setValue(_msg(None, [x], t=5, sig=good, has_key=False, sender=5))
     (_, got), = v.received(5)
     want = O.aggregate(D, 0, (1 << 64) - 1, [(k, [x])] * 2)[3][0]
+    assert np.array_equal(_bits(got), _bits(want))
+    v.close()
+
+
+@pytest.mark.gpu
+def test_key_cache_many_pending_checks_share_counter_slabs():
+    """More stored-pending entries than one counter slab holds (256): each
+    keeps its own pooled counter; one bad entry among them is caught at its
+    restore and the rest restore bit-exactly."""
+    import torch
+    assert torch.cuda.is_available()
+    from parameter_server_amd._lib import PSGError, PSG_ERR_SIGNATURE
+    rng = np.random.default_rng(21)
+    D = np.unique(rng.integers(0, 1 << 40, 4000, dtype=np.uint64))
+    v = _kvv()
+    v.setValue(_msg(D))
+    nsend, badsend = 300, 277
+    ks = [np.sort(rng.choice(D, 64, replace=False)) for _ in range(nsend)]
+    xs = [rng.standard_normal(64).astype(np.float32) for _ in range(nsend)]
+    for s in range(nsend):
+        sig = O.key_signature(ks[s]) ^ (1 if s == badsend else 0)
+        v.setValue(_msg(ks[s], [xs[s]], t=1, sig=sig, sender=s))
+    with pytest.raises(PSGError):
+        v.received(1)  # the bad one counted into the aggregate
+    for s in range(nsend):
+        sig = O.key_signature(ks[s]) ^ (1 if s == badsend else 0)
+        if s == badsend:
+            with pytest.raises(PSGError) as e:
+                v.setValue(_msg(None, [xs[s]], t=2, sig=sig, has_key=False, sender=s))
+            assert e.value.status == PSG_ERR_SIGNATURE
+        else:
+            v.setValue(_msg(None, [xs[s]], t=2, sig=sig, has_key=False, sender=s))
+    (_, got), = v.received(2)
+    want = O.aggregate(D, 0, (1 << 64) - 1,
+                       [(ks[s], [xs[s]]) for s in range(nsend) if s != badsend])[3][0]
     assert np.array_equal(_bits(got), _bits(want))
     v.close()
 
