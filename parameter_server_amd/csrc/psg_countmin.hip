@@ -523,7 +523,10 @@ __global__ __launch_bounds__(kQNT) void cm_qlook_kernel(const uint8_t* __restric
                                                         uint16_t* __restrict__ R2) {
   __shared__ __attribute__((aligned(16))) uint32_t tab[kQRegBytes / 4];
   __shared__ uint32_t seg[kQMaxBlocks];  // block b's run: start | length << 16
-  const uint32_t r = blockIdx.x, t = threadIdx.x;
+  // XCD-contiguous regions (as the insert's apply pass): a block's runs for
+  // neighbouring regions share their edge lines, read once per XCD's L2
+  // instead of once per region's workgroup
+  const uint32_t r = xcd_index(blockIdx.x, gridDim.x), t = threadIdx.x;
   const uint32_t lane = t & 63, w = t >> 6;
   const uint32_t r0 = r * kQRegBytes;
   const uint32_t rbytes = tb - r0 < kQRegBytes ? tb - r0 : kQRegBytes;  // a multiple of 4
