@@ -548,7 +548,10 @@ __global__ __launch_bounds__(kQNT) void cm_qlook_kernel(const uint8_t* __restric
   const uint32_t rb = kb * (uint32_t)k;
   // one block's run per wave step (about k * KB / nreg records): lanes over
   // the run; kQLU runs' loads issued before their lookups
-  constexpr int kQLU = 8;
+#ifndef PSG_QLU
+#define PSG_QLU 16  // runs per wave in flight (r06: 16 vs 8, query -4 %, profiles/r06_ab_countmin_look.txt)
+#endif
+  constexpr int kQLU = PSG_QLU;
   for (uint32_t b0 = w * (uint32_t)kQLU; b0 < nb; b0 += (kQNT / 64) * (uint32_t)kQLU) {
     uint32_t rec[kQLU], at[kQLU];
     bool have[kQLU];
