@@ -43,7 +43,7 @@
 
 #define AS1 __attribute__((address_space(1)))
 #ifndef PSG_SNAPPY_IR
-#define PSG_SNAPPY_IR 1  // A/B: 0 = launches of few parts take snappy_kernel too
+#define PSG_SNAPPY_IR 2  // few-part launches: 2 = the table form, 1 = the streamed form (A/B), 0 = snappy_kernel
 #endif
 #ifndef PSG_SNAPPY_PREFETCH
 #define PSG_SNAPPY_PREFETCH 1  // A/B: 0 = no L2 prefetch of the parts
@@ -81,6 +81,17 @@ constexpr uint32_t kMaxDef = PSG_SNAPPY_MAXDEF;  // deferred pieces per part (LD
 constexpr uint32_t kLitUnits = 256;  // 16-B units per copy-kernel chunk (4 KB)
 constexpr uint64_t kPrefetchParts = 64;         // parts per launch that are prefetched into L2
 constexpr uint64_t kPrefetchMax = 2ull << 20;   // largest part prefetched
+
+// This workgroup's earlier global stores visible to its own later loads (the
+// decoders read back output they wrote): its waves share the CU's L1, so a
+// workgroup-scope fence after the stores drain is enough.  __threadfence()
+// (agent scope) would write back and invalidate the XCD's L2 -- ~3.5 us each
+// (MI355X_MICROARCH.md), which r06 measured dominating the table form's
+// in-order step.
+__device__ __forceinline__ void own_stores_visible() {
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "workgroup");
+}
 
 __global__ __launch_bounds__(64) void snappy_kernel(const uint8_t* __restrict__ src,
                                                     const uint64_t* __restrict__ soff,
@@ -379,7 +390,7 @@ __global__ __launch_bounds__(64) void snappy_kernel(const uint8_t* __restrict__ 
         if (jj >= 0 && pos - tdst[jj] < tlen[jj]) from = tsrc[jj] + (pos - tdst[jj]);
         if (off > kRing) {
           flush(o);
-          __threadfence();
+          own_stores_visible();
         }
         const uint8_t b = lane < len ? (from != 0xffffffffu ? s0[from]
                                         : off <= kRing ? ring[pos & (kRing - 1)] : out[pos])
@@ -392,7 +403,7 @@ __global__ __launch_bounds__(64) void snappy_kernel(const uint8_t* __restrict__ 
       } else {
         // the source was flushed: read it back after this wave's stores land
         flush(o);
-        __threadfence();
+        own_stores_visible();
         room(len);
         if (lane < len) ring[(o + lane) & (kRing - 1)] = out[o - off + li];
       }
@@ -487,36 +498,31 @@ __device__ __forceinline__ uint32_t ir_wait(uint32_t n) {
 }
 #undef IRW
 
-__global__ __launch_bounds__(64) void snappy_ir_kernel(const uint8_t* __restrict__ src,
-                                                       const uint64_t* __restrict__ soff,
-                                                       uint8_t* __restrict__ dst,
-                                                       const uint64_t* __restrict__ doff,
-                                                       const uint64_t* __restrict__ dcap,
-                                                       uint64_t nmsg, int32_t* __restrict__ status,
-                                                       SnappyLit* __restrict__ lits,
-                                                       uint32_t* __restrict__ nlits,
-                                                       uint32_t lit_cap,
-                                                       unsigned long long* __restrict__ nbad,
-                                                       int pairs) {
-  __shared__ __attribute__((aligned(16))) uint8_t ir[kIRB];
-  __shared__ __attribute__((aligned(16))) uint8_t sb[kSB];
-  __shared__ uint32_t so[kMaxSt], ss[kMaxSt], sl[kMaxSt];   // staged: output pos, stage offset, length
-  __shared__ uint32_t tdst[kMaxDef], tsrc[kMaxDef], tlen[kMaxDef];  // deferred pieces
-  const uint32_t lane = threadIdx.x;
-  for (uint64_t msg = blockIdx.x; msg < nmsg; msg += gridDim.x) {
-    const AS1 uint8_t* const s0 =
-        (const AS1 uint8_t*)(pairs ? (const uint8_t*)soff[2 * msg] : src + soff[msg]);
-    const uint64_t slen = pairs ? soff[2 * msg + 1] - soff[2 * msg] : soff[msg + 1] - soff[msg];
-    AS1 uint8_t* const out = (AS1 uint8_t*)(dst + doff[msg]);
-    const uint64_t cap = dcap ? dcap[msg] : doff[msg + 1] - doff[msg];
-    if (slen == 0) {
-      if (lane == 0) status[msg] = cap == 0 ? 0 : PSG_ERR_SIZE;
-      continue;
-    }
-    if (slen >= (1ull << 31)) {
-      if (lane == 0) status[msg] = PSG_ERR_ARG;
-      continue;
-    }
+// LDS of the streamed decoder (one part per workgroup): the input ring, the
+// output stage and its map, the deferred pieces
+struct IrLds {
+  __attribute__((aligned(16))) uint8_t ir[kIRB];
+  __attribute__((aligned(16))) uint8_t sb[kSB];
+  uint32_t so[kMaxSt], ss[kMaxSt], sl[kMaxSt];  // staged: output pos, stage offset, length
+  uint32_t tdst[kMaxDef], tsrc[kMaxDef], tlen[kMaxDef];  // deferred pieces
+};
+
+// one part (slen in [1, 2^31)) by one wave, lanes 0..63 of the workgroup
+__device__ __forceinline__ void ir_part(IrLds& S, uint64_t msg, const AS1 uint8_t* const s0,
+                                        const uint64_t slen, AS1 uint8_t* const out,
+                                        const uint64_t cap, int32_t* __restrict__ status,
+                                        SnappyLit* __restrict__ lits,
+                                        uint32_t* __restrict__ nlits, uint32_t lit_cap,
+                                        unsigned long long* __restrict__ nbad) {
+    uint8_t* const ir = S.ir;
+    uint8_t* const sb = S.sb;
+    uint32_t* const so = S.so;
+    uint32_t* const ss = S.ss;
+    uint32_t* const sl = S.sl;
+    uint32_t* const tdst = S.tdst;
+    uint32_t* const tsrc = S.tsrc;
+    uint32_t* const tlen = S.tlen;
+    const uint32_t lane = threadIdx.x & 63u;
     const uint32_t e = (uint32_t)slen;
     int32_t st = 0;
 #ifdef PSG_SNAPPY_PROF
@@ -798,8 +804,7 @@ __global__ __launch_bounds__(64) void snappy_ir_kernel(const uint8_t* __restrict
       }
       if (wrote && __ballot(lane < len && where == 2u)) {
         // bytes written out earlier by this wave: visible to its loads
-        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-        __threadfence();
+        own_stores_visible();
         wrote = false;
       }
       const uint32_t b = lane < len ? (where == 0u ? inb(at) : where == 1u ? (uint32_t)sb[at]
@@ -838,6 +843,373 @@ __global__ __launch_bounds__(64) void snappy_ir_kernel(const uint8_t* __restrict
       for (int i = 0; i < 8; ++i) g_sprof[msg][i] = sp[i];
 #endif
     __builtin_amdgcn_wave_barrier();
+}
+
+__global__ __launch_bounds__(64) void snappy_ir_kernel(const uint8_t* __restrict__ src,
+                                                       const uint64_t* __restrict__ soff,
+                                                       uint8_t* __restrict__ dst,
+                                                       const uint64_t* __restrict__ doff,
+                                                       const uint64_t* __restrict__ dcap,
+                                                       uint64_t nmsg, int32_t* __restrict__ status,
+                                                       SnappyLit* __restrict__ lits,
+                                                       uint32_t* __restrict__ nlits,
+                                                       uint32_t lit_cap,
+                                                       unsigned long long* __restrict__ nbad,
+                                                       int pairs) {
+  __shared__ IrLds S;
+  const uint32_t lane = threadIdx.x;
+  for (uint64_t msg = blockIdx.x; msg < nmsg; msg += gridDim.x) {
+    const AS1 uint8_t* const s0 =
+        (const AS1 uint8_t*)(pairs ? (const uint8_t*)soff[2 * msg] : src + soff[msg]);
+    const uint64_t slen = pairs ? soff[2 * msg + 1] - soff[2 * msg] : soff[msg + 1] - soff[msg];
+    AS1 uint8_t* const out = (AS1 uint8_t*)(dst + doff[msg]);
+    const uint64_t cap = dcap ? dcap[msg] : doff[msg + 1] - doff[msg];
+    if (slen == 0) {
+      if (lane == 0) status[msg] = cap == 0 ? 0 : PSG_ERR_SIZE;
+      continue;
+    }
+    if (slen >= (1ull << 31)) {
+      if (lane == 0) status[msg] = PSG_ERR_ARG;
+      continue;
+    }
+    ir_part(S, msg, s0, slen, out, cap, status, lits, nlits, lit_cap, nbad);
+  }
+}
+
+// ---------------------------------------------------------------------------
+// The table form (launches of few parts; PSG_SNAPPY_IR == 2, the default).
+// r06 measured the streamed decoder above bound by its per-element chain on
+// one wave (~2.8 K clocks per element of a cfg2 value part: the copy-source
+// lookups among the deferred pieces, the stream's DMA issue, the stage's
+// map, profiles/r06_ab_snappy_stream.txt), while the parts of a compressed
+// push hold few elements (incompressible data: long literals and spurious
+// 4-byte matches).  Here one workgroup (4 waves) per part:
+//   1. wave 0 walks the TAGS only -- one dependent 64-byte lookahead load
+//      per element past the window (L2 hits: waves 1-3 pull the part into
+//      L2 meanwhile) -- into an LDS table (output position, input position
+//      or offset, length), with the streamed form's format checks in the
+//      same order (the same status for a corrupt part);
+//   2. all waves move the elements at once: short literals from the input,
+//      long ones (>= kTabBigLit) handed to the chip-wide copy kernel, and
+//      every byte of a copy resolved on its own lane through the table to
+//      the literal byte it repeats (copies of copies followed up to
+//      kTabDepth times), read from the input -- no output is read back, and
+//      no element waits for another;
+//   3. wave 0 writes the copies that did not resolve (chains deeper than
+//      kTabDepth: runs), in element order, from the output written so far.
+// A part of more than kTabMax elements, or of more than kTabPend unresolved
+// copies (compressible data: the streamed form's LDS-resident output serves
+// it better), runs ir_part instead, in the same workgroup.
+constexpr uint32_t kTabMax = 4096;
+constexpr uint32_t kTabPend = 64;
+constexpr uint32_t kTabBigLit = 512;
+constexpr int kTabDepth = 4;
+constexpr uint32_t kCopyBit = 0x80000000u;
+struct TabLds {
+  uint32_t to[kTabMax + 1];  // element i's output position (to[nel] = the part's length)
+  uint32_t ta[kTabMax];      // literal: input position; copy: offset
+  uint32_t tl[kTabMax];      // length, | kCopyBit for a copy
+  uint32_t tx[kTabMax];      // literal: deferred index (~0: moved in step 2); copy: 1 = unresolved
+  uint32_t nel, verdict, base, npend;
+};
+union SnappyTabLds {
+  IrLds ir;
+  TabLds tab;
+};
+
+__global__ __launch_bounds__(256) void snappy_tab_kernel(const uint8_t* __restrict__ src,
+                                                        const uint64_t* __restrict__ soff,
+                                                        uint8_t* __restrict__ dst,
+                                                        const uint64_t* __restrict__ doff,
+                                                        const uint64_t* __restrict__ dcap,
+                                                        uint64_t nmsg, int32_t* __restrict__ status,
+                                                        SnappyLit* __restrict__ lits,
+                                                        uint32_t* __restrict__ nlits,
+                                                        uint32_t lit_cap,
+                                                        unsigned long long* __restrict__ nbad,
+                                                        int pairs) {
+  __shared__ SnappyTabLds U;
+  TabLds& T = U.tab;
+  const uint32_t tid = threadIdx.x, lane = tid & 63u, w = tid >> 6;
+  for (uint64_t msg = blockIdx.x; msg < nmsg; msg += gridDim.x) {
+    const AS1 uint8_t* const s0 =
+        (const AS1 uint8_t*)(pairs ? (const uint8_t*)soff[2 * msg] : src + soff[msg]);
+    const uint64_t slen = pairs ? soff[2 * msg + 1] - soff[2 * msg] : soff[msg + 1] - soff[msg];
+    AS1 uint8_t* const out = (AS1 uint8_t*)(dst + doff[msg]);
+    const uint64_t cap = dcap ? dcap[msg] : doff[msg + 1] - doff[msg];
+    if (slen == 0 || slen >= (1ull << 31)) {  // the workgroup agrees: no barrier skipped
+      if (tid == 0) status[msg] = slen ? PSG_ERR_ARG : cap == 0 ? 0 : PSG_ERR_SIZE;
+      continue;
+    }
+    const uint32_t e = (uint32_t)slen;
+#ifdef PSG_SNAPPY_PROF
+    // [0] step 1 clocks, [1] step 2 (wave 0's share), [2] the part, [3] window
+    // loads, [4] unresolved copies, [5] step 3, [6] elements, [7] wave 1's
+    // prefetch
+    unsigned long long sp[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+    const unsigned long long sp_part = clock64();
+#endif
+    // ---- 1. the tags (wave 0); the part into L2 (waves 1-3)
+    if (w == 0) {
+      int32_t st = 0;
+      bool full = false;
+      uint32_t lp = 0xffffffffu - 64u, la = 0;
+      auto ub = [&](uint32_t q) -> uint32_t {
+        if (q - lp >= 64u) {
+          lp = q;
+          la = q + lane < e ? (uint32_t)s0[q + lane] : 0u;
+#ifdef PSG_SNAPPY_PROF
+          sp[3] += 1;
+#endif
+        }
+        return (uint32_t)__builtin_amdgcn_readlane((int)la, (int)(q - lp));
+      };
+      uint64_t ulen = 0;
+      bool done = false;
+      uint32_t p = 0;
+      while (p < 5 && p < e && !done) {
+        const uint32_t b = ub(p);
+        ulen |= (uint64_t)(b & 0x7f) << (7 * p);
+        done = !(b & 0x80);
+        ++p;
+      }
+      if (!done || ulen > 0xffffffffull) st = PSG_ERR_ARG;
+      if (!st && ulen != cap) st = PSG_ERR_SIZE;
+      const uint32_t ucap = (uint32_t)ulen;
+      uint32_t o = 0, n = 0, nd = 0;
+      while (!st && p < e) {
+        if (n == kTabMax) {
+          full = true;
+          break;
+        }
+        const uint32_t tag = ub(p++);
+        uint32_t len, a, x;
+        if ((tag & 3u) == 0u) {  // literal
+          len = (tag >> 2) + 1u;
+          if (len > 60u) {
+            const uint32_t nb = len - 60u;
+            if (e - p < nb) { st = PSG_ERR_ARG; break; }
+            len = 0;
+            for (uint32_t b = 0; b < nb; ++b) len |= ub(p + b) << (8 * b);
+            p += nb;
+            if (len == 0xffffffffu) { st = PSG_ERR_ARG; break; }
+            len += 1u;
+          }
+          if (e - p < len || ucap - o < len) { st = PSG_ERR_ARG; break; }
+          a = p;
+          x = lits && len >= kTabBigLit ? nd++ : 0xffffffffu;
+          p += len;
+          if (lane == 0) T.tl[n] = len;
+        } else {
+          uint32_t off;
+          if ((tag & 3u) == 1u) {
+            if (e - p < 1) { st = PSG_ERR_ARG; break; }
+            len = 4u + ((tag >> 2) & 7u);
+            off = (tag >> 5) << 8 | ub(p);
+            p += 1;
+          } else if ((tag & 3u) == 2u) {
+            if (e - p < 2) { st = PSG_ERR_ARG; break; }
+            len = 1u + (tag >> 2);
+            off = ub(p) | ub(p + 1) << 8;
+            p += 2;
+          } else {
+            if (e - p < 4) { st = PSG_ERR_ARG; break; }
+            len = 1u + (tag >> 2);
+            off = ub(p) | ub(p + 1) << 8 | ub(p + 2) << 16 | ub(p + 3) << 24;
+            p += 4;
+          }
+          if (off == 0 || off > o || ucap - o < len) { st = PSG_ERR_ARG; break; }
+          a = off;
+          x = 0;
+          if (lane == 0) T.tl[n] = len | kCopyBit;
+        }
+        if (lane == 0) {
+          T.to[n] = o;
+          T.ta[n] = a;
+          T.tx[n] = x;
+        }
+        o += len;
+        ++n;
+      }
+      if (!st && !full && o != ucap) st = PSG_ERR_ARG;
+#ifdef PSG_SNAPPY_PROF
+      sp[0] = clock64() - sp_part;
+      sp[6] = n;
+#endif
+      if (lane == 0) {
+        T.to[n] = o;
+        T.nel = n;
+        T.verdict = st ? 1u : full ? 2u : 0u;
+        T.npend = 0;
+        uint32_t base = 0;
+        if (st) {
+          status[msg] = st;
+          if (nbad) atomicAdd(nbad, 1ull);
+        } else if (!full && nd) {
+          base = atomicAdd(nlits, nd);
+        }
+        T.base = base;
+      }
+    } else {
+      // one load per 128-B line, eight in flight per lane
+      uint32_t acc = 0;
+      for (uint32_t x0 = (tid - 64u) * 128u; x0 < e; x0 += 8u * 192u * 128u) {
+        uint32_t v[8];
+#pragma unroll
+        for (int k = 0; k < 8; ++k) {
+          const uint32_t x = x0 + (uint32_t)k * 192u * 128u;
+          v[k] = x < e ? (uint32_t)s0[x] : 0u;
+        }
+#pragma unroll
+        for (int k = 0; k < 8; ++k) acc ^= v[k];
+      }
+      asm volatile("" ::"v"(acc));
+#ifdef PSG_SNAPPY_PROF
+      if (w == 1) {
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        sp[7] = clock64() - sp_part;
+      }
+#endif
+    }
+    __syncthreads();  // (1) the table
+    const uint32_t verdict = T.verdict, nel = T.nel, base = T.base;
+    __syncthreads();  // (1b) read by every wave before the LDS may be reused
+    if (verdict == 1u) continue;  // corrupt: reported in step 1
+    if (verdict == 2u) {          // too many elements: the streamed form
+      if (w == 0) ir_part(U.ir, msg, s0, slen, out, cap, status, lits, nlits, lit_cap, nbad);
+      __syncthreads();
+      continue;
+    }
+    // last element starting at or before output position x (< the part's length)
+    auto find = [&](uint32_t x) -> uint32_t {
+      uint32_t lo = 0, hi = nel;  // to[lo] <= x < to[hi]
+      while (hi - lo > 1u) {
+        const uint32_t mid = (lo + hi) >> 1;
+        if (T.to[mid] <= x) lo = mid;
+        else hi = mid;
+      }
+      return lo;
+    };
+    // ---- 2. the elements, round robin over the waves
+#ifdef PSG_SNAPPY_PROF
+    const unsigned long long sp_2 = clock64();
+#endif
+    // a copy byte at output position q (< the copy's own position), followed
+    // through the table to the literal byte it repeats: its input position,
+    // or ~0 past kTabDepth copies.  jc caches the last element found (the
+    // bytes of one copy mostly lie in one element)
+    auto resolve = [&](uint32_t q, uint32_t& jc) -> uint32_t {
+      for (int d = 0; d < kTabDepth; ++d) {
+        uint32_t j = jc;
+        if (!(T.to[j] <= q && q < T.to[j + 1])) j = find(q);
+        if (d == 0) jc = j;
+        const uint32_t lj = T.tl[j], dq = q - T.to[j], aj = T.ta[j];
+        if (!(lj & kCopyBit)) return aj + dq;
+        q = T.to[j] - aj + dq % aj;  // byte dq of copy j repeats this one
+      }
+      return 0xffffffffu;
+    };
+    constexpr uint32_t kLaneCopy = 8;  // copies this short: one lane each, below
+    for (uint32_t i = w; i < nel; i += 4u) {
+      const uint32_t oo = T.to[i], a = T.ta[i], lk = T.tl[i], x = T.tx[i];
+      const uint32_t len = lk & ~kCopyBit;
+      if (!(lk & kCopyBit)) {
+        if (x != 0xffffffffu && base + x < lit_cap) {
+          if (lane == 0)
+            lits[base + x] = SnappyLit{(const uint8_t*)(s0 + a), (uint8_t*)(out + oo), len};
+        } else {
+          for (uint32_t l = lane; l < len; l += 64u) out[oo + l] = s0[a + l];
+        }
+        continue;
+      }
+      if (len <= kLaneCopy) continue;
+      // a longer copy, one byte per lane: byte l is output[o - off + (l mod
+      // off)] (run-length copies included)
+      uint32_t from = 0;
+      if (lane < len) {
+        uint32_t jc = 0;
+        from = resolve(oo - a + (a >= 64u ? lane : lane % a), jc);
+      }
+      if (__ballot(lane < len && from == 0xffffffffu)) {
+        if (lane == 0) {
+          T.tx[i] = 1u;
+          atomicAdd(&T.npend, 1u);
+        }
+      } else if (lane < len) {
+        out[oo + lane] = s0[from];
+      }
+    }
+    // short copies (incompressible data: spurious 4-byte matches), one lane
+    // each: a wave resolves 64 of them at once instead of one
+    for (uint32_t i = tid; i < nel; i += 256u) {
+      const uint32_t lk = T.tl[i];
+      const uint32_t len = lk & ~kCopyBit;
+      if (!(lk & kCopyBit) || len > kLaneCopy) continue;
+      const uint32_t oo = T.to[i], a = T.ta[i];
+      uint32_t src[kLaneCopy];
+      uint32_t jc = 0;
+      bool ok = true;
+      for (uint32_t l = 0; l < len; ++l) {
+        src[l] = resolve(oo - a + (l < a ? l : l % a), jc);
+        ok = ok && src[l] != 0xffffffffu;
+      }
+      if (!ok) {
+        T.tx[i] = 1u;
+        atomicAdd(&T.npend, 1u);
+        continue;
+      }
+      uint8_t b[kLaneCopy];
+      for (uint32_t l = 0; l < len; ++l) b[l] = s0[src[l]];
+      for (uint32_t l = 0; l < len; ++l) out[oo + l] = b[l];
+    }
+    // step 2's stores visible to step 3's loads (and to ir_part's reads)
+    own_stores_visible();
+    __syncthreads();  // (2)
+    const uint32_t npend = T.npend;
+#ifdef PSG_SNAPPY_PROF
+    sp[1] = clock64() - sp_2;
+    sp[4] = npend;
+    const unsigned long long sp_3 = clock64();
+#endif
+    if (npend > kTabPend) {  // compressible: the streamed form rewrites the whole part
+      __syncthreads();
+      if (w == 0) ir_part(U.ir, msg, s0, slen, out, cap, status, lits, nlits, lit_cap, nbad);
+      __syncthreads();
+      continue;
+    }
+    // ---- 3. the unresolved copies in element order (wave 0): a source byte
+    // of a literal from the input, of a copy from the output (written in step
+    // 2, or earlier in this step)
+    if (w == 0) {
+      for (uint32_t i0 = 0; npend && i0 < nel; i0 += 64u) {
+        const uint32_t ii = i0 + lane;
+        unsigned long long m = __ballot(ii < nel && (T.tl[ii] & kCopyBit) && T.tx[ii] == 1u);
+        while (m) {
+          const uint32_t i = i0 + (uint32_t)__builtin_ctzll(m);
+          m &= m - 1;
+          const uint32_t oo = T.to[i], off = T.ta[i], len = T.tl[i] & ~kCopyBit;
+          if (lane < len) {
+            const uint32_t q = oo - off + (off >= 64u ? lane : lane % off);
+            const uint32_t j = find(q);
+            const uint32_t b = (T.tl[j] & kCopyBit) ? (uint32_t)out[q]
+                                                     : (uint32_t)s0[T.ta[j] + (q - T.to[j])];
+            out[oo + lane] = (uint8_t)b;
+          }
+          own_stores_visible();
+        }
+      }
+      if (lane == 0) status[msg] = 0;
+#ifdef PSG_SNAPPY_PROF
+      sp[5] = clock64() - sp_3;
+      sp[2] = clock64() - sp_part;
+      if (lane == 0 && msg < 4096)
+        for (int i = 0; i < 7; ++i) g_sprof[msg][i] = sp[i];
+#endif
+    }
+#ifdef PSG_SNAPPY_PROF
+    if (w == 1 && lane == 0 && msg < 4096) g_sprof[msg][7] = sp[7];
+#endif
+    __syncthreads();  // (3) before the next part's table
   }
 }
 
@@ -958,8 +1330,13 @@ hipError_t launch_snappy(const uint8_t* src, const uint64_t* soff, uint64_t nmsg
   constexpr uint64_t kPerCU = 163840ull / kLdsPerPart > 0 ? 163840ull / kLdsPerPart : 1;
   const uint64_t grid_cap = 256ull * kPerCU;
   const uint64_t blocks = nmsg < grid_cap ? nmsg : grid_cap;
-  if (PSG_SNAPPY_IR && nmsg <= kPrefetchParts)
-    // few parts (a message's): the streamed form, one part per CU
+  if (PSG_SNAPPY_IR == 2 && nmsg <= kPrefetchParts)
+    // few parts (a message's): the table form, one part per CU
+    hipLaunchKernelGGL(snappy_tab_kernel, dim3((uint32_t)nmsg), dim3(256), 0, stream, src, soff,
+                       dst, doff, dcap, nmsg, status, nlits ? lits : nullptr, nlits, cap, nbad,
+                       pairs ? 1 : 0);
+  else if (PSG_SNAPPY_IR && nmsg <= kPrefetchParts)
+    // the streamed form alone (A/B builds: PSG_SNAPPY_IR=1)
     hipLaunchKernelGGL(snappy_ir_kernel, dim3((uint32_t)nmsg), dim3(64), 0, stream, src, soff, dst,
                        doff, dcap, nmsg, status, nlits ? lits : nullptr, nlits, cap, nbad,
                        pairs ? 1 : 0);

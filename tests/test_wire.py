@@ -836,3 +836,67 @@ def test_gpu_snappy_streamed_and_per_wave_forms_agree():
     got, st = _gpu_snappy(many, [len(d) for d in want_many])
     assert st == [0] * len(many)
     assert all(g == d for g, d in zip(got, want_many))
+
+
+@pytest.mark.gpu
+def test_gpu_snappy_table_form_paths():
+    """Launches of <= 64 parts take the table form (psg_snappy.hip
+    snappy_tab_kernel): the tags walked into an LDS table, then every copy
+    byte resolved on its own lane through the table to the literal byte it
+    repeats.  Parts that exercise each of its paths, byte-exact against the
+    spec oracle: copies of copies (chains of depth 1..7: the deeper ones
+    written in order by the last step), copies straddling two literals and
+    overlapping their own output, copies into deferred (>= 512 B) literals,
+    a run of more than 64 unresolved copies (the whole part falls back to the
+    streamed form), a part of more than 4,096 elements (falls back before any
+    byte moves), and corrupt parts beside good ones."""
+    from parameter_server_amd import _lib
+    rng = np.random.default_rng(77)
+    lit = lambda n: ("lit", rng.integers(0, 256, n, dtype=np.uint8).tobytes())
+    parts, datas = [], []
+    # chains: each copy repeats the previous one (depth grows by one each)
+    el = [lit(1000), ("copy", 1000, 64)]
+    for _ in range(6):
+        el.append(("copy", 64, 64))
+    el += [lit(30), ("copy", 500, 40)]
+    parts.append(el)
+    # straddling and overlapping copies, deferred literals read back
+    el = [lit(100), lit(100), ("copy", 150, 64), ("copy", 30, 64), lit(700), ("copy", 650, 64),
+          ("copy", 1, 64), lit(5000), ("copy", 4000, 64), ("copy", 5100, 50), ("copy", 7, 9)]
+    parts.append(el)
+    # a run: "a" then 100 copies of offset 1 (chains too deep: > 64 unresolved)
+    parts.append([("lit", b"a")] + [("copy", 1, 64)] * 100)
+    # element-dense: 5,000 three-byte literals and short copies
+    el = []
+    for i in range(5000):
+        el.append(lit(3))
+        if i > 10 and i % 3 == 0:
+            el.append(("copy", int(rng.integers(1, 30)), int(rng.integers(1, 20))))
+    parts.append(el)
+    # incompressible-shaped: long literals and spurious 4-byte matches
+    el = []
+    o = 0
+    for _ in range(60):
+        n = int(rng.integers(1500, 4000))
+        el.append(lit(n))
+        o += n
+        el.append(("copy", int(rng.integers(4, min(o, 65535))), 4))
+        o += 4
+    parts.append(el)
+    streams = [_snappy_stream(e) for e in parts]
+    for c, d in streams:
+        assert O.snappy_uncompress(c) == d
+    comps = [c for c, _ in streams]
+    datas = [d for _, d in streams]
+    got, st = _gpu_snappy(comps, [len(d) for d in datas])
+    assert st == [0] * len(comps)
+    for g, d in zip(got, datas):
+        assert g == d
+    # corrupt parts between good ones: the table walk reports them
+    bad = [comps[0], bytes([0x04, 0x01, 0x05]), comps[1], bytes([0x06, 0x04]) + b"ab", comps[4]]
+    got, st = _gpu_snappy(bad, [len(datas[0]), 4, len(datas[1]), 6, len(datas[4])])
+    assert st[1] == _lib.PSG_ERR_ARG and st[3] == _lib.PSG_ERR_ARG
+    assert st[0] == st[2] == st[4] == 0
+    assert got[0] == datas[0] and got[2] == datas[1] and got[4] == datas[4]
+    got, st = _gpu_snappy([comps[0]], [len(datas[0]) + 1])
+    assert st == [_lib.PSG_ERR_SIZE]

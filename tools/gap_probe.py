@@ -68,6 +68,61 @@ def cfg2_plan(dev):
     return bench.make_plan(insts, dev, 0)
 
 
+def modes(K):
+    """cfg2: the step timed several ways, wall clock of K steps (best of 3)."""
+    import torch
+    plan, keep, _ = cfg2_plan(torch.device("cuda", 0))
+    st = torch.cuda.current_stream()
+    sh = st.cuda_stream
+    E = lambda: torch.cuda.Event(enable_timing=True)
+
+    def run(body):
+        for _ in range(3):
+            body(-1)
+        torch.cuda.synchronize()
+        best = 1e9
+        for _ in range(3):
+            torch.cuda.synchronize()
+            t0 = time.perf_counter()
+            for k in range(K):
+                body(k)
+            torch.cuda.synchronize()
+            best = min(best, (time.perf_counter() - t0) / K * 1e3)
+        return best
+
+    ev = [[E() for _ in range(3)] for _ in range(K)]
+
+    def ev3(k):
+        if k >= 0:
+            ev[k][0].record(st)
+        plan.run_stage(0, sh)
+        if k >= 0:
+            ev[k][1].record(st)
+        plan.run_stage(1, sh)
+        if k >= 0:
+            ev[k][2].record(st)
+
+    def ev_agg(k):
+        plan.run_stage(0, sh)
+        if k >= 0:
+            ev[k][1].record(st)
+        plan.run_stage(1, sh)
+        if k >= 0:
+            ev[k][2].record(st)
+
+    out = {"events3": run(ev3)}
+    out["agg_by_events3"] = float(np.mean([ev[k][1].elapsed_time(ev[k][2]) for k in range(K)]))
+    out["events_agg_only"] = run(ev_agg)
+    out["agg_by_events2"] = float(np.mean([ev[k][1].elapsed_time(ev[k][2]) for k in range(K)]))
+    out["plain"] = run(lambda k: plan.run(sh))
+    out["partition_only"] = run(lambda k: plan.run_stage(0, sh))
+    out["aggregate_only"] = run(lambda k: plan.run_stage(1, sh))
+    out["plain_again"] = run(lambda k: plan.run(sh))
+    ok = plan.matched()
+    print("cfg2 " + " ".join(f"{k} {v:.4f}" for k, v in out.items()) + f" matched {int(ok.sum())}",
+          flush=True)
+
+
 def trace(mode, K):
     import torch
     plan, keep, _ = cfg2_plan(torch.device("cuda", 0))
@@ -91,7 +146,10 @@ if __name__ == "__main__":
     K = int(sys.argv[1]) if len(sys.argv) > 1 else 20
     if len(sys.argv) > 2:
         bench.ARENA = True
-        trace(sys.argv[2], K)
+        if sys.argv[2] == "modes":
+            modes(K)
+        else:
+            trace(sys.argv[2], K)
         sys.exit(0)
     dev = torch.device("cuda", 0)
     bench.ARENA = True

@@ -57,7 +57,12 @@ def main():
                                    "total_clk": int(r[2]), "refills": int(r[3]),
                                    "deferred": int(r[4]), "literal_clk": int(r[5]),
                                    "end_clk": int(r[7]),
-                                   "elements": int(r[6]), "bytes_in": int(comps[base + i].size)}
+                                   "elements": int(r[6]), "bytes_in": int(comps[base + i].size),
+                                   # the table form's fields (psg_snappy.hip snappy_tab_kernel)
+                                   "tab": {"walk_clk": int(r[0]), "move_clk": int(r[1]),
+                                           "total_clk": int(r[2]), "window_loads": int(r[3]),
+                                           "unresolved": int(r[4]), "inorder_clk": int(r[5]),
+                                           "elements": int(r[6]), "prefetch_clk": int(r[7])}}
                                   for i, r in enumerate(prof)]}
     got = dd.cpu().numpy()
     assert all(np.array_equal(got[int(doff[i]):int(doff[i + 1])], raws[i]) for i in range(len(raws)))
