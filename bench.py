@@ -79,6 +79,9 @@ def parse():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=20)
     ap.add_argument("--warmup", type=int, default=5)
+    ap.add_argument("--prewarm-ms", type=float, default=100.0,
+                    help="untimed steps for this long before each timed region's warm-up "
+                         "steps (the GPU's clock ramp after host-side phases; 0 = off)")
     ap.add_argument("--batch", type=int, default=0,
                     help="aggregates per GPU per step (default: 64 for cfg2, else 1-2)")
     ap.add_argument("--npush", type=int, default=8)
@@ -177,13 +180,41 @@ def make_plan(insts, dev, local):
     return plan, keep, jobs
 
 
+PREWARM_S = 0.1  # --prewarm-ms / 1000
+
+
+def prewarm(step):
+    """Untimed steps for PREWARM_S seconds of wall time before a timed
+    region's W warm-up steps.  MI355X raises its clocks over ~25 ms of
+    sustained work after an idle spell (here: the host generating the next
+    block's data), so a timed region that starts on a cold GPU measures the
+    ramp, not the kernel: cfg2 steps run 0.43 ms in the first ~10 ms and
+    0.362 ms from ~25 ms on (tools/warm_probe.py,
+    profiles/r06_warm_probe.txt).  The timed region itself is unchanged:
+    exactly K whole steps.  Returns the steps run."""
+    import torch
+    if PREWARM_S <= 0:
+        return 0
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    n = 0
+    while True:
+        for _ in range(4):  # a few at a time: the host stays ahead of the GPU
+            step()
+            n += 1
+        torch.cuda.synchronize()
+        if time.perf_counter() - t0 >= PREWARM_S:
+            return n
+
+
 def timed_steps(plan, K, W, stream, dist):
-    """W untimed warm-up steps, then exactly K timed steps bracketed by a
-    barrier + device synchronize on both sides.  Returns (wall s, mean
-    partition ms, mean aggregate ms); the stage times are HIP events on the
-    launch stream."""
+    """W untimed warm-up steps (after the prewarm), then exactly K timed steps
+    bracketed by a barrier + device synchronize on both sides.  Returns (wall
+    s, mean partition ms, mean aggregate ms); the stage times are HIP events
+    on the launch stream."""
     import torch
     sh = stream.cuda_stream
+    prewarm(lambda: plan.run(sh))
     for _ in range(W):
         plan.run(sh)
     torch.cuda.synchronize()
@@ -212,6 +243,8 @@ def main():
     global PLAN_FLAGS, ARENA, ARENA_PUSHES
     args = parse()
     PLAN_FLAGS = args.plan_flags
+    global PREWARM_S
+    PREWARM_S = args.prewarm_ms / 1000.0
     ARENA = args.layout == "arena"
     ARENA_PUSHES = args.arena_pushes
     if args.cfg5_unsliced_child:
@@ -308,6 +341,7 @@ def main():
         "n_gpus": world,
         "steps": K,
         "warmup": args.warmup,
+        "prewarm_ms": args.prewarm_ms,
         "ms_per_step": ms_per_step,
         "higher_is_better": True,
         "scaling": "weak",
@@ -407,9 +441,14 @@ def timed_stages(stages, K, W, stream, dist):
     synchronize pairs.  Returns (wall s, [mean ms per stage]) (HIP events on
     `stream` between the stages)."""
     import torch
-    for _ in range(W):
+
+    def step():
         for f in stages:
             f()
+
+    prewarm(step)
+    for _ in range(W):
+        step()
     torch.cuda.synchronize()
     if dist:
         dist.barrier()
@@ -440,6 +479,14 @@ def timed_rotating(plans, K, W, stream):
     import torch
     sh = stream.cuda_stream
     R = len(plans)
+    rot = [0]
+
+    def step():
+        plans[rot[0] % R].run_stage(0, sh)
+        plans[rot[0] % R].run_stage(1, sh)
+        rot[0] += 1
+
+    prewarm(step)
     for s in range(W):
         plans[s % R].run_stage(0, sh)
         plans[s % R].run_stage(1, sh)
@@ -643,7 +690,8 @@ def cfg5_unsliced_child(args, rank, world, dist):
     if world > 1:
         env["MASTER_PORT"] = str(int(os.environ.get("MASTER_PORT", "29500")) + 1)
     cmd = [sys.executable, os.path.join(ROOT, "bench.py"), "--cfg5-unsliced-child",
-           "--cfg5-steps", str(args.cfg5_steps)] + (["--no-check"] if args.no_check else [])
+           "--cfg5-steps", str(args.cfg5_steps), "--prewarm-ms", str(args.prewarm_ms)] + \
+        (["--no-check"] if args.no_check else [])
     res = {"error": "child did not report"}
     try:
         p = subprocess.run(cmd, env=env, stdout=subprocess.PIPE, stderr=None, timeout=400,
@@ -1045,6 +1093,7 @@ def bench_rows(device, reps=5, insts=None, only=None):
     out = {}
 
     def timed(fn):
+        prewarm(fn)  # the clock ramp, as before every timed region (PREWARM_S)
         fn()
         torch.cuda.synchronize()
         e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)

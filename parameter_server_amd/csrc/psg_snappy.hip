@@ -930,7 +930,10 @@ __global__ __launch_bounds__(256) void snappy_tab_kernel(const uint8_t* __restri
                                                         int pairs) {
   __shared__ SnappyTabLds U;
   TabLds& T = U.tab;
-  const uint32_t tid = threadIdx.x, lane = tid & 63u, w = tid >> 6;
+  // the wave index as a wave-uniform (scalar) value: branches on it are not
+  // divergent, so the walk's state stays in SGPRs
+  const uint32_t tid = threadIdx.x, lane = tid & 63u,
+                 w = (uint32_t)__builtin_amdgcn_readfirstlane((int)(tid >> 6));
   for (uint64_t msg = blockIdx.x; msg < nmsg; msg += gridDim.x) {
     const AS1 uint8_t* const s0 =
         (const AS1 uint8_t*)(pairs ? (const uint8_t*)soff[2 * msg] : src + soff[msg]);
@@ -953,16 +956,29 @@ __global__ __launch_bounds__(256) void snappy_tab_kernel(const uint8_t* __restri
     if (w == 0) {
       int32_t st = 0;
       bool full = false;
-      uint32_t lp = 0xffffffffu - 64u, la = 0;
+      // a 256-byte window of the part in the wave's registers (lane l: the
+      // dword at wb + 4 l of the 4-B aligned stream, clamped to the dword
+      // holding the last byte: never past it, so never into another page),
+      // its bytes taken by readlane.  Every branch here is on wave-uniform
+      // values: r06's first form loaded the window under a per-lane bound
+      // test, which made every byte read a divergent branch with exec-mask
+      // saves (~1.4 K clocks per element)
+      const uint32_t mis4 = (uint32_t)((uintptr_t)s0 & 3u);
+      const AS1 uint32_t* const s4 = (const AS1 uint32_t*)(s0 - mis4);
+      const uint32_t lastw = (e - 1u + mis4) >> 2;  // dword holding the last byte
+      uint32_t wb = 0xffffffffu - 1024u, la = 0;     // window start (dword index)
       auto ub = [&](uint32_t q) -> uint32_t {
-        if (q - lp >= 64u) {
-          lp = q;
-          la = q + lane < e ? (uint32_t)s0[q + lane] : 0u;
+        const uint32_t a = __builtin_amdgcn_readfirstlane(q + mis4);
+        if ((a >> 2) - wb >= 64u) {
+          wb = a >> 2;
+          const uint32_t d = wb + lane;
+          la = s4[d < lastw ? d : lastw];
 #ifdef PSG_SNAPPY_PROF
           sp[3] += 1;
 #endif
         }
-        return (uint32_t)__builtin_amdgcn_readlane((int)la, (int)(q - lp));
+        const uint32_t k = a - 4u * wb;
+        return ((uint32_t)__builtin_amdgcn_readlane((int)la, (int)(k >> 2)) >> (8u * (k & 3u))) & 0xffu;
       };
       uint64_t ulen = 0;
       bool done = false;
@@ -976,49 +992,79 @@ __global__ __launch_bounds__(256) void snappy_tab_kernel(const uint8_t* __restri
       if (!done || ulen > 0xffffffffull) st = PSG_ERR_ARG;
       if (!st && ulen != cap) st = PSG_ERR_SIZE;
       const uint32_t ucap = (uint32_t)ulen;
+      // eight bytes at input position q in one 64-bit value (the tag and
+      // every length / offset byte of an element): three readlanes from the
+      // window instead of a window test and a readlane per byte; bytes past
+      // the part's end are garbage, and the header checks below never use
+      // them
+      auto u8x8 = [&](uint32_t q) -> uint64_t {
+        const uint32_t a = __builtin_amdgcn_readfirstlane(q + mis4);
+        const uint32_t d0 = a >> 2;
+        if (d0 - wb > 61u) {  // dwords d0 .. d0 + 2 in the window
+          wb = d0;
+          const uint32_t d = wb + lane;
+          la = s4[d < lastw ? d : lastw];
+#ifdef PSG_SNAPPY_PROF
+          sp[3] += 1;
+#endif
+        }
+        const uint32_t k = d0 - wb;
+        const uint64_t x01 = (uint64_t)(uint32_t)__builtin_amdgcn_readlane((int)la, (int)k) |
+                             (uint64_t)(uint32_t)__builtin_amdgcn_readlane((int)la, (int)k + 1) << 32;
+        const uint32_t sh = 8u * (a & 3u);
+        if (!sh) return x01;
+        const uint64_t x2 = (uint32_t)__builtin_amdgcn_readlane((int)la, (int)k + 2);
+        return (x01 >> sh) | (x2 << (64u - sh));
+      };
       uint32_t o = 0, n = 0, nd = 0;
       while (!st && p < e) {
         if (n == kTabMax) {
           full = true;
           break;
         }
-        const uint32_t tag = ub(p++);
-        uint32_t len, a, x;
-        if ((tag & 3u) == 0u) {  // literal
-          len = (tag >> 2) + 1u;
-          if (len > 60u) {
-            const uint32_t nb = len - 60u;
-            if (e - p < nb) { st = PSG_ERR_ARG; break; }
-            len = 0;
-            for (uint32_t b = 0; b < nb; ++b) len |= ub(p + b) << (8 * b);
-            p += nb;
-            if (len == 0xffffffffu) { st = PSG_ERR_ARG; break; }
-            len += 1u;
+        // the element's header: the same checks, in the same order, as the
+        // byte-by-byte parse of the streamed form (a corrupt part gets the
+        // same status)
+        const uint64_t hv = u8x8(p);
+        const uint32_t tag = (uint32_t)hv & 0xffu, t3 = tag & 3u;
+        const uint32_t rem = e - p;  // >= 1
+        uint32_t len, a, x, hdr;
+        if (t3 == 0u) {  // literal
+          const uint32_t l6 = tag >> 2;
+          if (l6 < 60u) {
+            hdr = 1u;
+            len = l6 + 1u;
+          } else {
+            const uint32_t nb = l6 - 59u;  // 1..4 length bytes
+            hdr = 1u + nb;
+            if (rem < hdr) { st = PSG_ERR_ARG; break; }
+            const uint32_t lv = (uint32_t)(hv >> 8) & (nb == 4u ? 0xffffffffu : (1u << (8u * nb)) - 1u);
+            if (lv == 0xffffffffu) { st = PSG_ERR_ARG; break; }
+            len = lv + 1u;
           }
-          if (e - p < len || ucap - o < len) { st = PSG_ERR_ARG; break; }
-          a = p;
+          if (rem - hdr < len || ucap - o < len) { st = PSG_ERR_ARG; break; }
+          a = p + hdr;
           x = lits && len >= kTabBigLit ? nd++ : 0xffffffffu;
-          p += len;
+          p = a + len;
           if (lane == 0) T.tl[n] = len;
         } else {
           uint32_t off;
-          if ((tag & 3u) == 1u) {
-            if (e - p < 1) { st = PSG_ERR_ARG; break; }
+          if (t3 == 1u) {
+            hdr = 2u;
             len = 4u + ((tag >> 2) & 7u);
-            off = (tag >> 5) << 8 | ub(p);
-            p += 1;
-          } else if ((tag & 3u) == 2u) {
-            if (e - p < 2) { st = PSG_ERR_ARG; break; }
+            off = (tag >> 5) << 8 | ((uint32_t)(hv >> 8) & 0xffu);
+          } else if (t3 == 2u) {
+            hdr = 3u;
             len = 1u + (tag >> 2);
-            off = ub(p) | ub(p + 1) << 8;
-            p += 2;
+            off = (uint32_t)(hv >> 8) & 0xffffu;
           } else {
-            if (e - p < 4) { st = PSG_ERR_ARG; break; }
+            hdr = 5u;
             len = 1u + (tag >> 2);
-            off = ub(p) | ub(p + 1) << 8 | ub(p + 2) << 16 | ub(p + 3) << 24;
-            p += 4;
+            off = (uint32_t)(hv >> 8);
           }
+          if (rem < hdr) { st = PSG_ERR_ARG; break; }
           if (off == 0 || off > o || ucap - o < len) { st = PSG_ERR_ARG; break; }
+          p += hdr;
           a = off;
           x = 0;
           if (lane == 0) T.tl[n] = len | kCopyBit;
