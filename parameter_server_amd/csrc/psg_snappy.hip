@@ -905,11 +905,13 @@ constexpr uint32_t kTabPend = 64;
 constexpr uint32_t kTabBigLit = 512;
 constexpr int kTabDepth = 4;
 constexpr uint32_t kCopyBit = 0x80000000u;
+typedef uint32_t u32x4_t __attribute__((ext_vector_type(4)));
 struct TabLds {
-  uint32_t to[kTabMax + 1];  // element i's output position (to[nel] = the part's length)
-  uint32_t ta[kTabMax];      // literal: input position; copy: offset
-  uint32_t tl[kTabMax];      // length, | kCopyBit for a copy
-  uint32_t tx[kTabMax];      // literal: deferred index (~0: moved in step 2); copy: 1 = unresolved
+  // element i: x = output position (rec[nel].x = the part's length), y =
+  // literal: input position / copy: offset, z = length (| kCopyBit for a
+  // copy), w = literal: deferred index (~0: moved in step 2) / copy: 1 =
+  // unresolved
+  u32x4_t rec[kTabMax + 1];
   uint32_t nel, verdict, base, npend;
 };
 union SnappyTabLds {
@@ -947,8 +949,8 @@ __global__ __launch_bounds__(256) void snappy_tab_kernel(const uint8_t* __restri
     const uint32_t e = (uint32_t)slen;
 #ifdef PSG_SNAPPY_PROF
     // [0] step 1 clocks, [1] step 2 (wave 0's share), [2] the part, [3] window
-    // loads, [4] unresolved copies, [5] step 3, [6] elements, [7] wave 1's
-    // prefetch
+    // loads, [4] unresolved copies, [5] step 3, [6] elements, [7] clocks in
+    // the window loads' round trips
     unsigned long long sp[8] = {0, 0, 0, 0, 0, 0, 0, 0};
     const unsigned long long sp_part = clock64();
 #endif
@@ -1003,9 +1005,14 @@ __global__ __launch_bounds__(256) void snappy_tab_kernel(const uint8_t* __restri
         if (d0 - wb > 61u) {  // dwords d0 .. d0 + 2 in the window
           wb = d0;
           const uint32_t d = wb + lane;
+#ifdef PSG_SNAPPY_PROF
+          const unsigned long long t_ld = clock64();
+#endif
           la = s4[d < lastw ? d : lastw];
 #ifdef PSG_SNAPPY_PROF
           sp[3] += 1;
+          (void)__builtin_amdgcn_readfirstlane((int)la);  // the load's latency, in sp[7]
+          sp[7] += clock64() - t_ld;
 #endif
         }
         const uint32_t k = d0 - wb;
@@ -1017,73 +1024,65 @@ __global__ __launch_bounds__(256) void snappy_tab_kernel(const uint8_t* __restri
         return (x01 >> sh) | (x2 << (64u - sh));
       };
       uint32_t o = 0, n = 0, nd = 0;
+      // one element per iteration, with no divergent code in the loop (the
+      // walk is issue-bound on its one wave: r06 measured ~1 K clocks per
+      // element while a lane-0 LDS store made the compiler keep the loop's
+      // state in VGPRs under exec masks): records collect in registers, lane
+      // k of rx..rw holding element n0 + k (a per-lane select), and go to LDS
+      // 64 at a time
+      uint32_t rx = 0, ry = 0, rz = 0, rw = 0;
+      auto flush_recs = [&](uint32_t n0, uint32_t cnt) {
+        if (lane < cnt) *(u32x4_t*)&T.rec[n0 + lane] = u32x4_t{rx, ry, rz, rw};
+      };
       while (!st && p < e) {
         if (n == kTabMax) {
           full = true;
           break;
         }
-        // the element's header: the same checks, in the same order, as the
-        // byte-by-byte parse of the streamed form (a corrupt part gets the
-        // same status)
         const uint64_t hv = u8x8(p);
-        const uint32_t tag = (uint32_t)hv & 0xffu, t3 = tag & 3u;
+        const uint32_t tag = (uint32_t)hv & 0xffu, t3 = tag & 3u, l6 = tag >> 2;
         const uint32_t rem = e - p;  // >= 1
-        uint32_t len, a, x, hdr;
-        if (t3 == 0u) {  // literal
-          const uint32_t l6 = tag >> 2;
-          if (l6 < 60u) {
-            hdr = 1u;
-            len = l6 + 1u;
-          } else {
-            const uint32_t nb = l6 - 59u;  // 1..4 length bytes
-            hdr = 1u + nb;
-            if (rem < hdr) { st = PSG_ERR_ARG; break; }
-            const uint32_t lv = (uint32_t)(hv >> 8) & (nb == 4u ? 0xffffffffu : (1u << (8u * nb)) - 1u);
-            if (lv == 0xffffffffu) { st = PSG_ERR_ARG; break; }
-            len = lv + 1u;
-          }
-          if (rem - hdr < len || ucap - o < len) { st = PSG_ERR_ARG; break; }
-          a = p + hdr;
-          x = lits && len >= kTabBigLit ? nd++ : 0xffffffffu;
-          p = a + len;
-          if (lane == 0) T.tl[n] = len;
-        } else {
-          uint32_t off;
-          if (t3 == 1u) {
-            hdr = 2u;
-            len = 4u + ((tag >> 2) & 7u);
-            off = (tag >> 5) << 8 | ((uint32_t)(hv >> 8) & 0xffu);
-          } else if (t3 == 2u) {
-            hdr = 3u;
-            len = 1u + (tag >> 2);
-            off = (uint32_t)(hv >> 8) & 0xffffu;
-          } else {
-            hdr = 5u;
-            len = 1u + (tag >> 2);
-            off = (uint32_t)(hv >> 8);
-          }
-          if (rem < hdr) { st = PSG_ERR_ARG; break; }
-          if (off == 0 || off > o || ucap - o < len) { st = PSG_ERR_ARG; break; }
-          p += hdr;
-          a = off;
-          x = 0;
-          if (lane == 0) T.tl[n] = len | kCopyBit;
+        const uint32_t b32 = (uint32_t)(hv >> 8);  // the bytes after the tag
+        const bool lit = t3 == 0u;
+        // literal: 0..4 length bytes after the tag; copies: 1, 2 or 4 offset bytes
+        const uint32_t nb = lit ? (l6 < 60u ? 0u : l6 - 59u) : (t3 == 3u ? 4u : t3);
+        const uint32_t hdr = 1u + nb;
+        const uint32_t bmask = nb >= 4u ? 0xffffffffu : (1u << (8u * nb)) - 1u;
+        const uint32_t field = b32 & bmask;
+        // literal length (a length field of 2^32 - 1 is corrupt), copy length and offset
+        const uint32_t len = lit ? (nb ? field + 1u : l6 + 1u)
+                                 : (t3 == 1u ? 4u + (l6 & 7u) : l6 + 1u);
+        const uint32_t off = t3 == 1u ? ((tag >> 5) << 8 | field) : field;
+        const bool bad = rem < hdr || (lit ? (nb && field == 0xffffffffu) || rem - hdr < len
+                                           : off == 0u || off > o) ||
+                         ucap - o < len;
+        if (bad) {
+          st = PSG_ERR_ARG;
+          break;
         }
-        if (lane == 0) {
-          T.to[n] = o;
-          T.ta[n] = a;
-          T.tx[n] = x;
-        }
+        const uint32_t a = lit ? p + hdr : off;
+        const bool dfr = lit && lits && len >= kTabBigLit;
+        const uint32_t x = dfr ? nd : lit ? 0xffffffffu : 0u;
+        nd += dfr ? 1u : 0u;
+        const uint32_t k = n & 63u;
+        const bool mine = lane == k;  // a select per lane, not a branch
+        rx = mine ? o : rx;
+        ry = mine ? a : ry;
+        rz = mine ? (lit ? len : len | kCopyBit) : rz;
+        rw = mine ? x : rw;
+        if (k == 63u) flush_recs(n - 63u, 64u);
+        p += lit ? hdr + len : hdr;
         o += len;
         ++n;
       }
+      if (n & 63u) flush_recs(n & ~63u, n & 63u);
       if (!st && !full && o != ucap) st = PSG_ERR_ARG;
 #ifdef PSG_SNAPPY_PROF
       sp[0] = clock64() - sp_part;
       sp[6] = n;
 #endif
       if (lane == 0) {
-        T.to[n] = o;
+        T.rec[n].x = o;
         T.nel = n;
         T.verdict = st ? 1u : full ? 2u : 0u;
         T.npend = 0;
@@ -1110,12 +1109,7 @@ __global__ __launch_bounds__(256) void snappy_tab_kernel(const uint8_t* __restri
         for (int k = 0; k < 8; ++k) acc ^= v[k];
       }
       asm volatile("" ::"v"(acc));
-#ifdef PSG_SNAPPY_PROF
-      if (w == 1) {
-        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-        sp[7] = clock64() - sp_part;
-      }
-#endif
+
     }
     __syncthreads();  // (1) the table
     const uint32_t verdict = T.verdict, nel = T.nel, base = T.base;
@@ -1131,7 +1125,7 @@ __global__ __launch_bounds__(256) void snappy_tab_kernel(const uint8_t* __restri
       uint32_t lo = 0, hi = nel;  // to[lo] <= x < to[hi]
       while (hi - lo > 1u) {
         const uint32_t mid = (lo + hi) >> 1;
-        if (T.to[mid] <= x) lo = mid;
+        if (T.rec[mid].x <= x) lo = mid;
         else hi = mid;
       }
       return lo;
@@ -1147,17 +1141,17 @@ __global__ __launch_bounds__(256) void snappy_tab_kernel(const uint8_t* __restri
     auto resolve = [&](uint32_t q, uint32_t& jc) -> uint32_t {
       for (int d = 0; d < kTabDepth; ++d) {
         uint32_t j = jc;
-        if (!(T.to[j] <= q && q < T.to[j + 1])) j = find(q);
+        if (!(T.rec[j].x <= q && q < T.rec[j + 1].x)) j = find(q);
         if (d == 0) jc = j;
-        const uint32_t lj = T.tl[j], dq = q - T.to[j], aj = T.ta[j];
+        const uint32_t lj = T.rec[j].z, dq = q - T.rec[j].x, aj = T.rec[j].y;
         if (!(lj & kCopyBit)) return aj + dq;
-        q = T.to[j] - aj + dq % aj;  // byte dq of copy j repeats this one
+        q = T.rec[j].x - aj + dq % aj;  // byte dq of copy j repeats this one
       }
       return 0xffffffffu;
     };
     constexpr uint32_t kLaneCopy = 8;  // copies this short: one lane each, below
     for (uint32_t i = w; i < nel; i += 4u) {
-      const uint32_t oo = T.to[i], a = T.ta[i], lk = T.tl[i], x = T.tx[i];
+      const uint32_t oo = T.rec[i].x, a = T.rec[i].y, lk = T.rec[i].z, x = T.rec[i].w;
       const uint32_t len = lk & ~kCopyBit;
       if (!(lk & kCopyBit)) {
         if (x != 0xffffffffu && base + x < lit_cap) {
@@ -1178,7 +1172,7 @@ __global__ __launch_bounds__(256) void snappy_tab_kernel(const uint8_t* __restri
       }
       if (__ballot(lane < len && from == 0xffffffffu)) {
         if (lane == 0) {
-          T.tx[i] = 1u;
+          T.rec[i].w = 1u;
           atomicAdd(&T.npend, 1u);
         }
       } else if (lane < len) {
@@ -1188,10 +1182,10 @@ __global__ __launch_bounds__(256) void snappy_tab_kernel(const uint8_t* __restri
     // short copies (incompressible data: spurious 4-byte matches), one lane
     // each: a wave resolves 64 of them at once instead of one
     for (uint32_t i = tid; i < nel; i += 256u) {
-      const uint32_t lk = T.tl[i];
+      const uint32_t lk = T.rec[i].z;
       const uint32_t len = lk & ~kCopyBit;
       if (!(lk & kCopyBit) || len > kLaneCopy) continue;
-      const uint32_t oo = T.to[i], a = T.ta[i];
+      const uint32_t oo = T.rec[i].x, a = T.rec[i].y;
       uint32_t src[kLaneCopy];
       uint32_t jc = 0;
       bool ok = true;
@@ -1200,7 +1194,7 @@ __global__ __launch_bounds__(256) void snappy_tab_kernel(const uint8_t* __restri
         ok = ok && src[l] != 0xffffffffu;
       }
       if (!ok) {
-        T.tx[i] = 1u;
+        T.rec[i].w = 1u;
         atomicAdd(&T.npend, 1u);
         continue;
       }
@@ -1229,16 +1223,16 @@ __global__ __launch_bounds__(256) void snappy_tab_kernel(const uint8_t* __restri
     if (w == 0) {
       for (uint32_t i0 = 0; npend && i0 < nel; i0 += 64u) {
         const uint32_t ii = i0 + lane;
-        unsigned long long m = __ballot(ii < nel && (T.tl[ii] & kCopyBit) && T.tx[ii] == 1u);
+        unsigned long long m = __ballot(ii < nel && (T.rec[ii].z & kCopyBit) && T.rec[ii].w == 1u);
         while (m) {
           const uint32_t i = i0 + (uint32_t)__builtin_ctzll(m);
           m &= m - 1;
-          const uint32_t oo = T.to[i], off = T.ta[i], len = T.tl[i] & ~kCopyBit;
+          const uint32_t oo = T.rec[i].x, off = T.rec[i].y, len = T.rec[i].z & ~kCopyBit;
           if (lane < len) {
             const uint32_t q = oo - off + (off >= 64u ? lane : lane % off);
             const uint32_t j = find(q);
-            const uint32_t b = (T.tl[j] & kCopyBit) ? (uint32_t)out[q]
-                                                     : (uint32_t)s0[T.ta[j] + (q - T.to[j])];
+            const uint32_t b = (T.rec[j].z & kCopyBit) ? (uint32_t)out[q]
+                                                     : (uint32_t)s0[T.rec[j].y + (q - T.rec[j].x)];
             out[oo + lane] = (uint8_t)b;
           }
           own_stores_visible();
@@ -1249,12 +1243,9 @@ __global__ __launch_bounds__(256) void snappy_tab_kernel(const uint8_t* __restri
       sp[5] = clock64() - sp_3;
       sp[2] = clock64() - sp_part;
       if (lane == 0 && msg < 4096)
-        for (int i = 0; i < 7; ++i) g_sprof[msg][i] = sp[i];
+        for (int i = 0; i < 8; ++i) g_sprof[msg][i] = sp[i];
 #endif
     }
-#ifdef PSG_SNAPPY_PROF
-    if (w == 1 && lane == 0 && msg < 4096) g_sprof[msg][7] = sp[7];
-#endif
     __syncthreads();  // (3) before the next part's table
   }
 }

@@ -62,7 +62,7 @@ def main():
                                    "tab": {"walk_clk": int(r[0]), "move_clk": int(r[1]),
                                            "total_clk": int(r[2]), "window_loads": int(r[3]),
                                            "unresolved": int(r[4]), "inorder_clk": int(r[5]),
-                                           "elements": int(r[6]), "prefetch_clk": int(r[7])}}
+                                           "elements": int(r[6]), "window_load_clk": int(r[7])}}
                                   for i, r in enumerate(prof)]}
     got = dd.cpu().numpy()
     assert all(np.array_equal(got[int(doff[i]):int(doff[i + 1])], raws[i]) for i in range(len(raws)))
