@@ -1044,26 +1044,32 @@ __global__ __launch_bounds__(256) void snappy_tab_kernel(const uint8_t* __restri
         const uint32_t rem = e - p;  // >= 1
         const uint32_t b32 = (uint32_t)(hv >> 8);  // the bytes after the tag
         const bool lit = t3 == 0u;
-        // literal: 0..4 length bytes after the tag; copies: 1, 2 or 4 offset bytes
-        const uint32_t nb = lit ? (l6 < 60u ? 0u : l6 - 59u) : (t3 == 3u ? 4u : t3);
-        const uint32_t hdr = 1u + nb;
-        const uint32_t bmask = nb >= 4u ? 0xffffffffu : (1u << (8u * nb)) - 1u;
-        const uint32_t field = b32 & bmask;
-        // literal length (a length field of 2^32 - 1 is corrupt), copy length and offset
-        const uint32_t len = lit ? (nb ? field + 1u : l6 + 1u)
-                                 : (t3 == 1u ? 4u + (l6 & 7u) : l6 + 1u);
-        const uint32_t off = t3 == 1u ? ((tag >> 5) << 8 | field) : field;
-        const bool bad = rem < hdr || (lit ? (nb && field == 0xffffffffu) || rem - hdr < len
-                                           : off == 0u || off > o) ||
-                         ucap - o < len;
+        uint32_t len, a, x, adv;
+        bool bad;
+        if (lit) {  // 0..4 length bytes after the tag
+          const uint32_t nb = __builtin_elementwise_max(l6, 59u) - 59u;
+          const uint32_t hdr = 1u + nb;
+          const uint32_t field = nb >= 4u ? b32 : b32 & ((1u << (8u * nb)) - 1u);
+          len = nb ? field + 1u : l6 + 1u;  // a length field of 2^32 - 1 is corrupt
+          bad = rem < hdr || (nb && field == 0xffffffffu) || rem - hdr < len || ucap - o < len;
+          a = p + hdr;
+          const bool dfr = lits && len >= kTabBigLit;
+          x = dfr ? nd : 0xffffffffu;
+          nd += dfr ? 1u : 0u;
+          adv = hdr + len;
+        } else {  // 1, 2 or 4 offset bytes
+          const uint32_t nb = t3 + (t3 >> 1 & t3);  // 1, 2, 4
+          len = t3 == 1u ? 4u + (l6 & 7u) : l6 + 1u;
+          const uint32_t field = nb >= 4u ? b32 : b32 & ((1u << (8u * nb)) - 1u);
+          a = t3 == 1u ? ((tag >> 5) << 8 | field) : field;  // the offset
+          bad = rem < 1u + nb || a == 0u || a > o || ucap - o < len;
+          x = 0u;
+          adv = 1u + nb;
+        }
         if (bad) {
           st = PSG_ERR_ARG;
           break;
         }
-        const uint32_t a = lit ? p + hdr : off;
-        const bool dfr = lit && lits && len >= kTabBigLit;
-        const uint32_t x = dfr ? nd : lit ? 0xffffffffu : 0u;
-        nd += dfr ? 1u : 0u;
         const uint32_t k = n & 63u;
         const bool mine = lane == k;  // a select per lane, not a branch
         rx = mine ? o : rx;
@@ -1071,7 +1077,7 @@ __global__ __launch_bounds__(256) void snappy_tab_kernel(const uint8_t* __restri
         rz = mine ? (lit ? len : len | kCopyBit) : rz;
         rw = mine ? x : rw;
         if (k == 63u) flush_recs(n - 63u, 64u);
-        p += lit ? hdr + len : hdr;
+        p += adv;
         o += len;
         ++n;
       }
