@@ -1011,7 +1011,7 @@ __global__ __launch_bounds__(256) void snappy_tab_kernel(const uint8_t* __restri
           la = s4[d < lastw ? d : lastw];
 #ifdef PSG_SNAPPY_PROF
           sp[3] += 1;
-          (void)__builtin_amdgcn_readfirstlane((int)la);  // the load's latency, in sp[7]
+          asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // the load's latency, in sp[7]
           sp[7] += clock64() - t_ld;
 #endif
         }
