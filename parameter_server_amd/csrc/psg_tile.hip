@@ -99,9 +99,6 @@ __device__ __forceinline__ uint64_t uni64(uint64_t v) {
   return ((uint64_t)uni((uint32_t)(v >> 32)) << 32) | uni((uint32_t)v);
 }
 
-#ifndef PSG_FOLDSPLIT
-#define PSG_FOLDSPLIT 0  // A/B builds: 1 = the 64-push form folds one-wave slots unordered
-#endif
 #ifndef PSG_FUSECNT
 #define PSG_FUSECNT 1  // A/B builds: 0 = sums and contributor counts in separate arrays
 #endif
@@ -201,11 +198,6 @@ __global__ __launch_bounds__(nt_of(kGroup), (occupancy<V, M, kGroup>())) void ti
   // updates both with one 8-B read and one 8-B write and the order check
   // issues no LDS atomic
   constexpr bool kFuse = PSG_FUSECNT && kGroup == 32 && M == 1 && sizeof(V) == 4;
-  // 64-push form (8 waves): slots that one wave alone holds in a pass fold
-  // at once, in parallel across waves; only slots several waves hold go
-  // through the wave-ordered fold (a per-slot mask of the waves holding it)
-  constexpr bool kSplit = PSG_FOLDSPLIT && kGroup == 64;
-  __shared__ uint32_t wm32[kSplit ? kTS / 4 : 1];
   __shared__ __attribute__((aligned(16))) V acc[kFuse ? 1 : M][kFuse ? 1 : kTS];
   // serial mode: pushes holding the slot (u16 pairs, counted by non-returning
   // LDS adds during the search, off the fold's dependency chain): the fold
@@ -378,10 +370,6 @@ __global__ __launch_bounds__(nt_of(kGroup), (occupancy<V, M, kGroup>())) void ti
     for (int i = 0; i < kBPT / 2; ++i) bt32[tid * (kBPT / 2) + i] = z;
   }
   if (tid == 0) pcarry = -1;
-  if constexpr (kSplit) {
-    static_assert(!kSplit || kTS / 4 == kNT, "one mask word per thread");
-    wm32[tid] = 0u;
-  }
   if (dma)
     lds_barrier();  // (1) tables, sums, counts (D and the bucket table still in flight)
   else
@@ -668,28 +656,6 @@ __global__ __launch_bounds__(nt_of(kGroup), (occupancy<V, M, kGroup>())) void ti
       }
     }
 
-    if constexpr (kSplit) {
-      // the waves holding each slot, then this wave's one-wave slots folded
-      // now (in round order: push order); the rest below, wave by wave
-#pragma unroll
-      for (int r = 0; r < kCap; ++r)
-        if ((uint32_t)r < nrw && ((okb >> r) & 1u))
-          __hip_atomic_fetch_or(&wm32[pos[r] >> 2], 1u << (8u * (pos[r] & 3u) + w),
-                                __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
-      __syncthreads();  // (5b)
-#pragma unroll
-      for (int r = 0; r < kCap; ++r) {
-        if ((uint32_t)r < nrw && ((okb >> r) & 1u)) {
-          const uint32_t s = pos[r];
-          if (((wm32[s >> 2] >> (8u * (s & 3u))) & 0xffu) == (1u << w)) {
-            const bool first = g0 + (re[r] >> kCB) == 0u && !cont;
-#pragma unroll
-            for (int mi = 0; mi < M; ++mi) acc[mi][s] = first ? ev[r][mi] : acc[mi][s] + ev[r][mi];
-            okb &= ~(1u << r);
-          }
-        }
-      }
-    }
     // ---- fold, wave by wave (rounds are push-major)
     const uint32_t inpass = (U - done) < kNW * Rw ? U - done : kNW * Rw;
     const uint32_t wl = (inpass - 1) / Rw;  // wave holding the pass's last round
@@ -723,7 +689,6 @@ __global__ __launch_bounds__(nt_of(kGroup), (occupancy<V, M, kGroup>())) void ti
       }
       __syncthreads();
     }
-    if constexpr (kSplit) wm32[threadIdx.x] = 0u;  // for the next pass (after its (5))
     PH(4);
 
     // ---- next pass, or next group of pushes
