@@ -448,8 +448,10 @@ def f64_block(args, insts, dist, dev, local, stream):
 def timed_stages(stages, K, W, stream, dist):
     """Like timed_steps for a step made of `stages` (callables enqueuing on
     `stream`): W warm-up steps, then K timed steps between barrier +
-    synchronize pairs.  Returns (wall s, [mean ms per stage]) (HIP events on
-    `stream` between the stages)."""
+    synchronize pairs.  Returns (wall s, [mean ms per stage]).  As in
+    timed_steps, the timed region holds two HIP events per step, around the
+    last stage (the aggregate kernel); every stage's time comes from a
+    second, untimed pass of K steps with an event between each."""
     import torch
 
     def step():
@@ -466,6 +468,18 @@ def timed_stages(stages, K, W, stream, dist):
     ev = [[torch.cuda.Event(enable_timing=True) for _ in range(len(stages) + 1)] for _ in range(K)]
     t0 = time.perf_counter()
     for s in range(K):
+        for f in stages[:-1]:
+            f()
+        ev[s][0].record(stream)
+        stages[-1]()
+        ev[s][1].record(stream)
+    torch.cuda.synchronize()
+    if dist:
+        dist.barrier()
+    torch.cuda.synchronize()
+    wall = time.perf_counter() - t0
+    last = float(np.mean([ev[s][0].elapsed_time(ev[s][1]) for s in range(K)]))
+    for s in range(K):  # untimed: every stage between events
         ev[s][0].record(stream)
         for i, f in enumerate(stages):
             f()
@@ -473,10 +487,8 @@ def timed_stages(stages, K, W, stream, dist):
     torch.cuda.synchronize()
     if dist:
         dist.barrier()
-    torch.cuda.synchronize()
-    wall = time.perf_counter() - t0
     ms = [float(np.mean([ev[s][i].elapsed_time(ev[s][i + 1]) for s in range(K)]))
-          for i in range(len(stages))]
+          for i in range(len(stages) - 1)] + [last]
     return wall, ms
 
 
@@ -503,16 +515,21 @@ def timed_rotating(plans, K, W, stream):
     torch.cuda.synchronize()
     ev = [[torch.cuda.Event(enable_timing=True) for _ in range(3)] for _ in range(K)]
     t0 = time.perf_counter()
-    for s in range(K):
-        ev[s][0].record(stream)
+    for s in range(K):  # two events per step, around the aggregate (timed_steps)
         plans[s % R].run_stage(0, sh)
         ev[s][1].record(stream)
         plans[s % R].run_stage(1, sh)
         ev[s][2].record(stream)
     torch.cuda.synchronize()
     wall = time.perf_counter() - t0
-    part = float(np.mean([ev[s][0].elapsed_time(ev[s][1]) for s in range(K)]))
     agg = float(np.mean([ev[s][1].elapsed_time(ev[s][2]) for s in range(K)]))
+    for s in range(K):  # untimed: the partition between events
+        ev[s][0].record(stream)
+        plans[s % R].run_stage(0, sh)
+        ev[s][1].record(stream)
+        plans[s % R].run_stage(1, sh)
+    torch.cuda.synchronize()
+    part = float(np.mean([ev[s][0].elapsed_time(ev[s][1]) for s in range(K)]))
     return wall, part, agg
 
 
