@@ -117,9 +117,11 @@ struct DenseCheck {
 // partition: splitters + fail reset of kStream jobs (one block of 256
 // splitters per split item; entry = job index), then the search / stream
 // items (u64: job << 37 | push << 24 | boundary group or chunk)
+// xcd: deal the items to the XCDs in contiguous runs (launches whose jobs are
+// all search mode)
 hipError_t launch_partition(const JobDev* d_jobs, const uint32_t* d_split_item_job,
                             uint32_t nsplit_items, const uint64_t* d_items,
-                            uint32_t nitems, hipStream_t stream);
+                            uint32_t nitems, hipStream_t stream, bool xcd = false);
 // aggregate: one workgroup per tile of kTileSlots slots.  psg_tile.hip:
 // every round holds one push (long pieces); psg_tile_packed.hip: rounds may
 // hold several pushes (many short pieces)

@@ -241,11 +241,23 @@ __device__ __forceinline__ void stream_item(const JobDev& J, uint32_t p, uint32_
   if (c == 0 && lane == 0) J.fail[p] = 0ull;
 }
 
+// blocks b and b+8 share an XCD (observed dispatch, speed only).  `xcd`: each
+// XCD takes a contiguous run of items, so neighbouring boundary groups of one
+// push, whose probes touch the same lines, share one L2 -- for launches of
+// search-mode jobs only (r06: cfg2 / cfg3 partition -2..-4 %; stream-mode
+// chunks read their keys once and lost 5 % that way,
+// profiles/r06_ab_partition_xcd.txt)
+__device__ __forceinline__ uint32_t xcd_block(uint32_t b, uint32_t n) {
+  const uint32_t x = b & 7u, j = b >> 3, q = n >> 3, r = n & 7u;
+  return x * q + (x < r ? x : r) + j;
+}
+
 __global__ __launch_bounds__(256) void partition_kernel(const JobDev* __restrict__ jobs,
                                                         const uint64_t* __restrict__ items,
-                                                        uint32_t nitems) {
+                                                        uint32_t nitems, int xcd) {
   __shared__ uint64_t ck[4][kStreamChunk];
-  const uint32_t item = uni((blockIdx.x * 256u + threadIdx.x) >> 6);
+  const uint32_t blk = xcd ? xcd_block(blockIdx.x, gridDim.x) : blockIdx.x;
+  const uint32_t item = uni((blk * 256u + threadIdx.x) >> 6);
   const int lane = threadIdx.x & 63;
   if (item >= nitems) return;
   const uint64_t it = uni64(items[item]);
@@ -263,13 +275,13 @@ __global__ __launch_bounds__(256) void partition_kernel(const JobDev* __restrict
 
 hipError_t launch_partition(const JobDev* d_jobs, const uint32_t* d_split_item_job,
                             uint32_t nsplit_items, const uint64_t* d_items, uint32_t nitems,
-                            hipStream_t stream) {
+                            hipStream_t stream, bool xcd) {
   if (nsplit_items)
     hipLaunchKernelGGL(splitter_kernel, dim3(nsplit_items), dim3(256), 0, stream, d_jobs,
                        d_split_item_job, nsplit_items);
   if (nitems)
     hipLaunchKernelGGL(partition_kernel, dim3((nitems + 3) / 4), dim3(256), 0, stream, d_jobs,
-                       d_items, nitems);
+                       d_items, nitems, xcd ? 1 : 0);
   return hipGetLastError();
 }
 

@@ -197,6 +197,7 @@ struct JobTable {
   // plans (D fixed for their lifetime): the stream jobs' splitters are
   // written once, at build, and a run launches only the partition proper
   bool split_once = false;
+  bool all_search = false;  // every job's partition searches (launch_partition xcd)
   void* blob = nullptr;
   size_t blob_bytes = 0;
   JobDev* d_jobs = nullptr;
@@ -673,6 +674,8 @@ struct JobTable {
       HIP_TRY(psg::launch_bucket_index(d_tiles, ntiles, tile,
                                        (uint32_t*)((char*)blob + index_off), strm));
     split_once = index && nsplit > 0 && !dense && !cursor && !pcursor;
+    all_search = true;
+    for (const JobDev& d : h) all_search = all_search && d.mode == psg::kSearch;
     if (split_once)  // the splitter pass alone (it also clears the fail counters once)
       HIP_TRY(psg::launch_partition(d_jobs, d_split_items, nsplit, nullptr, 0, strm));
     if (!async) HIP_TRY(hipStreamSynchronize(strm));
@@ -686,7 +689,7 @@ struct JobTable {
         HIP_TRY(hipMemsetAsync(d_zero, 0, zero_bytes, s));
       else if (!dense)
         HIP_TRY(psg::launch_partition(d_jobs, d_split_items, split_once ? 0u : nsplit, d_items,
-                                      nitems, s));
+                                      nitems, s, all_search));
     } else if (cursor)
       HIP_TRY(psg::launch_aggregate_cursor(dtype, m, (int)ckr, d_cjobs, d_chunks, nchunks, d_bx, s));
     else if (dense)
